@@ -1,0 +1,139 @@
+#!/usr/bin/env python
+"""Headline benchmark: rows/s of GBDT training on 10M-row LendingClub-shaped data (+ AUC).
+
+Metric and config come from BASELINE.json: "rows/sec GBDT train on 10M-row LendingClub-shaped
+tabular; AUC parity", with the deployed hyper-parameters of the reference model (300 trees, depth 7,
+eta 0.05, gamma 5, lambda 1, min_child_weight 1, max_bin 256, scale_pos_weight = neg/pos,
+binary:logistic, 20 features). One step = one complete fit (quantile sketch + binning + 300
+boosting rounds + model fetch), i.e. BASELINE.md's ``rows_per_s = N_train_rows / wall_seconds(fit)``.
+
+Data: synthetic LendingClub-shaped rows (no dataset download is possible) generated on each GPU for
+its own shard by global row index, so the global dataset is identical for any GPU count. Scaling
+mode "strong" (default) keeps the 10M global rows fixed and shards them over the ranks; "weak"
+gives every rank 10M rows.
+
+Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_ROWS_PER_S = None  # the reference publishes no throughput (BASELINE.json "published": {})
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=10_000_000, help="training rows (global for strong scaling)")
+    ap.add_argument("--test-rows", type=int, default=1_000_000)
+    ap.add_argument("--trees", type=int, default=300)
+    ap.add_argument("--depth", type=int, default=7)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--profile-fit", action="store_true", help="print per-phase timings to stderr")
+    a = ap.parse_args()
+
+    from cobalt_smart_lender_ai_amd.dataio import synth
+    from cobalt_smart_lender_ai_amd.metrics.auc import roc_auc
+    from cobalt_smart_lender_ai_amd.models import gbdt
+    from cobalt_smart_lender_ai_amd.parallel import dist as pdist
+
+    ctx = pdist.init_from_env()
+    world, rank = ctx.world, ctx.rank
+    if world != a.gpus:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", ctx.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+
+    n_global = a.rows if a.scaling == "strong" else a.rows * world
+    start, end = pdist.shard_range(n_global, rank, world)
+    X, y = synth.make_lendingclub(end - start, seed=a.seed, row_offset=start, device=dev)
+    pos = ctx.allreduce_scalar(float(y.sum()), "sum", dev)
+    spw = (n_global - pos) / pos
+    params = gbdt.GBDTParams(n_estimators=a.trees, max_depth=a.depth, learning_rate=0.05, gamma=5.0,
+                             reg_lambda=1.0, min_child_weight=1.0, max_bin=256, scale_pos_weight=spw,
+                             random_state=78)
+
+    def fit():
+        rep = gbdt.FitReport()
+        b = gbdt.train(X, y, params, device=dev, dist=ctx if world > 1 else None, n_rows_global=n_global,
+                       row_offset=start, report=rep, feature_names=synth.FEATURES,
+                       feature_types=synth.FEATURE_TYPES)
+        return b, rep
+
+    for _ in range(a.warmup):
+        fit()
+    ctx.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    reps = []
+    booster = None
+    for _ in range(a.steps):
+        booster, rep = fit()
+        reps.append(rep)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = ctx.allreduce_scalar(elapsed, "max", dev)
+
+    auc = None
+    if rank == 0 and booster is not None:
+        Xt, yt = synth.make_lendingclub(a.test_rows, seed=a.seed, row_offset=n_global, device=dev)
+        p = booster.predict_proba(Xt, device=dev)
+        auc = float(roc_auc(yt, p))
+    ms = elapsed / max(a.steps, 1) * 1e3
+    value = n_global * a.steps / elapsed
+    if a.profile_fit and rank == 0:
+        for r in reps:
+            print(f"[bench] sketch {r.t_sketch*1e3:.1f} ms  bin {r.t_bin*1e3:.1f} ms  boost {r.t_boost*1e3:.1f} ms"
+                  f"  total {r.t_total*1e3:.1f} ms", file=sys.stderr)
+    if rank == 0:
+        out = {
+            "metric": "rows/sec GBDT train on 10M-row LendingClub-shaped tabular; AUC parity",
+            "value": round(value, 1),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": None if BASELINE_ROWS_PER_S is None else value / BASELINE_ROWS_PER_S,
+            "dtype": "fp32",
+            "precision": "fp32 features, fp64 gradients, exact int64 fixed-point histogram sums",
+            "data": "synthetic LendingClub-shaped (20 deployed features, 12.9% positives), generated on device",
+            "config": {
+                "model": "GBDT binary:logistic, 300 trees depth 7 eta 0.05 gamma 5 lambda 1 max_bin 256 spw=neg/pos",
+                "global_batch": n_global,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "n_features": len(synth.FEATURES),
+                "trees": a.trees,
+                "max_depth": a.depth,
+            },
+            "auc": None if auc is None else round(auc, 5),
+            "test_rows": a.test_rows,
+            "fit_breakdown_ms": {
+                "sketch": round(sum(r.t_sketch for r in reps) / len(reps) * 1e3, 3),
+                "bin": round(sum(r.t_bin for r in reps) / len(reps) * 1e3, 3),
+                "boost": round(sum(r.t_boost for r in reps) / len(reps) * 1e3, 3),
+            } if reps else None,
+        }
+        print(json.dumps(out), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+// Tree-ensemble inference (K21) and path-dependent TreeSHAP (K22) for gfx950.
+//
+// Replaces XGBoost's predictor (`predict_proba`, reference src/api/cobalt_fast_api.py:90-91,
+// src/model_train_test/model_tree_train_test.py:171-172) and SHAP's C TreeSHAP extension
+// (`shap.TreeExplainer(...).shap_values`, src/api/cobalt_fast_api.py:46,100).
+//
+// Forest layout (built on the host at model load, ops/predict_ops.py): every tree is renumbered in
+// BFS order so the right child is always left+1; a node is 8 bytes
+//   uint32 meta = left_child(16 bits, 0xFFFF = leaf) | feature(15 bits) << 16 | default_left << 31
+//   float  val  = split threshold (x < val goes left) or leaf value
+// Trees are grouped into tiles of <= kTileNodes nodes that are staged in LDS; each thread walks
+// one row (features staged in LDS with an odd stride, conflict-free) through every tree of the
+// tile, accumulating the margin in fp32 in tree order (XGBoost CPU predictor semantics).
+//
+// TreeSHAP follows the path formulation (every root->leaf path with repeated features merged into
+// one element: feature, [lo, hi) interval, NaN-follows flag, product of cover ratios): one thread
+// per (row, path) runs EXTEND over the path and the UNWOUND sum per element in fp64, contributions
+// are reduced per block in LDS and flushed with one fp64 atomic per (row, feature).
+#include "common.h"
+#include <algorithm>
+
+using namespace cobalt;
+
+namespace {
+constexpr int kTileNodes = 6144;   // 48 KiB of nodes per LDS tile
+constexpr int kMaxPath = 16;       // max unique elements per path (incl. bias) in the SHAP kernel
+}
+
+// ------------------------------------------------------------------------------------ predictor
+__global__ __launch_bounds__(256) void k_predict(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
+                                                 const uint2* __restrict__ nodes, const int32_t* __restrict__ tree_ptr,
+                                                 const int32_t* __restrict__ tile_ptr, int n_tiles, float base_margin,
+                                                 float* __restrict__ out_margin, float* __restrict__ out_prob) {
+  extern __shared__ unsigned char smem[];
+  uint2* s_nodes = reinterpret_cast<uint2*>(smem);
+  float* s_x = reinterpret_cast<float*>(smem + kTileNodes * sizeof(uint2));
+  const int xs = F | 1;  // odd stride -> conflict-free LDS reads
+  const int64_t row0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t row = row0 + threadIdx.x;
+  const int nrows = (int)min((int64_t)blockDim.x, n - row0);
+  // stage the block's rows (coalesced over the contiguous [nrows][F] slab when ldx == F)
+  for (int e = threadIdx.x; e < nrows * F; e += blockDim.x) {
+    const int r = e / F, f = e - r * F;
+    s_x[r * xs + f] = X[(row0 + r) * ldx + f];
+  }
+  float acc = base_margin;
+  const float* x = s_x + threadIdx.x * xs;
+  for (int tile = 0; tile < n_tiles; ++tile) {
+    const int t_begin = tile_ptr[tile], t_end = tile_ptr[tile + 1];
+    const int nbase = tree_ptr[t_begin];
+    const int nn = tree_ptr[t_end] - nbase;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nn; i += blockDim.x) s_nodes[i] = nodes[nbase + i];
+    __syncthreads();
+    if (row < n) {
+      for (int t = t_begin; t < t_end; ++t) {
+        const uint2* tn = s_nodes + (tree_ptr[t] - nbase);
+        uint32_t id = 0;
+        uint2 nd = tn[0];
+        while ((nd.x & 0xFFFFu) != 0xFFFFu) {
+          const int f = (nd.x >> 16) & 0x7FFF;
+          const float v = x[f];
+          const float thr = __uint_as_float(nd.y);
+          const bool left = (v != v) ? ((nd.x >> 31) != 0) : (v < thr);
+          id = (nd.x & 0xFFFFu) + (left ? 0u : 1u);
+          nd = tn[id];
+        }
+        acc += __uint_as_float(nd.y);
+      }
+    }
+  }
+  if (row < n) {
+    if (out_margin) out_margin[row] = acc;
+    if (out_prob) out_prob[row] = 1.0f / (1.0f + expf(-acc));
+  }
+}
+
+COBALT_API int cobalt_predict(const float* X, int64_t n, int F, int64_t ldx, const void* nodes, const int32_t* tree_ptr,
+                              const int32_t* tile_ptr, int n_tiles, float base_margin, float* out_margin,
+                              float* out_prob, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const int block = 256;
+  const size_t lds = kTileNodes * sizeof(uint2) + (size_t)block * (F | 1) * sizeof(float);
+  if (lds > 160 * 1024) return -3;
+  static bool attr_set = false;
+  if (!attr_set) {
+    CK(hipFuncSetAttribute((const void*)k_predict, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int grid = ceil_div(n, block);
+  hipLaunchKernelGGL(k_predict, dim3(grid), dim3(block), lds, stream, X, n, F, ldx,
+                     static_cast<const uint2*>(nodes), tree_ptr, tile_ptr, n_tiles, base_margin, out_margin, out_prob);
+  CK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------ TreeSHAP
+struct PathElem {
+  float lo, hi;        // row follows the path on this feature iff lo <= x < hi (non-missing)
+  int32_t feat;        // feature index
+  int32_t nan_ok;      // row with NaN follows the path on this feature
+  double zero;         // product of cover(child)/cover(parent) over the merged occurrences
+};
+static_assert(sizeof(PathElem) == 24, "PathElem");
+
+__global__ __launch_bounds__(256) void k_treeshap(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
+                                                  const PathElem* __restrict__ elems,
+                                                  const int32_t* __restrict__ path_ptr,
+                                                  const double* __restrict__ path_val, int n_paths,
+                                                  double* __restrict__ phi) {
+  extern __shared__ double s_phi[];  // [F]
+  const int64_t row = blockIdx.y;
+  for (int f = threadIdx.x; f < F; f += blockDim.x) s_phi[f] = 0.0;
+  __syncthreads();
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_paths) {
+    const int e0 = path_ptr[p], k = path_ptr[p + 1] - e0;  // k unique features (bias excluded)
+    const float* x = X + row * ldx;
+    double z[kMaxPath], o[kMaxPath], w[kMaxPath];
+    int feat[kMaxPath];
+    // bias element
+    z[0] = 1.0; o[0] = 1.0; w[0] = 1.0; feat[0] = -1;
+#pragma unroll
+    for (int i = 1; i < kMaxPath; ++i) { z[i] = 0.0; o[i] = 0.0; w[i] = 0.0; feat[i] = -1; }
+    // EXTEND each element
+#pragma unroll
+    for (int l = 1; l < kMaxPath; ++l) {
+      if (l <= k) {
+        const PathElem e = elems[e0 + l - 1];
+        const float v = x[e.feat];
+        const double one = (v != v) ? (e.nan_ok ? 1.0 : 0.0) : ((v >= e.lo && v < e.hi) ? 1.0 : 0.0);
+        z[l] = e.zero; o[l] = one; feat[l] = e.feat;
+        w[l] = 0.0;
+#pragma unroll
+        for (int j = kMaxPath - 2; j >= 0; --j) {
+          if (j <= l - 1) {
+            w[j + 1] += one * w[j] * (double)(j + 1) / (double)(l + 1);
+            w[j] = e.zero * w[j] * (double)(l - j) / (double)(l + 1);
+          }
+        }
+      }
+    }
+    const double leaf = path_val[p];
+    // UNWOUND sum per element
+#pragma unroll
+    for (int i = 1; i < kMaxPath; ++i) {
+      if (i <= k) {
+        const double one = o[i], zero = z[i];
+        double total = 0.0;
+        if (one != 0.0) {
+          double next = w[k];
+#pragma unroll
+          for (int j = kMaxPath - 2; j >= 0; --j) {
+            if (j <= k - 1) {
+              const double tmp = next / ((double)(j + 1) * one);
+              total += tmp;
+              next = w[j] - tmp * zero * (double)(k - j);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = kMaxPath - 2; j >= 0; --j) {
+            if (j <= k - 1) total += w[j] / (zero * (double)(k - j));
+          }
+        }
+        total *= (double)(k + 1);
+        atomicAdd(&s_phi[feat[i]], total * (one - zero) * leaf);
+      }
+    }
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < F; f += blockDim.x) {
+    const double v = s_phi[f];
+    if (v != 0.0) atomicAdd(&phi[row * F + f], v);
+  }
+}
+
+COBALT_API int cobalt_treeshap(const float* X, int64_t n, int F, int64_t ldx, const void* elems, const int32_t* path_ptr,
+                               const double* path_val, int n_paths, int max_len, double* phi, hipStream_t stream) {
+  if (n <= 0 || n_paths <= 0) return 0;
+  if (max_len + 1 > kMaxPath) return -3;
+  if (n > 65535) return -4;  // grid.y limit; the caller batches rows
+  const int block = 256;
+  dim3 grid(ceil_div(n_paths, block), (unsigned)n);
+  hipLaunchKernelGGL(k_treeshap, grid, dim3(block), F * sizeof(double), stream, X, n, F, ldx,
+                     static_cast<const PathElem*>(elems), path_ptr, path_val, n_paths, phi);
+  CK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,403 @@
+"""Gradient-boosted decision trees for binary credit-default classification.
+
+Public API:
+
+* :func:`train` — fit a :class:`~.booster.Booster` on a feature matrix (GPU: hand-written gfx950
+  kernels, optionally data-parallel across ranks; CPU: the NumPy reference trainer).
+* :class:`GBDTClassifier` — an sklearn-compatible estimator with the constructor arguments and
+  attributes of ``xgboost.XGBClassifier`` used by the reference (``n_estimators``, ``max_depth``,
+  ``learning_rate``, ``gamma``, ``subsample``, ``colsample_bytree``, ``scale_pos_weight``,
+  ``random_state``, ``eval_metric``, ``feature_importances_``, ``get_booster()``, ``predict_proba``),
+  so it drops into sklearn's RFE / RandomizedSearchCV exactly where the reference used XGBClassifier
+  (src/model_train_test/model_tree_train_test.py:111-164).
+
+A fit = quantile sketch (K12) + binning (K13) + ``n_estimators`` boosting rounds of depthwise
+histogram trees (K14-K20). See ``csrc/gbdt.hip`` for the device design.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Any, Sequence
+
+import numpy as np
+import torch
+
+from . import gbdt_host, sketch
+from .booster import Booster, dump_pickle_bytes, sigmoid32, trees_from_heap_nodes
+
+XGB_DEFAULTS = dict(n_estimators=100, max_depth=6, learning_rate=0.3, gamma=0.0, min_child_weight=1.0,
+                    reg_lambda=1.0, reg_alpha=0.0, subsample=1.0, colsample_bytree=1.0, max_bin=256,
+                    scale_pos_weight=1.0, random_state=0, base_score=None)
+
+
+@dataclass
+class GBDTParams:
+    n_estimators: int = 100
+    max_depth: int = 6
+    learning_rate: float = 0.3
+    gamma: float = 0.0
+    min_child_weight: float = 1.0
+    reg_lambda: float = 1.0
+    reg_alpha: float = 0.0
+    subsample: float = 1.0
+    colsample_bytree: float = 1.0
+    max_bin: int = 256
+    scale_pos_weight: float = 1.0
+    random_state: int = 0
+    base_score: float | None = None
+    sketch_rows: int = 1 << 18
+
+    @classmethod
+    def from_kwargs(cls, **kw) -> "GBDTParams":
+        names = {f for f in cls.__dataclass_fields__}
+        alias = {"eta": "learning_rate", "lambda": "reg_lambda", "alpha": "reg_alpha", "min_split_loss": "gamma",
+                 "seed": "random_state"}
+        out = {}
+        for k, v in kw.items():
+            k = alias.get(k, k)
+            if k in names and v is not None:
+                out[k] = v
+        return cls(**out)
+
+
+@dataclass
+class FitReport:
+    """Timings and sizes of one fit (for logs / bench)."""
+    n_rows: int = 0
+    n_rows_global: int = 0
+    n_features: int = 0
+    n_trees: int = 0
+    device: str = "cpu"
+    world: int = 1
+    t_sketch: float = 0.0
+    t_bin: float = 0.0
+    t_boost: float = 0.0
+    t_total: float = 0.0
+    extra: dict[str, Any] = field(default_factory=dict)
+
+
+def _to_tensor(X, device, dtype=torch.float32) -> torch.Tensor:
+    if isinstance(X, torch.Tensor):
+        return X.to(device=device, dtype=dtype).contiguous()
+    if hasattr(X, "to_numpy"):
+        X = X.to_numpy(dtype=np.float32, na_value=np.nan) if hasattr(X, "columns") else X.to_numpy()
+    return torch.as_tensor(np.ascontiguousarray(np.asarray(X, dtype=np.float32)), device=device).to(dtype).contiguous()
+
+
+def _resolve_device(device: str | torch.device | None, X) -> torch.device:
+    if device is None:
+        if isinstance(X, torch.Tensor):
+            return X.device
+        return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+def feature_masks(n_trees: int, n_feat: int, colsample: float, seed: int) -> np.ndarray:
+    """Per-tree column masks for ``colsample_bytree`` (all ones when 1.0)."""
+    m = np.ones((n_trees, n_feat), dtype=np.uint8)
+    if colsample >= 1.0:
+        return m
+    k = max(1, int(math.floor(colsample * n_feat)))
+    rng = np.random.default_rng(seed + 0x5EED)
+    for t in range(n_trees):
+        m[t] = 0
+        m[t, rng.choice(n_feat, size=k, replace=False)] = 1
+    return m
+
+
+def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, device=None,
+          feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
+          dist=None, n_rows_global: int | None = None, row_offset: int = 0,
+          report: FitReport | None = None) -> Booster:
+    """Fit a binary:logistic GBDT. With ``dist`` (a :class:`~..parallel.dist.DistContext`) each rank
+    passes its local row shard (``row_offset`` = global index of its first row)."""
+    if params is None:
+        params = GBDTParams()
+    elif isinstance(params, dict):
+        params = GBDTParams.from_kwargs(**params)
+    dev = _resolve_device(device, X)
+    world = dist.world if dist is not None else 1
+    t0 = time.perf_counter()
+    Xt = _to_tensor(X, dev)
+    yt = _to_tensor(y, dev).reshape(-1)
+    N, F = Xt.shape
+    if yt.shape[0] != N:
+        raise ValueError("X and y row counts differ")
+    n_glob = n_rows_global if n_rows_global is not None else (
+        int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
+    wt = _to_tensor(sample_weight, dev).reshape(-1) if sample_weight is not None else torch.ones(N, device=dev)
+    spw = float(params.scale_pos_weight if params.scale_pos_weight is not None else 1.0)
+    wt = wt * torch.where(yt == 1.0, torch.tensor(spw, device=dev), torch.tensor(1.0, device=dev))
+    wt = wt.to(torch.float32).contiguous()
+
+    # base score = weighted label mean (XGBoost boost_from_average for binary:logistic)
+    if params.base_score is None:
+        sw = float(wt.double().sum())
+        swy = float((wt.double() * yt.double()).sum())
+        if world > 1:
+            sw = dist.allreduce_scalar(sw, "sum", dev)
+            swy = dist.allreduce_scalar(swy, "sum", dev)
+        base_score = min(max(swy / sw if sw > 0 else 0.5, 1e-6), 1 - 1e-6)
+    else:
+        base_score = float(params.base_score)
+    base_score = float(np.float32(base_score))
+    booster_shell = Booster([], base_score=base_score, num_feature=F)
+    base_margin = booster_shell.base_margin
+
+    wmax = float(wt.max()) if N else 1.0
+    if world > 1:
+        wmax = dist.allreduce_scalar(wmax, "max", dev)
+    gscale, hscale = gbdt_host.quant_scales(wmax)
+
+    # ---- K12 quantile sketch on a global strided sample
+    ts = time.perf_counter()
+    stride = sketch.sample_stride(n_glob, params.sketch_rows)
+    samp = sketch.local_sample(Xt, row_offset, stride)
+    if world > 1:
+        samp = dist.allgather_rows(samp)
+    cuts, nbins = sketch.compute_cuts(samp, params.max_bin)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t_sketch = time.perf_counter() - ts
+
+    T = int(params.n_estimators)
+    fmask_np = feature_masks(T, F, float(params.colsample_bytree), int(params.random_state))
+    hp = gbdt_host.HostGbdtParams(max_depth=int(params.max_depth), eta=float(params.learning_rate),
+                                  reg_lambda=float(params.reg_lambda), reg_alpha=float(params.reg_alpha),
+                                  gamma=float(params.gamma), min_child_weight=float(params.min_child_weight),
+                                  subsample=float(params.subsample), seed=int(params.random_state),
+                                  gscale=gscale, hscale=hscale)
+    if dev.type == "cuda":
+        from ..ops import gbdt_ops
+
+        tb = time.perf_counter()
+        bins, binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
+        torch.cuda.synchronize(dev)
+        t_bin = time.perf_counter() - tb
+        tb = time.perf_counter()
+        margin = torch.full((N,), base_margin, dtype=torch.float32, device=dev)
+        comm = dist.native_comm if (dist is not None and world > 1) else None
+        if world > 1 and comm is None:
+            raise RuntimeError("data-parallel GPU training needs the native RCCL communicator")
+        tr = gbdt_ops.GpuGbdtTrainer(n_rows=N, n_feat=F, max_depth=hp.max_depth, max_trees=T, eta=hp.eta,
+                                     reg_lambda=hp.reg_lambda, reg_alpha=hp.reg_alpha, gamma=hp.gamma,
+                                     min_child_weight=hp.min_child_weight, subsample=hp.subsample,
+                                     gscale=gscale, hscale=hscale, base_margin=base_margin,
+                                     seed=hp.seed, row_offset=row_offset, world_size=world, comm=comm)
+        fm = torch.as_tensor(fmask_np, device=dev).contiguous()
+        tr.set_data(bins, binsT, cuts.contiguous(), nbins.to(torch.int32).contiguous(), yt.contiguous(), wt,
+                    margin, fm)
+        tr.grow(0, T)
+        nodes = tr.fetch(0, T)
+        tr.close()
+        t_boost = time.perf_counter() - tb
+    else:
+        tb = time.perf_counter()
+        cuts_np = cuts.cpu().numpy()
+        nb_np = nbins.cpu().numpy()
+        bins_np = sketch.bin_matrix_host(Xt.cpu().numpy(), cuts_np, nb_np)
+        t_bin = time.perf_counter() - tb
+        tb = time.perf_counter()
+        margin_np = np.full(N, np.float32(base_margin), dtype=np.float32)
+        y_np = yt.cpu().numpy()
+        w_np = wt.cpu().numpy()
+        allreduce = None
+        if world > 1:
+            def allreduce(a: np.ndarray) -> np.ndarray:
+                t = torch.from_numpy(np.ascontiguousarray(a))
+                dist.allreduce(t, "sum")
+                return t.numpy()
+        recs = []
+        for t in range(T):
+            gq, hq = gbdt_host.gradients_host(margin_np, y_np, w_np, hp, t, row_offset)
+            recs.append(gbdt_host.grow_tree_host(bins_np, cuts_np, nb_np, gq, hq, margin_np, hp, fmask_np[t],
+                                                 allreduce))
+        nodes = np.stack(recs) if recs else np.zeros((0, (1 << (hp.max_depth + 1)) - 1),
+                                                      dtype=gbdt_host.NODE_DTYPE)
+        t_boost = time.perf_counter() - tb
+    trees = trees_from_heap_nodes(nodes, hp.max_depth)
+    names = list(feature_names) if feature_names is not None else None
+    ftypes = list(feature_types) if feature_types is not None else None
+    bst = Booster(trees=trees, feature_names=names, feature_types=ftypes, base_score=base_score, num_feature=F,
+                  train_params=dict(eta=hp.eta, gamma=hp.gamma, max_depth=hp.max_depth,
+                                    min_child_weight=hp.min_child_weight, reg_lambda=hp.reg_lambda,
+                                    reg_alpha=hp.reg_alpha, subsample=hp.subsample,
+                                    colsample_bytree=float(params.colsample_bytree), max_bin=int(params.max_bin),
+                                    scale_pos_weight=spw, seed=hp.seed))
+    if report is not None:
+        report.n_rows, report.n_rows_global, report.n_features, report.n_trees = N, n_glob, F, T
+        report.device, report.world = str(dev), world
+        report.t_sketch, report.t_bin, report.t_boost = t_sketch, t_bin, t_boost
+        report.t_total = time.perf_counter() - t0
+        report.extra["cuts"] = cuts
+        report.extra["nbins"] = nbins
+    return bst
+
+
+def _feature_info(X) -> tuple[list[str] | None, list[str] | None]:
+    if hasattr(X, "columns"):
+        names = [str(c) for c in X.columns]
+        types = []
+        for c in X.columns:
+            dt = X[c].dtype
+            if dt == bool or str(dt) == "bool":
+                types.append("i")
+            elif np.issubdtype(dt, np.integer):
+                types.append("int")
+            else:
+                types.append("float")
+        return names, types
+    return None, None
+
+
+class GBDTClassifier:
+    """sklearn-compatible drop-in for ``xgboost.XGBClassifier`` backed by this framework's trainer."""
+
+    _param_names = ["n_estimators", "max_depth", "learning_rate", "gamma", "min_child_weight", "reg_lambda",
+                    "reg_alpha", "subsample", "colsample_bytree", "max_bin", "scale_pos_weight", "random_state",
+                    "base_score", "eval_metric", "use_label_encoder", "device", "importance_type", "n_jobs",
+                    "sketch_rows"]
+
+    def __init__(self, n_estimators=None, max_depth=None, learning_rate=None, gamma=None, min_child_weight=None,
+                 reg_lambda=None, reg_alpha=None, subsample=None, colsample_bytree=None, max_bin=None,
+                 scale_pos_weight=None, random_state=None, base_score=None, eval_metric=None,
+                 use_label_encoder=None, device=None, importance_type=None, n_jobs=None, sketch_rows=None):
+        self.n_estimators = n_estimators
+        self.max_depth = max_depth
+        self.learning_rate = learning_rate
+        self.gamma = gamma
+        self.min_child_weight = min_child_weight
+        self.reg_lambda = reg_lambda
+        self.reg_alpha = reg_alpha
+        self.subsample = subsample
+        self.colsample_bytree = colsample_bytree
+        self.max_bin = max_bin
+        self.scale_pos_weight = scale_pos_weight
+        self.random_state = random_state
+        self.base_score = base_score
+        self.eval_metric = eval_metric
+        self.use_label_encoder = use_label_encoder
+        self.device = device
+        self.importance_type = importance_type
+        self.n_jobs = n_jobs
+        self.sketch_rows = sketch_rows
+
+    # sklearn protocol
+    def get_params(self, deep: bool = True) -> dict[str, Any]:
+        return {k: getattr(self, k) for k in self._param_names}
+
+    def set_params(self, **params) -> "GBDTClassifier":
+        for k, v in params.items():
+            if k not in self._param_names:
+                raise ValueError(f"invalid parameter {k!r}")
+            setattr(self, k, v)
+        return self
+
+    def __sklearn_tags__(self):
+        from sklearn.utils import Tags, ClassifierTags, TargetTags, InputTags
+        return Tags(estimator_type="classifier", target_tags=TargetTags(required=True),
+                    classifier_tags=ClassifierTags(), input_tags=InputTags(allow_nan=True))
+
+    _estimator_type = "classifier"
+
+    def _train_params(self) -> GBDTParams:
+        kw = {k: v for k, v in self.get_params().items() if v is not None}
+        return GBDTParams.from_kwargs(**{k: v for k, v in {**XGB_DEFAULTS, **kw}.items()})
+
+    def fit(self, X, y, sample_weight=None, **_):
+        names, types = _feature_info(X)
+        y_np = np.asarray(y.to_numpy() if hasattr(y, "to_numpy") else y).reshape(-1)
+        self.classes_ = np.unique(y_np)
+        if len(self.classes_) > 2:
+            raise ValueError("GBDTClassifier supports binary targets")
+        self.n_classes_ = 2
+        yb = (y_np == self.classes_[-1]).astype(np.float32) if len(self.classes_) == 2 else y_np.astype(np.float32)
+        rep = FitReport()
+        self._Booster = train(X, yb, self._train_params(), sample_weight=sample_weight, device=self.device,
+                              feature_names=names, feature_types=types, report=rep)
+        self.fit_report_ = rep
+        self.n_features_in_ = self._Booster.num_feature
+        if names is not None:
+            self.feature_names_in_ = np.array(names, dtype=object)
+        return self
+
+    def get_booster(self) -> Booster:
+        if not hasattr(self, "_Booster"):
+            raise ValueError("need to call fit or load_model beforehand")
+        return self._Booster
+
+    def _matrix(self, X) -> np.ndarray | torch.Tensor:
+        if isinstance(X, torch.Tensor):
+            return X
+        if hasattr(X, "columns") and getattr(self, "feature_names_in_", None) is not None:
+            X = X[list(self.feature_names_in_)]
+        return np.asarray(X.to_numpy(dtype=np.float32, na_value=np.nan) if hasattr(X, "to_numpy") else X,
+                          dtype=np.float32)
+
+    def predict_proba(self, X) -> np.ndarray:
+        p = self.get_booster().predict_proba(self._matrix(X), device=self.device)
+        p = p.cpu().numpy() if isinstance(p, torch.Tensor) else np.asarray(p)
+        return np.stack([1.0 - p, p], axis=1)
+
+    def predict(self, X) -> np.ndarray:
+        p = self.predict_proba(X)[:, 1]
+        pred = (p > 0.5).astype(np.int64)
+        return self.classes_[pred] if getattr(self, "classes_", None) is not None and len(self.classes_) == 2 else pred
+
+    def score(self, X, y) -> float:
+        from ..metrics.classification import accuracy_score
+
+        return accuracy_score(np.asarray(y), self.predict(X))
+
+    @property
+    def feature_importances_(self) -> np.ndarray:
+        return self.get_booster().feature_importances(self.importance_type or "gain")
+
+    # checkpoint I/O (reference: joblib.dump(best_model_tree) -> xgb_model_tree.pkl)
+    def sklearn_state_params(self) -> dict[str, Any]:
+        p = {k: getattr(self, k) for k in ["n_estimators", "max_depth", "learning_rate", "gamma", "min_child_weight",
+                                           "reg_alpha", "reg_lambda", "subsample", "colsample_bytree",
+                                           "scale_pos_weight", "base_score", "random_state", "max_bin", "device",
+                                           "importance_type", "n_jobs", "eval_metric"]}
+        p["kwargs"] = {"use_label_encoder": self.use_label_encoder} if self.use_label_encoder is not None else {}
+        return p
+
+    def save_pickle(self, path) -> None:
+        from pathlib import Path
+
+        Path(path).write_bytes(dump_pickle_bytes(self.get_booster(), self.sklearn_state_params()))
+
+    @classmethod
+    def load_pickle(cls, path) -> "GBDTClassifier":
+        from pathlib import Path
+        from .booster import load_pickle_bytes
+
+        st, bst = load_pickle_bytes(Path(path).read_bytes())
+        kw = {k: st.get(k) for k in cls._param_names if k in st and k not in ("use_label_encoder",)}
+        if isinstance(kw.get("scale_pos_weight"), np.floating):
+            kw["scale_pos_weight"] = float(kw["scale_pos_weight"])
+        m = cls(**kw)
+        m._Booster = bst
+        m.classes_ = np.array([0, 1])
+        m.n_classes_ = 2
+        m.n_features_in_ = bst.num_feature
+        if bst.feature_names:
+            m.feature_names_in_ = np.array(bst.feature_names, dtype=object)
+        return m
+
+    def save_model(self, path) -> None:
+        self.get_booster().save_model(path)
+
+    def load_model(self, path) -> None:
+        self._Booster = Booster.load_model(path)
+        self.classes_ = np.array([0, 1])
+        self.n_classes_ = 2
+
+
+# XGBoost-compatible alias used by the reference-shaped CLIs
+XGBClassifier = GBDTClassifier

@@ -1,0 +1,149 @@
+"""ctypes wrappers around the gfx950 GBDT trainer (``csrc/gbdt.hip``).
+
+``GpuGbdtTrainer`` owns a native trainer context: its workspace (packed gradients, ping-pong row
+indices, per-level histogram slots, node records) is allocated once per fit in HBM; inputs (bins,
+labels, weights, margins) are PyTorch tensors on the same device. ``grow`` enqueues whole trees on
+the current HIP stream without host synchronisation; ``fetch`` copies the node records back once.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..models.booster import NODE_DTYPE
+
+
+class GbdtConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_rows", ctypes.c_int64),
+        ("row_offset", ctypes.c_int64),
+        ("n_feat", ctypes.c_int32),
+        ("row_stride", ctypes.c_int32),
+        ("max_depth", ctypes.c_int32),
+        ("max_trees", ctypes.c_int32),
+        ("chunk", ctypes.c_int32),
+        ("feat_tile", ctypes.c_int32),
+        ("eta", ctypes.c_double),
+        ("lambda_", ctypes.c_double),
+        ("alpha", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("min_child_weight", ctypes.c_double),
+        ("subsample", ctypes.c_double),
+        ("gscale", ctypes.c_double),
+        ("hscale", ctypes.c_double),
+        ("base_margin", ctypes.c_float),
+        ("world_size", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("comm", ctypes.c_void_p),
+    ]
+
+
+assert ctypes.sizeof(GbdtConfig) == 128
+
+
+def row_stride(n_feat: int) -> int:
+    return (n_feat + 3) // 4 * 4
+
+
+def pick_chunk(n_rows: int) -> int:
+    """Rows per histogram/partition work item: aim for >= 2048 root items (8 per CU), pow2 in
+    [512, 16384] (16384 keeps per-block packed sums below 2^30)."""
+    target = max(1, n_rows // 2048)
+    c = 512
+    while c < target and c < 16384:
+        c *= 2
+    return c
+
+
+def pick_feat_tile(n_feat: int) -> int:
+    """Features per histogram block: all of them up to 32 (64 KiB of LDS), else tiles of 32."""
+    return min(row_stride(n_feat), 32)
+
+
+def bin_matrix(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Quantise ``X`` [N, F] float32 (CUDA) -> (bins [N, stride] uint8, binsT [F, N] uint8)."""
+    if X.device.type != "cuda":
+        raise ValueError("bin_matrix expects a CUDA tensor")
+    X = X.contiguous()
+    N, F = X.shape
+    st = row_stride(F)
+    bins = torch.empty((N, st), dtype=torch.uint8, device=X.device)
+    binsT = torch.empty((F, N), dtype=torch.uint8, device=X.device)
+    lib = _native.lib()
+    rc = lib.cobalt_bin_matrix(X.data_ptr(), N, F, F, cuts.contiguous().data_ptr(),
+                               nbins.to(torch.int32).contiguous().data_ptr(), bins.data_ptr(), st,
+                               binsT.data_ptr(), _native.stream_handle())
+    _native.check(rc, "cobalt_bin_matrix")
+    return bins, binsT
+
+
+class GpuGbdtTrainer:
+    def __init__(self, *, n_rows: int, n_feat: int, max_depth: int, max_trees: int, eta: float,
+                 reg_lambda: float, reg_alpha: float, gamma: float, min_child_weight: float, subsample: float,
+                 gscale: float, hscale: float, base_margin: float, seed: int, row_offset: int = 0,
+                 world_size: int = 1, comm: int | None = None, chunk: int | None = None,
+                 feat_tile: int | None = None):
+        self.lib = _native.lib()
+        cfg = GbdtConfig()
+        cfg.n_rows = n_rows
+        cfg.row_offset = row_offset
+        cfg.n_feat = n_feat
+        cfg.row_stride = row_stride(n_feat)
+        cfg.max_depth = max_depth
+        cfg.max_trees = max_trees
+        cfg.chunk = chunk or pick_chunk(n_rows)
+        cfg.feat_tile = feat_tile or pick_feat_tile(n_feat)
+        cfg.eta = eta
+        cfg.lambda_ = reg_lambda
+        cfg.alpha = reg_alpha
+        cfg.gamma = gamma
+        cfg.min_child_weight = min_child_weight
+        cfg.subsample = subsample
+        cfg.gscale = gscale
+        cfg.hscale = hscale
+        cfg.base_margin = base_margin
+        cfg.world_size = world_size
+        cfg.seed = seed & ((1 << 64) - 1)
+        cfg.comm = comm
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        rc = self.lib.cobalt_gbdt_create(ctypes.byref(cfg), ctypes.byref(h))
+        _native.check(rc, "cobalt_gbdt_create")
+        self.h = h
+        self.max_nodes = int(self.lib.cobalt_gbdt_max_nodes(h))
+        self._keep: list[torch.Tensor] = []
+
+    def set_data(self, bins, binsT, cuts, nbins, label, weight, margin, fmask) -> None:
+        ts = [bins, binsT, cuts, nbins, label, weight, margin, fmask]
+        for t in ts:
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError("trainer inputs must be contiguous CUDA tensors")
+        self._keep = ts
+        rc = self.lib.cobalt_gbdt_set_data(self.h, *[t.data_ptr() for t in ts])
+        _native.check(rc, "cobalt_gbdt_set_data")
+
+    def grow(self, t0: int, n_trees: int) -> None:
+        rc = self.lib.cobalt_gbdt_grow(self.h, t0, n_trees, _native.stream_handle())
+        if rc != 0 and self.cfg.comm:
+            raise RuntimeError(f"cobalt_gbdt_grow failed ({rc}): {self.lib.cobalt_comm_last_error().decode()}")
+        _native.check(rc, "cobalt_gbdt_grow")
+
+    def fetch(self, t0: int, n: int) -> np.ndarray:
+        out = np.zeros((n, self.max_nodes), dtype=NODE_DTYPE)
+        rc = self.lib.cobalt_gbdt_fetch_trees(self.h, t0, n, out.ctypes.data, _native.stream_handle())
+        _native.check(rc, "cobalt_gbdt_fetch_trees")
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.cobalt_gbdt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

@@ -1,0 +1,237 @@
+"""Inference entry points: margins, probabilities and TreeSHAP for a :class:`Booster`.
+
+GPU path: gfx950 kernels in ``csrc/predict.hip`` (forest packed once per booster and device, cached).
+CPU path: the NumPy reference implementations in ``models/booster.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..models.booster import Booster, Tree, predict_margin_host, sigmoid32, treeshap_host
+
+TILE_NODES = 6144
+MAX_PATH = 15
+
+_native.register("cobalt_predict", ctypes.c_int,
+                 [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
+_native.register("cobalt_treeshap", ctypes.c_int,
+                 [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p])
+
+PATH_ELEM = np.dtype([("lo", "<f4"), ("hi", "<f4"), ("feat", "<i4"), ("nan_ok", "<i4"), ("zero", "<f8")])
+
+
+def _bfs_order(t: Tree) -> list[int]:
+    order, q = [], [0]
+    while q:
+        nxt = []
+        for j in q:
+            order.append(j)
+            if t.left_children[j] != -1:
+                nxt += [int(t.left_children[j]), int(t.right_children[j])]
+        q = nxt
+    return order
+
+
+def pack_forest(b: Booster, n_trees: int | None = None) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(nodes uint32 [M, 2], tree_ptr int32 [T+1], tile_ptr int32 [n_tiles+1])."""
+    trees = b.trees[: (n_trees if n_trees is not None else b.num_trees)]
+    metas, vals, tree_ptr = [], [], [0]
+    for t in trees:
+        order = _bfs_order(t)
+        if len(order) > 0xFFFE:
+            raise ValueError("tree too large for the packed predictor")
+        nid = {j: i for i, j in enumerate(order)}
+        meta = np.zeros(len(order), dtype=np.uint32)
+        val = np.zeros(len(order), dtype=np.float32)
+        for j, i in nid.items():
+            if t.left_children[j] == -1:
+                meta[i] = 0xFFFF
+            else:
+                l, r = nid[int(t.left_children[j])], nid[int(t.right_children[j])]
+                assert r == l + 1
+                f = int(t.split_indices[j])
+                if f > 0x7FFF:
+                    raise ValueError("feature index too large for the packed predictor")
+                meta[i] = (l & 0xFFFF) | (f << 16) | (int(t.default_left[j]) << 31)
+            val[i] = t.split_conditions[j]
+        metas.append(meta)
+        vals.append(val)
+        tree_ptr.append(tree_ptr[-1] + len(order))
+    M = tree_ptr[-1]
+    nodes = np.zeros((M, 2), dtype=np.uint32)
+    if M:
+        nodes[:, 0] = np.concatenate(metas)
+        nodes[:, 1] = np.concatenate(vals).view(np.uint32)
+    tiles = [0]
+    acc = 0
+    for i in range(len(trees)):
+        sz = tree_ptr[i + 1] - tree_ptr[i]
+        if sz > TILE_NODES:
+            raise ValueError("tree exceeds the LDS tile")
+        if acc + sz > TILE_NODES:
+            tiles.append(i)
+            acc = 0
+        acc += sz
+    tiles.append(len(trees))
+    return nodes, np.asarray(tree_ptr, dtype=np.int32), np.asarray(tiles, dtype=np.int32)
+
+
+def extract_paths(b: Booster) -> tuple[np.ndarray, np.ndarray, np.ndarray, int]:
+    """Leaf paths with repeated features merged (elements, path_ptr, leaf values, max unique len)."""
+    elems: list[tuple] = []
+    ptr = [0]
+    vals: list[float] = []
+    max_len = 0
+    for t in b.trees:
+        cov = t.sum_hessian.astype(np.float64)
+        stack = [(0, [])]
+        while stack:
+            j, path = stack.pop()
+            if t.left_children[j] == -1:
+                merged: dict[int, list] = {}
+                order: list[int] = []
+                for (parent, f, went_left, child) in path:
+                    if f not in merged:
+                        merged[f] = [-np.inf, np.inf, True, 1.0]
+                        order.append(f)
+                    m = merged[f]
+                    thr = float(t.split_conditions[parent])
+                    if went_left:
+                        m[1] = min(m[1], thr)
+                    else:
+                        m[0] = max(m[0], thr)
+                    m[2] = m[2] and (bool(t.default_left[parent]) == went_left)
+                    m[3] *= cov[child] / cov[parent]
+                for f in order:
+                    lo, hi, nan_ok, z = merged[f]
+                    elems.append((np.float32(lo), np.float32(hi), f, int(nan_ok), z))
+                max_len = max(max_len, len(order))
+                ptr.append(len(elems))
+                vals.append(float(t.split_conditions[j]))
+                continue
+            f = int(t.split_indices[j])
+            l, r = int(t.left_children[j]), int(t.right_children[j])
+            stack.append((r, path + [(j, f, False, r)]))
+            stack.append((l, path + [(j, f, True, l)]))
+    arr = np.array(elems, dtype=PATH_ELEM) if elems else np.zeros(0, dtype=PATH_ELEM)
+    return arr, np.asarray(ptr, dtype=np.int32), np.asarray(vals, dtype=np.float64), max_len
+
+
+@dataclass
+class _GpuForest:
+    nodes: torch.Tensor
+    tree_ptr: torch.Tensor
+    tile_ptr: torch.Tensor
+    n_tiles: int
+    n_trees: int
+    elems: torch.Tensor | None = None
+    path_ptr: torch.Tensor | None = None
+    path_val: torch.Tensor | None = None
+    n_paths: int = 0
+    max_len: int = 0
+
+
+def gpu_forest(b: Booster, device: torch.device, n_trees: int | None = None, with_shap: bool = False) -> _GpuForest:
+    cache = b.__dict__.setdefault("_gpu_cache", {})
+    key = (str(device), n_trees if n_trees is not None else b.num_trees)
+    gf = cache.get(key)
+    if gf is None:
+        nodes, tptr, tiles = pack_forest(b, n_trees)
+        gf = _GpuForest(torch.from_numpy(nodes).to(device), torch.from_numpy(tptr).to(device),
+                        torch.from_numpy(tiles).to(device), len(tiles) - 1, len(tptr) - 1)
+        cache[key] = gf
+    if with_shap and gf.elems is None:
+        el, pp, pv, ml = extract_paths(b)
+        if ml > MAX_PATH:
+            raise ValueError(f"path with {ml} unique features exceeds the GPU TreeSHAP limit {MAX_PATH}")
+        gf.elems = torch.from_numpy(el.view(np.uint8).copy()).to(device)
+        gf.path_ptr = torch.from_numpy(pp).to(device)
+        gf.path_val = torch.from_numpy(pv).to(device)
+        gf.n_paths = len(pv)
+        gf.max_len = ml
+    return gf
+
+
+def _device_of(X, device) -> torch.device:
+    if device is not None:
+        d = torch.device(device)
+    elif isinstance(X, torch.Tensor):
+        d = X.device
+    else:
+        d = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+def _as_f32(X, device: torch.device) -> torch.Tensor:
+    if isinstance(X, torch.Tensor):
+        return X.to(device=device, dtype=torch.float32).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(np.asarray(X, dtype=np.float32)), device=device)
+
+
+def predict_gpu(b: Booster, X: torch.Tensor, n_trees: int | None = None, out_margin: torch.Tensor | None = None,
+                out_prob: torch.Tensor | None = None) -> None:
+    """Launch the predictor on the current stream (graph-capturable; no allocation, no sync)."""
+    gf = gpu_forest(b, X.device, n_trees)
+    N, F = X.shape
+    if F < b.num_feature:
+        raise ValueError(f"X has {F} features, model needs {b.num_feature}")
+    rc = _native.lib().cobalt_predict(X.data_ptr(), N, F, X.stride(0), gf.nodes.data_ptr(), gf.tree_ptr.data_ptr(),
+                                      gf.tile_ptr.data_ptr(), gf.n_tiles, b.base_margin,
+                                      out_margin.data_ptr() if out_margin is not None else None,
+                                      out_prob.data_ptr() if out_prob is not None else None,
+                                      _native.stream_handle())
+    _native.check(rc, "cobalt_predict")
+
+
+def treeshap_gpu(b: Booster, X: torch.Tensor, phi: torch.Tensor) -> None:
+    """Accumulate TreeSHAP values into ``phi`` [N, F] float64 (must be zeroed) on the current stream."""
+    gf = gpu_forest(b, X.device, None, with_shap=True)
+    N, F = X.shape
+    lib = _native.lib()
+    for s in range(0, N, 65535):
+        e = min(N, s + 65535)
+        rc = lib.cobalt_treeshap(X[s:e].data_ptr(), e - s, F, X.stride(0), gf.elems.data_ptr(), gf.path_ptr.data_ptr(),
+                                 gf.path_val.data_ptr(), gf.n_paths, gf.max_len, phi[s:e].data_ptr(),
+                                 _native.stream_handle())
+        _native.check(rc, "cobalt_treeshap")
+
+
+def predict_margin(b: Booster, X, device=None, n_trees: int | None = None):
+    d = _device_of(X, device)
+    if d.type == "cuda":
+        Xt = _as_f32(X, d)
+        out = torch.empty(Xt.shape[0], dtype=torch.float32, device=d)
+        predict_gpu(b, Xt, n_trees, out_margin=out)
+        return out if isinstance(X, torch.Tensor) else out.cpu().numpy()
+    Xn = X.cpu().numpy() if isinstance(X, torch.Tensor) else np.asarray(X, dtype=np.float32)
+    return predict_margin_host(b, Xn, n_trees)
+
+
+def predict_proba(b: Booster, X, device=None):
+    d = _device_of(X, device)
+    if d.type == "cuda":
+        Xt = _as_f32(X, d)
+        out = torch.empty(Xt.shape[0], dtype=torch.float32, device=d)
+        predict_gpu(b, Xt, None, out_prob=out)
+        return out if isinstance(X, torch.Tensor) else out.cpu().numpy()
+    return sigmoid32(predict_margin(b, X, "cpu"))
+
+
+def shap_values(b: Booster, X, device=None):
+    d = _device_of(X, device)
+    if d.type == "cuda":
+        Xt = _as_f32(X, d)
+        phi = torch.zeros((Xt.shape[0], Xt.shape[1]), dtype=torch.float64, device=d)
+        treeshap_gpu(b, Xt, phi)
+        return phi if isinstance(X, torch.Tensor) else phi.cpu().numpy()
+    Xn = X.cpu().numpy() if isinstance(X, torch.Tensor) else np.asarray(X, dtype=np.float32)
+    return treeshap_host(b, Xn)

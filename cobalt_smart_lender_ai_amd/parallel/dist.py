@@ -1,0 +1,168 @@
+"""Process-group management for data-parallel training and scoring (one process per GPU).
+
+Bootstrap and small metadata collectives go through ``torch.distributed`` (backend ``"nccl"`` is RCCL
+on ROCm; ``"gloo"`` for CPU rehearsals). The hot GBDT collective — the per-level int64 histogram
+all-reduce — runs on a dedicated native RCCL communicator (``csrc/comm.cpp``) created here from a
+unique id broadcast over the torch group, so the C++ trainer can enqueue it on its own HIP stream
+in the middle of a tree without returning to Python.
+
+The reference has no distributed layer; this module is the MI355X-native
+replacement for its ``n_jobs=-1`` process parallelism (model_tree_train_test.py:155).
+"""
+from __future__ import annotations
+
+import ctypes
+import datetime
+import os
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as tdist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    native_comm: int | None = None          # cobalt_comm handle (GPU) or None
+    _owns_group: bool = field(default=False, repr=False)
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world > 1
+
+    # ------------------------------------------------------------------ small collectives
+    def allreduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.world == 1:
+            return t
+        rop = {"sum": tdist.ReduceOp.SUM, "max": tdist.ReduceOp.MAX, "min": tdist.ReduceOp.MIN}[op]
+        tdist.all_reduce(t, op=rop)
+        return t
+
+    def allreduce_scalar(self, v: float, op: str = "sum", device: torch.device | str = "cpu") -> float:
+        if self.world == 1:
+            return float(v)
+        t = torch.tensor([v], dtype=torch.float64, device=self._coll_device(device))
+        self.allreduce(t, op)
+        return float(t.item())
+
+    def allgather_rows(self, t: torch.Tensor, pad_value: float = float("nan")) -> torch.Tensor:
+        """All-gather a [n_local, F] tensor with per-rank row counts (pads with ``pad_value``)."""
+        if self.world == 1:
+            return t
+        dev = self._coll_device(t.device)
+        x = t.to(dev)
+        n = torch.tensor([x.shape[0]], dtype=torch.int64, device=dev)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        tdist.all_gather(ns, n)
+        mx = int(max(int(v.item()) for v in ns))
+        if x.shape[0] < mx:
+            pad = torch.full((mx - x.shape[0],) + tuple(x.shape[1:]), pad_value, dtype=x.dtype, device=dev)
+            x = torch.cat([x, pad], 0)
+        outs = [torch.empty_like(x) for _ in range(self.world)]
+        tdist.all_gather(outs, x.contiguous())
+        return torch.cat(outs, 0).to(t.device)
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            if self.backend == "nccl":
+                tdist.barrier(device_ids=[self.local_rank])
+            else:
+                tdist.barrier()
+
+    def _coll_device(self, dev) -> torch.device:
+        if self.backend == "nccl":
+            return torch.device("cuda", self.local_rank)
+        return torch.device("cpu")
+
+    def close(self) -> None:
+        if self.native_comm:
+            from .. import _native
+
+            _native.lib().cobalt_comm_destroy(ctypes.c_void_p(self.native_comm), 0)
+            self.native_comm = None
+        if self._owns_group and tdist.is_initialized():
+            tdist.destroy_process_group()
+            self._owns_group = False
+
+
+_CTX: DistContext | None = None
+
+
+def init_from_env(backend: str | None = None, native: bool | None = None, timeout_s: int = 600) -> DistContext:
+    """Initialise from torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (single process if absent)."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        _CTX = DistContext()
+        return _CTX
+    use_gpu = torch.cuda.is_available()
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    owns = False
+    if not tdist.is_initialized():
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local_rank)
+        tdist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        owns = True
+    ctx = DistContext(rank=rank, world=world, local_rank=local_rank, backend=backend, _owns_group=owns)
+    if native is None:
+        native = backend == "nccl"
+    if native:
+        ctx.native_comm = create_native_comm(ctx)
+    _CTX = ctx
+    return ctx
+
+
+def create_native_comm(ctx: DistContext) -> int:
+    """Create the trainer's RCCL communicator; the unique id travels over the torch group."""
+    from .. import _native
+
+    lib = _native.lib()
+    rc = lib.cobalt_comm_load(_native.rccl_path().encode())
+    if rc != 0:
+        raise RuntimeError(f"RCCL load failed: {lib.cobalt_comm_last_error().decode()}")
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if ctx.rank == 0:
+        buf = (ctypes.c_uint8 * 128)()
+        rc = lib.cobalt_comm_unique_id(buf)
+        if rc != 0:
+            raise RuntimeError(f"ncclGetUniqueId failed: {lib.cobalt_comm_last_error().decode()}")
+        uid = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+    dev_uid = uid.to(ctx._coll_device("cpu"))
+    tdist.broadcast(dev_uid, src=0)
+    raw = bytes(dev_uid.cpu().tolist())
+    cbuf = (ctypes.c_uint8 * 128).from_buffer_copy(raw)
+    handle = ctypes.c_void_p()
+    rc = lib.cobalt_comm_init(cbuf, ctx.world, ctx.rank, ctypes.byref(handle))
+    if rc != 0:
+        raise RuntimeError(f"ncclCommInitRank failed: {lib.cobalt_comm_last_error().decode()}")
+    return int(handle.value)
+
+
+def get_context() -> DistContext:
+    return _CTX if _CTX is not None else DistContext()
+
+
+def shutdown() -> None:
+    global _CTX
+    if _CTX is not None:
+        _CTX.close()
+        _CTX = None
+
+
+def shard_range(n_global: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous row shard [start, end) of rank ``rank`` (first ``n % world`` ranks get one more)."""
+    base, rem = divmod(n_global, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)

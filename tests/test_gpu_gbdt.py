@@ -1,0 +1,113 @@
+"""GPU (gfx950) tests of the GBDT kernels against the NumPy oracles (run with ``-m gpu``)."""
+import numpy as np
+import pytest
+import torch
+
+from cobalt_smart_lender_ai_amd.dataio import synth
+from cobalt_smart_lender_ai_amd.models import booster as B
+from cobalt_smart_lender_ai_amd.models import gbdt, sketch
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, seed=0):
+    X, y = synth.make_lendingclub(n, seed=seed)
+    return X, y
+
+
+def test_native_library_loads():
+    from cobalt_smart_lender_ai_amd import _native
+
+    lib = _native.load()
+    assert lib is not None and _native.loaded_path().endswith("libcobalt_hip.so")
+
+
+def test_bin_matrix_matches_host():
+    from cobalt_smart_lender_ai_amd.ops import gbdt_ops
+
+    X, _ = _data(50_000)
+    cuts, nb = sketch.compute_cuts(X, 256)
+    Xg = X.cuda()
+    bins, binsT = gbdt_ops.bin_matrix(Xg, cuts.cuda(), nb.cuda())
+    ref = sketch.bin_matrix_host(X.numpy(), cuts.numpy(), nb.numpy())
+    F = X.shape[1]
+    assert np.array_equal(bins[:, :F].cpu().numpy(), ref)
+    assert np.array_equal(binsT.cpu().numpy(), ref.T)
+
+
+def test_sketch_gpu_equals_cpu():
+    X, _ = _data(100_000, seed=3)
+    c1, n1 = sketch.compute_cuts(X, 256)
+    c2, n2 = sketch.compute_cuts(X.cuda(), 256)
+    assert torch.equal(n1, n2.cpu())
+    assert torch.equal(c1, c2.cpu())
+
+
+@pytest.mark.parametrize("kw", [
+    dict(n_estimators=8, max_depth=5, learning_rate=0.3, gamma=0.0),
+    dict(n_estimators=6, max_depth=7, learning_rate=0.05, gamma=5.0, scale_pos_weight=6.7),
+    dict(n_estimators=5, max_depth=4, learning_rate=0.1, reg_alpha=0.5, reg_lambda=2.0, min_child_weight=3.0,
+         subsample=0.8, colsample_bytree=0.5),
+])
+def test_gpu_trees_identical_to_host_oracle(kw):
+    X, y = _data(30_000, seed=1)
+    p = gbdt.GBDTParams(random_state=7, **kw)
+    bg = gbdt.train(X, y, p, device="cuda")
+    bc = gbdt.train(X, y, p, device="cpu")
+    assert bg.num_trees == bc.num_trees
+    for tg, tc in zip(bg.trees, bc.trees):
+        assert tg.num_nodes == tc.num_nodes
+        assert np.array_equal(tg.split_indices, tc.split_indices)
+        assert np.array_equal(tg.left_children, tc.left_children)
+        assert np.array_equal(tg.default_left, tc.default_left)
+        assert np.array_equal(tg.split_conditions, tc.split_conditions)
+        assert np.array_equal(tg.loss_changes, tc.loss_changes)
+        assert np.array_equal(tg.sum_hessian, tc.sum_hessian)
+
+
+def test_gpu_training_margin_consistent_with_predictor():
+    X, y = _data(20_000, seed=2)
+    b = gbdt.train(X, y, gbdt.GBDTParams(n_estimators=10, max_depth=6), device="cuda")
+    mg = b.predict_margin(X.cuda()).cpu().numpy()
+    mh = B.predict_margin_host(b, X.numpy())
+    assert np.array_equal(mg, mh)
+
+
+def test_predict_reference_model_gpu(reference_booster):
+    b = reference_booster
+    X, _ = _data(20_000, seed=5)
+    Xr = synth.make_lendingclub(20_000, seed=5, log_space=False)[0]
+    for M in (X, Xr):
+        mg = b.predict_margin(M.cuda()).cpu().numpy()
+        mh = B.predict_margin_host(b, M.numpy())
+        assert np.array_equal(mg, mh)
+
+
+def test_treeshap_gpu_matches_recursive_oracle(reference_booster):
+    b = reference_booster
+    X, _ = _data(6, seed=9)
+    X[0, 5] = float("nan")
+    ui = torch.tensor([[10000, 36, 300, 660, 700, 1, 2, 2000, 10, 0, 3, 4000, 0, 0, 0, 0, 0, 0, 0, 0]],
+                      dtype=torch.float32)
+    X = torch.cat([X, ui])
+    phi_g = b.shap_values(X.cuda()).cpu().numpy()
+    phi_h = B.treeshap_host(b, X.numpy())
+    np.testing.assert_allclose(phi_g, phi_h, rtol=1e-9, atol=1e-9)
+    # local accuracy against the GPU margin
+    m = b.predict_margin(X.cuda()).cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(phi_g.sum(1) + b.expected_value(), m, atol=2e-5)
+
+
+def test_gpu_auc_parity_with_cpu_oracle():
+    from cobalt_smart_lender_ai_amd.metrics.auc import roc_auc
+
+    X, y = _data(60_000, seed=11)
+    Xtr, ytr, Xte, yte = X[:40_000], y[:40_000], X[40_000:], y[40_000:]
+    spw = float((ytr == 0).sum() / (ytr == 1).sum())
+    p = gbdt.GBDTParams(n_estimators=40, max_depth=7, learning_rate=0.05, gamma=5.0, scale_pos_weight=spw)
+    bg = gbdt.train(Xtr, ytr, p, device="cuda")
+    bc = gbdt.train(Xtr, ytr, p, device="cpu")
+    ag = roc_auc(yte, bg.predict_proba(Xte.cuda()).cpu())
+    ac = roc_auc(yte, bc.predict_proba(Xte.numpy(), device="cpu"))
+    assert abs(ag - ac) <= 0.002
+    assert ag > 0.9
