@@ -24,6 +24,7 @@
 #include "common.h"
 #include <math.h>
 #include <string.h>
+#include <stdlib.h>
 #include <vector>
 #include <algorithm>
 
@@ -93,7 +94,7 @@ struct GbdtConfig {
 
 struct GbdtDev {
   // inputs
-  const uint8_t* bins;    // [N][stride]
+  uint8_t* bins;          // [N][stride] row records: bins[0..F) | pad | packed (g,h) u64 at goff
   const uint8_t* binsT;   // [F][N]
   const float* cuts;      // [F][256]
   const int32_t* nbins;   // [F]
@@ -102,7 +103,7 @@ struct GbdtDev {
   float* margin;          // [N]
   const uint8_t* fmask;   // [max_trees][F] colsample_bytree masks
   // workspace
-  uint64_t* gpair;        // [N]
+  int32_t goff;           // byte offset of the packed gradient pair inside a row record
   int32_t* ridx[2];       // [N] x2
   int64_t* hist_b[2];     // [pairs][F+1][256][2]
   int64_t* hist_s[2];
@@ -112,6 +113,13 @@ struct GbdtDev {
   WorkItem* items_p;      // partition work list
   int32_t* counters;      // [0] = #hist items, [1] = #partition items
   int32_t* cursors;       // [max_nodes][2]
+  int32_t* item_left;     // [items] left-row count per partition work item
+  int2* layout;           // [F] histogram LDS layout: x = cell offset within tile, y = log2(copies)
+  int32_t* tile_entries;  // [n_tiles] LDS cells per feature tile
+  int64_t* child_cnt;     // [max_nodes] row counts of the current level's nodes (global under DP)
+  uint64_t* slab;         // [items][F][256] packed per-item partial histograms
+  int64_t* slab_tot;      // [items][2] per-item (G, H) totals
+  int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush
   int64_t n;
   int64_t row_offset;
   int32_t F, stride, max_depth, max_nodes, chunk, feat_tile;
@@ -139,7 +147,8 @@ __global__ __launch_bounds__(256) void k_bin(const float* __restrict__ X, int64_
        row += (int64_t)gridDim.x * blockDim.x) {
     const float* x = X + row * ldx;
     uint32_t word = 0;
-    for (int f = 0; f < stride; ++f) {
+    const int fw = (F + 3) & ~3;  // bytes written per row (the record tail holds the gradient pair)
+    for (int f = 0; f < fw; ++f) {
       uint32_t b = 0;
       if (f < F) {
         float v = x[f];
@@ -187,12 +196,62 @@ __global__ void k_init_tree(GbdtDev d) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree) {
+// Stage tree `t` (heap-ordered node records) into LDS as {meta, leaf value}:
+// meta = feat | bin << 16 | default_left << 24 | is_split << 25.
+__device__ __forceinline__ void stage_tree(const GbdtDev& d, int t, uint32_t* s_meta, float* s_leaf) {
+  const Node* tr = d.trees + (int64_t)t * d.max_nodes;
+  for (int i = threadIdx.x; i < d.max_nodes; i += blockDim.x) {
+    const Node nd = tr[i];
+    const uint32_t split = nd.status == kSplit ? 1u : 0u;
+    s_meta[i] = (uint32_t)(nd.feat & 0xFFFF) | ((uint32_t)(nd.bin & 0xFF) << 16) |
+                ((uint32_t)(nd.default_left & 1) << 24) | (split << 25);
+    s_leaf[i] = nd.leaf_value;
+  }
+}
+
+// Leaf of row `r` in a staged tree, walking the bins exactly like the partition step does.
+__device__ __forceinline__ float tree_leaf(const GbdtDev& d, int64_t r, const uint32_t* s_meta, const float* s_leaf) {
+  const uint8_t* row = d.bins + r * d.stride;
+  int n = 0;
+  uint32_t m = s_meta[0];
+  while (m & (1u << 25)) {
+    const int f = m & 0xFFFF;
+    const uint32_t b = row[f];
+    const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+    n = 2 * n + (left ? 1 : 2);
+    m = s_meta[n];
+  }
+  return s_leaf[n];
+}
+
+// Gradient kernel. When `apply_tree >= 0` it first adds that tree's leaf value to every row's margin
+// (the prediction-cache update, done as a coalesced traversal over row-major bins instead of a
+// scatter over the leaves' row lists), then computes binary:logistic g/h in fp64, applies row
+// subsampling, quantises and packs them. Also resets ridx to the identity for the root.
+__global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tree) {
+  extern __shared__ uint32_t s_tree[];
+  {  // zero the root histogram slot
+    int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
+         e += (int64_t)gridDim.x * blockDim.x)
+      zp[e] = make_int4(0, 0, 0, 0);
+  }
+  uint32_t* s_meta = s_tree;
+  float* s_leaf = reinterpret_cast<float*>(s_tree + d.max_nodes);
+  if (apply_tree >= 0) {
+    stage_tree(d, apply_tree, s_meta, s_leaf);
+    __syncthreads();
+  }
   const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n;
        i += (int64_t)gridDim.x * blockDim.x) {
     d.ridx[0][i] = (int32_t)i;
-    const double m = (double)d.margin[i];
+    float mf = d.margin[i];
+    if (apply_tree >= 0) {
+      mf += tree_leaf(d, i, s_meta, s_leaf);
+      d.margin[i] = mf;
+    }
+    const double m = (double)mf;
     const double p = 1.0 / (1.0 + exp(-m));
     const double y = (double)d.label[i];
     const double w = (double)d.weight[i];
@@ -206,18 +265,82 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree) {
     int64_t hq = (int64_t)rint(h * d.hscale);
     gq = gq > 65536 ? 65536 : (gq < -65536 ? -65536 : gq);
     hq = hq > 65536 ? 65536 : (hq < 0 ? 0 : hq);
-    d.gpair[i] = ((uint64_t)(uint32_t)(int32_t)gq << 32) | (uint64_t)(uint32_t)hq;
+    *reinterpret_cast<uint64_t*>(d.bins + i * d.stride + d.goff) =
+        ((uint64_t)(uint32_t)(int32_t)gq << 32) | (uint64_t)(uint32_t)hq;
   }
+}
+
+// Add tree `t`'s leaf values to the margins (used after the last boosting round).
+__global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
+  extern __shared__ uint32_t s_tree[];
+  uint32_t* s_meta = s_tree;
+  float* s_leaf = reinterpret_cast<float*>(s_tree + d.max_nodes);
+  stage_tree(d, t, s_meta, s_leaf);
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    d.margin[i] += tree_leaf(d, i, s_meta, s_leaf);
 }
 
 // ------------------------------------------------------------------------------------------
 // Level planning: child row ranges from partition cursors, choose which child to build,
-// emit histogram work items. One block.
+// emit histogram work items. One block; work items are emitted by all threads in parallel.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level) {
-  __shared__ int32_t s_chunks[1024];
+// Exclusive scan of v[0..n) (n <= 1024) in LDS by a 256-thread block; returns the total.
+__device__ int block_excl_scan_1024(int32_t* v, int n, int32_t* s_wave) {
+  // each thread owns 4 consecutive entries
+  const int t = threadIdx.x;
+  int a[4], tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = t * 4 + k;
+    a[k] = i < n ? v[i] : 0;
+    tot += a[k];
+  }
+  const int incl = wave_incl_scan(tot);
+  if (lane_id() == kWave - 1) s_wave[wave_id()] = incl;
+  __syncthreads();
+  int wbase = 0, all = 0;
+  for (int w = 0; w < (int)(blockDim.x / kWave); ++w) {
+    if (w < wave_id()) wbase += s_wave[w];
+    all += s_wave[w];
+  }
+  int run = wbase + incl - tot;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = t * 4 + k;
+    if (i < n) v[i] = run;
+    run += a[k];
+  }
+  __syncthreads();
+  return all;
+}
+
+// Emit `total` work items: item i belongs to slot p with off[p] <= i < off[p+1].
+__device__ void emit_items(WorkItem* out, int total, const int32_t* s_off, int nslots, const int32_t* s_node,
+                           const Node* nodes, int chunk, bool slot_is_pair) {
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    int lo = 0, hi = nslots - 1;
+    while (lo < hi) {  // largest p with s_off[p] <= i
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int p = lo;
+    const int nd = s_node[p];
+    const int c = i - s_off[p];
+    WorkItem w;
+    w.node = nd;
+    w.slot = slot_is_pair ? p : 0;
+    w.begin = nodes[nd].start + c * chunk;
+    w.end = min(nodes[nd].start + nodes[nd].count, w.begin + chunk);
+    out[i] = w;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level, int chunk) {
+  __shared__ int32_t s_off[1024];
   __shared__ int32_t s_node[1024];
-  __shared__ int32_t s_off[1025];
+  __shared__ int32_t s_wave[8];
   const int npairs = level == 0 ? 1 : (1 << (level - 1));
   for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
     int built = -1;
@@ -233,14 +356,15 @@ __global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level) {
         d.nodes[L].count = lc;
         d.nodes[R].start = par.start + lc;
         d.nodes[R].count = par.count - lc;
-        const bool left_small = d.nodes[L].H <= d.nodes[R].H;
+        // histogram the child with fewer (global) rows; the sibling comes by exact subtraction
+        const bool left_small = d.child_cnt[L] <= d.child_cnt[R];
         d.nodes[L].build = left_small ? 1 : 0;
         d.nodes[R].build = left_small ? 0 : 1;
         built = left_small ? L : R;
       }
     }
     s_node[p] = built;
-    s_chunks[p] = built >= 0 ? (d.nodes[built].count + d.chunk - 1) / d.chunk : 0;
+    s_off[p] = built >= 0 ? (d.nodes[built].count + chunk - 1) / chunk : 0;
   }
   // reset partition cursors of this level's nodes
   const int first = (1 << level) - 1, nlev = 1 << level;
@@ -249,93 +373,205 @@ __global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level) {
     d.cursors[2 * (first + i) + 1] = 0;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int p = 0; p < npairs; ++p) { s_off[p] = acc; acc += s_chunks[p]; }
-    s_off[npairs] = acc;
-    d.counters[0] = acc;
-  }
-  __syncthreads();
-  for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
-    const int nd = s_node[p];
-    if (nd < 0) continue;
-    const int st = d.nodes[nd].start, cnt = d.nodes[nd].count;
-    for (int c = 0; c < s_chunks[p]; ++c) {
-      WorkItem w;
-      w.node = nd;
-      w.slot = p;
-      w.begin = st + c * d.chunk;
-      w.end = min(st + cnt, w.begin + d.chunk);
-      d.items_h[s_off[p] + c] = w;
-    }
-  }
+  const int total = block_excl_scan_1024(s_off, npairs, s_wave);
+  if (threadIdx.x == 0) d.counters[0] = total;
+  emit_items(d.items_h, total, s_off, npairs, s_node, d.nodes, chunk, true);
 }
 
 // ------------------------------------------------------------------------------------------
 // Histogram build (K15): LDS-privatised packed-u64 histograms, one work item per block,
-// blockIdx.y = feature tile. Flush = one int64 global atomic per non-zero cell per block.
+// blockIdx.y = feature tile. LDS layout is bin-count aware: feature f occupies nb_f * K_f cells
+// where K_f = min(64, 2^floor(log2(256/nb_f))) lane-private copies (lane l adds into copy
+// l % K_f), so a 2-bin dummy feature gets 64 copies and its 64 lanes never collide on one LDS
+// address, while a 255-bin quantile feature (naturally spread) keeps one copy. Flush sums the
+// copies and issues one int64 global atomic per non-zero (feature, bin, stat) per block.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_hist(GbdtDev d, int parity, int tree) {
-  extern __shared__ uint64_t s_hist[];  // [feat_tile][256]
-  __shared__ int64_t s_tot[2][4];
+constexpr int kMaxTileWords = 8;   // feature tile <= 32 features (8 dwords of bins)
+
+__global__ __launch_bounds__(512) void k_hist(GbdtDev d, int parity, int tree) {
+  extern __shared__ uint64_t s_hist[];
+  __shared__ int64_t s_tot[2][8];
   const int item = blockIdx.x;
   if (item >= d.counters[0]) return;
   const WorkItem w = d.items_h[item];
   const int f0 = blockIdx.y * d.feat_tile;
   if (f0 >= d.F) return;
   const int ft = min(d.feat_tile, d.F - f0);
+  const int2* __restrict__ lay = d.layout + f0;
+  const int entries = d.tile_entries[blockIdx.y] + kWave;  // + per-lane trash cells
   const uint8_t* fm = d.fmask + (int64_t)tree * d.F + f0;
   uint64_t fbits = 0;
   for (int k = 0; k < ft; ++k) fbits |= (uint64_t)(fm[k] != 0) << k;
 
-  for (int i = threadIdx.x; i < ft * kMaxBins; i += blockDim.x) s_hist[i] = 0ull;
+  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   __syncthreads();
 
   const int32_t* rix = d.ridx[parity];
+  const bool identity = parity == 0 && w.node == 0;  // root level: ridx is the identity
+  const int lane = lane_id();
   int64_t tg = 0, th = 0;
-  const int nwords = (ft + 3) >> 2;
-  for (int i = w.begin + threadIdx.x; i < w.end; i += blockDim.x) {
-    const int r = rix[i];
-    const uint64_t gp = d.gpair[r];
-    tg += (int64_t)(int32_t)(uint32_t)(gp >> 32);
-    th += (int64_t)(uint32_t)gp;
-    if (gp == 0ull) continue;
-    const uint32_t* row = reinterpret_cast<const uint32_t*>(d.bins + (int64_t)r * d.stride + f0);
-    for (int q = 0; q < nwords; ++q) {
-      const uint32_t word = row[q];
+  const int B = blockDim.x;
+  constexpr int U = 4;  // rows in flight per thread
+  // per-feature copy shift (3 bits) for each 8-feature chunk, kept in scalar registers: reading
+  // them from LDS or scalar memory inside the loop would force lgkmcnt waits on in-flight ds_add
+  uint32_t sh0 = 0, sh1 = 0, sh2 = 0, sh3 = 0;
+  for (int fl = 0; fl < ft; ++fl) {
+    const uint32_t v = (uint32_t)(lay[fl].y & 7) << (3 * (fl & 7));
+    switch (fl >> 3) { case 0: sh0 |= v; break; case 1: sh1 |= v; break; case 2: sh2 |= v; break; default: sh3 |= v; }
+  }
+  const uint32_t trash = (uint32_t)(ft * kMaxBins) + lane;
+  if (d.stride == 32 && ft == d.F && ft <= 24) {
+    // 32-byte records (bins | pad | (g,h)): one pair of 16-byte loads per row
+    for (int i0 = w.begin + threadIdx.x; i0 < w.end; i0 += U * B) {
+      int r[U];
+      uint4 a[U], b2[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int fl = q * 4 + k;
-        const uint32_t b = (word >> (8 * k)) & 0xffu;
-        if (fl < ft && b != kMissingBin && ((fbits >> fl) & 1ull)) atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[fl * kMaxBins + b]),
-                                                               (unsigned long long)gp);
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * B;
+        r[u] = i < w.end ? (identity ? i : rix[i]) : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint4* rec = reinterpret_cast<const uint4*>(d.bins + (int64_t)(r[u] >= 0 ? r[u] : r[0]) * 32);
+        a[u] = rec[0];
+        b2[u] = rec[1];
+        if (r[u] < 0) { b2[u].z = 0u; b2[u].w = 0u; }
+        tg += (int64_t)(int32_t)b2[u].w;
+        th += (int64_t)b2[u].z;
+      }
+#pragma unroll
+      for (int fl = 0; fl < 24; ++fl) {
+        if (fl < ft) {
+          const bool fen = (fbits >> fl) & 1ull;  // colsample: disabled features add into trash
+          const uint32_t shw = fl < 8 ? sh0 : (fl < 16 ? sh1 : sh2);
+          const uint32_t sh = (shw >> (3 * (fl & 7))) & 7u;
+          const uint32_t cbase = (uint32_t)(fl * kMaxBins) + (lane & ((1u << sh) - 1u));
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int q = fl >> 2;
+            const uint32_t word = q == 0 ? a[u].x : q == 1 ? a[u].y : q == 2 ? a[u].z : q == 3 ? a[u].w
+                                : q == 4 ? b2[u].x : b2[u].y;
+            const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
+            const uint32_t cell = (bb != kMissingBin && fen) ? cbase + (bb << sh) : trash;
+            const uint64_t gp = ((uint64_t)b2[u].w << 32) | b2[u].z;
+            atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp);
+          }
+        }
+      }
+    }
+  } else {
+  const int nchunks = (ft + 7) >> 3;
+  for (int i0 = w.begin + threadIdx.x; i0 < w.end; i0 += U * B) {
+    int r[U];
+    uint64_t gp[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * B;
+      r[u] = i < w.end ? (identity ? i : rix[i]) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      gp[u] = r[u] >= 0 ? *reinterpret_cast<const uint64_t*>(d.bins + (int64_t)r[u] * d.stride + d.goff) : 0ull;
+      tg += (int64_t)(int32_t)(uint32_t)(gp[u] >> 32);
+      th += (int64_t)(uint32_t)gp[u];
+    }
+    for (int c = 0; c < nchunks; ++c) {
+      uint32_t lo[U], hi[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = r[u] >= 0 ? r[u] : r[0];
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(d.bins + (int64_t)rr * d.stride + f0 + c * 8);
+        lo[u] = row[0];
+        hi[u] = (c * 8 + 4 < ft) ? row[1] : 0xFFFFFFFFu;
+      }
+      const uint32_t shc = c == 0 ? sh0 : (c == 1 ? sh1 : (c == 2 ? sh2 : sh3));
+      const uint32_t fbc = (uint32_t)(fbits >> (c * 8)) & 0xFFu;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if ((fbc >> k) & 1u) {
+          const uint32_t sh = (shc >> (3 * k)) & 7u;
+          const uint32_t cbase = (uint32_t)((c * 8 + k) * kMaxBins) + (lane & ((1u << sh) - 1u));
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            // branch-free: missing values (and padded rows, gp == 0) add into a per-lane trash cell
+            const uint32_t b = ((k < 4 ? lo[u] : hi[u]) >> (8 * (k & 3))) & 0xffu;
+            const uint32_t cell = b != kMissingBin ? cbase + (b << sh) : trash;
+            if (d.ablate == 1) tg += cell; else
+            atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp[u]);
+          }
+        }
       }
     }
   }
+  }
   __syncthreads();
-  int64_t* gh = d.hist_b[parity] + (int64_t)w.slot * d.slot_elems;
+  // Per-item partial histogram -> slab (plain coalesced stores; the packed u64 of the K copies can
+  // be summed directly because the per-item sums obey the same < 2^31 / < 2^32 bounds).
+  uint64_t* slab = d.slab + (int64_t)item * d.F * kMaxBins + (int64_t)f0 * kMaxBins;
   for (int e = threadIdx.x; e < ft * kMaxBins; e += blockDim.x) {
-    const uint64_t v = s_hist[e];
-    if (v) {
-      const int64_t g = (int64_t)(int32_t)(uint32_t)(v >> 32);
-      const int64_t h = (int64_t)(uint32_t)v;
-      int64_t* cell = gh + ((int64_t)(f0 * kMaxBins + e)) * 2;
-      atomicAdd(reinterpret_cast<unsigned long long*>(cell), (unsigned long long)g);
-      atomicAdd(reinterpret_cast<unsigned long long*>(cell + 1), (unsigned long long)h);
+    const int fl = e >> 8, b = e & 255;
+    uint64_t v = 0;
+    if (((fbits >> fl) & 1ull) && b < d.nbins[f0 + fl]) {
+      const int sh = lay[fl].y;
+      const uint64_t* cell = s_hist + fl * kMaxBins + (b << sh);
+      for (int c = 0; c < (1 << sh); ++c) v += cell[c];
     }
+    slab[e] = v;
   }
   if (blockIdx.y == 0) {
     tg = wave_sum(tg);
     th = wave_sum(th);
-    if (lane_id() == 0) { s_tot[0][wave_id()] = tg; s_tot[1][wave_id()] = th; }
+    if (lane == 0) { s_tot[0][wave_id()] = tg; s_tot[1][wave_id()] = th; }
     __syncthreads();
     if (threadIdx.x == 0) {
       int64_t G = 0, H = 0;
       for (int k = 0; k < (int)(blockDim.x / kWave); ++k) { G += s_tot[0][k]; H += s_tot[1][k]; }
-      int64_t* cell = gh + (int64_t)d.F * kMaxBins * 2;
-      atomicAdd(reinterpret_cast<unsigned long long*>(cell), (unsigned long long)G);
-      atomicAdd(reinterpret_cast<unsigned long long*>(cell + 1), (unsigned long long)H);
+      d.slab_tot[2 * item] = G;
+      d.slab_tot[2 * item + 1] = H;
     }
+  }
+}
+
+// Reduce the per-item slabs into the level's histogram slots: thread = one (feature, bin) cell
+// (cell == F*256 is the node-total cell), block.x = a run of kRedItems consecutive items; one int64
+// global atomic per non-zero cell per (run, slot) -- coalesced, 30-100x fewer than per-block flushes.
+constexpr int kRedItems = 16;
+
+__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity) {
+  const int n_items = d.counters[0];
+  const int i0 = blockIdx.x * kRedItems;
+  if (i0 >= n_items) return;
+  const int i1 = min(n_items, i0 + kRedItems);
+  const int ncell = d.F * kMaxBins;
+  const int cell = blockIdx.y * blockDim.x + threadIdx.x;
+  if (cell > ncell) return;
+  const bool tot = cell == ncell;
+  int cur = -1;
+  int64_t g = 0, h = 0;
+  for (int i = i0; i < i1; ++i) {
+    const int slot = d.items_h[i].slot;
+    if (slot != cur) {
+      if (cur >= 0 && (g | h)) {
+        int64_t* dst = d.hist_b[parity] + (int64_t)cur * d.slot_elems + (int64_t)cell * 2;
+        atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)g);
+        atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)h);
+      }
+      cur = slot;
+      g = h = 0;
+    }
+    if (tot) {
+      g += d.slab_tot[2 * i];
+      h += d.slab_tot[2 * i + 1];
+    } else {
+      const uint64_t v = d.slab[(int64_t)i * ncell + cell];
+      g += (int64_t)(int32_t)(uint32_t)(v >> 32);
+      h += (int64_t)(uint32_t)v;
+    }
+  }
+  if (cur >= 0 && (g | h)) {
+    int64_t* dst = d.hist_b[parity] + (int64_t)cur * d.slot_elems + (int64_t)cell * 2;
+    atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)g);
+    atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)h);
   }
 }
 
@@ -361,12 +597,12 @@ __device__ __forceinline__ double calc_weight(double g, double h, double lambda_
   return -t / (h + lambda_);
 }
 
-__global__ __launch_bounds__(256) void k_eval(GbdtDev d, int level, int parity, int tree) {
+__global__ __launch_bounds__(512) void k_eval(GbdtDev d, int level, int parity, int tree) {
   const int pos = blockIdx.x;
   const int n = (1 << level) - 1 + pos;
   Node* nodes = d.nodes;
   if (nodes[n].status != kActive) return;
-  __shared__ Cand s_best[4];
+  __shared__ Cand s_best[8];
   __shared__ int64_t s_GH[2];
 
   const int pair = level == 0 ? 0 : (pos >> 1);
@@ -514,81 +750,146 @@ __global__ __launch_bounds__(256) void k_eval(GbdtDev d, int level, int parity, 
 // ------------------------------------------------------------------------------------------
 // Partition planning + row partition (K18) + leaf margin update (K19)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_plan_part(GbdtDev d, int level) {
-  __shared__ int32_t s_chunks[1024];
-  __shared__ int32_t s_off[1025];
+__global__ __launch_bounds__(256) void k_plan_part(GbdtDev d, int level, int chunk) {
+  __shared__ int32_t s_off[1024];
+  __shared__ int32_t s_node[1024];
+  __shared__ int32_t s_wave[8];
   const int first = (1 << level) - 1, nlev = 1 << level;
+  // children row counts are (re)written by the partition; nodes without local rows stay 0
+  for (int i = threadIdx.x; i < 2 * nlev && level < d.max_depth; i += blockDim.x) d.child_cnt[2 * first + 1 + i] = 0;
   for (int i = threadIdx.x; i < nlev; i += blockDim.x) {
     const Node& nd = d.nodes[first + i];
-    const bool live = (nd.status == kSplit || nd.status == kLeaf) && nd.count > 0;
-    s_chunks[i] = live ? (nd.count + d.chunk - 1) / d.chunk : 0;
+    const bool live = nd.status == kSplit && nd.count > 0;
+    s_off[i] = live ? (nd.count + chunk - 1) / chunk : 0;
+    s_node[i] = first + i;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int i = 0; i < nlev; ++i) { s_off[i] = acc; acc += s_chunks[i]; }
-    d.counters[1] = acc;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nlev; i += blockDim.x) {
-    const Node& nd = d.nodes[first + i];
-    for (int c = 0; c < s_chunks[i]; ++c) {
-      WorkItem w;
-      w.node = first + i;
-      w.slot = 0;
-      w.begin = nd.start + c * d.chunk;
-      w.end = min(nd.start + nd.count, w.begin + d.chunk);
-      d.items_p[s_off[i] + c] = w;
-    }
-  }
+  const int total = block_excl_scan_1024(s_off, nlev, s_wave);
+  if (threadIdx.x == 0) d.counters[1] = total;
+  emit_items(d.items_p, total, s_off, nlev, s_node, d.nodes, chunk, false);
 }
 
-__global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity) {
-  __shared__ int32_t s_cnt[2][4];
-  __shared__ int32_t s_base[2];
+// Stable, atomic-free row partition of the split nodes of a level (K18), two launches:
+//  k_part_count  : per work item, number of rows going left  -> item_left[item]
+//  k_part_scatter: per work item, base offsets = sums of the preceding items of the same node
+//                  (items of a node are contiguous and in row order), then ballot-rank scatter.
+// Left rows keep their relative order, right rows too, so every node's row list stays sorted by
+// row id (ridx starts as the identity each tree) -> histogram gathers walk memory monotonically.
+constexpr int kPartU = 4;      // rows per lane per step (memory-level parallelism)
+constexpr int kPartWaves = 4;  // partition blocks are 256 threads; each wave owns a sub-range
+
+__device__ __forceinline__ bool goes_left(const uint8_t* col, int r, int j, bool dl) {
+  const int b = col[r];
+  return (b == kMissingBin) ? dl : (b <= j);
+}
+
+// Contiguous, 64-aligned sub-range [wb, we) of work item w owned by wave `wv`.
+__device__ __forceinline__ void wave_range(const WorkItem& w, int wv, int& wb, int& we) {
+  const int len = w.end - w.begin;
+  const int per = ((len + kPartWaves - 1) / kPartWaves + kWave - 1) / kWave * kWave;
+  wb = min(w.end, w.begin + wv * per);
+  we = min(w.end, wb + per);
+}
+
+__global__ __launch_bounds__(256) void k_part_count(GbdtDev d, int parity) {
   const int item = blockIdx.x;
   if (item >= d.counters[1]) return;
   const WorkItem w = d.items_p[item];
   const Node nd = d.nodes[w.node];
   const int32_t* cur = d.ridx[parity];
-  if (nd.status == kLeaf) {
-    const float v = nd.leaf_value;
-    for (int i = w.begin + threadIdx.x; i < w.end; i += blockDim.x) d.margin[cur[i]] += v;
-    return;
+  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.n;
+  const int j = nd.bin;
+  const bool dl = nd.default_left != 0;
+  const int lane = lane_id();
+  int wb, we;
+  wave_range(w, wave_id(), wb, we);
+  int nl = 0;
+  for (int i0 = wb; i0 < we; i0 += kWave * kPartU) {
+    int r[kPartU];
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int i = i0 + u * kWave + lane;
+      r[u] = i < we ? cur[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) nl += __popcll(__ballot(r[u] >= 0 && goes_left(col, r[u], j, dl)));
   }
+  if (lane == 0) d.item_left[item * kPartWaves + wave_id()] = nl;
+}
+
+__global__ __launch_bounds__(256) void k_part_scatter(GbdtDev d, int parity, int64_t zero_next, int chunk) {
+  __shared__ int32_t s_red[2][kPartWaves];
+  __shared__ int32_t s_base[2];
+  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
+  {
+    int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
+    const int64_t nz = zero_next / 2;  // int64 pairs per int4
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
+      zp[e] = make_int4(0, 0, 0, 0);
+  }
+  const int item = blockIdx.x;
+  if (item >= d.counters[1]) return;
+  const WorkItem w = d.items_p[item];
+  const Node nd = d.nodes[w.node];
+  const int c = (w.begin - nd.start) / chunk;
+  const int first = item - c;
+  const int nitems = (nd.count + chunk - 1) / chunk;
+  // left rows of the node's preceding items, and of the whole node
+  int before = 0, all = 0;
+  const int32_t* il = d.item_left + first * kPartWaves;
+  for (int k = threadIdx.x; k < nitems * kPartWaves; k += blockDim.x) {
+    const int v = il[k];
+    all += v;
+    if (k < c * kPartWaves) before += v;
+  }
+  before = wave_sum(before);
+  all = wave_sum(all);
+  if (lane_id() == 0) { s_red[0][wave_id()] = before; s_red[1][wave_id()] = all; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int b = 0, a = 0;
+    for (int k = 0; k < kPartWaves; ++k) { b += s_red[0][k]; a += s_red[1][k]; }
+    s_base[0] = b;
+    s_base[1] = a;
+    if (c == 0) {
+      d.cursors[2 * w.node] = a;  // local left child size, read by the next k_plan_hist
+      d.child_cnt[2 * w.node + 1] = a;              // local child row counts; all-reduced under
+      d.child_cnt[2 * w.node + 2] = nd.count - a;   // data parallelism before k_plan_hist
+    }
+  }
+  __syncthreads();
+  const int wv = wave_id(), lane = lane_id();
+  int wb, we;
+  wave_range(w, wv, wb, we);
+  int bl = s_base[0];
+  for (int k = 0; k < wv; ++k) bl += d.item_left[item * kPartWaves + k];
+  int br = (wb - nd.start) - bl;  // rows before this wave's range that went right
+  const int rbase = nd.start + s_base[1];
+  const int32_t* cur = d.ridx[parity];
   int32_t* nxt = d.ridx[parity ^ 1];
   const uint8_t* col = d.binsT + (int64_t)nd.feat * d.n;
   const int j = nd.bin;
   const bool dl = nd.default_left != 0;
-  const int wv = wave_id(), nw = blockDim.x / kWave;
-  int32_t* cursor = d.cursors + 2 * w.node;
-  for (int base = w.begin; base < w.end; base += blockDim.x) {
-    const int i = base + threadIdx.x;
-    const bool valid = i < w.end;
-    int r = 0;
-    bool left = false;
-    if (valid) {
-      r = cur[i];
-      const int b = col[r];
-      left = (b == kMissingBin) ? dl : (b <= j);
+  for (int i0 = wb; i0 < we; i0 += kWave * kPartU) {
+    int r[kPartU];
+    bool lf[kPartU];
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int i = i0 + u * kWave + lane;
+      r[u] = i < we ? cur[i] : -1;
     }
-    const bool right = valid && !left;
-    const uint64_t lm = __ballot(left), rm = __ballot(right);
-    const int lo = mask_rank(lm), ro = mask_rank(rm);
-    if (lane_id() == 0) { s_cnt[0][wv] = __popcll(lm); s_cnt[1][wv] = __popcll(rm); }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int tl = 0, tr = 0;
-      for (int k = 0; k < nw; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
-      s_base[0] = tl ? atomicAdd(cursor, tl) : 0;
-      s_base[1] = tr ? atomicAdd(cursor + 1, tr) : 0;
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) lf[u] = r[u] >= 0 && goes_left(col, r[u], j, dl);
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const uint64_t lm = __ballot(lf[u]), rm = __ballot(r[u] >= 0 && !lf[u]);
+      if (r[u] >= 0) {
+        if (lf[u]) nxt[nd.start + bl + mask_rank(lm)] = r[u];
+        else nxt[rbase + br + mask_rank(rm)] = r[u];
+      }
+      bl += __popcll(lm);
+      br += __popcll(rm);
     }
-    __syncthreads();
-    int wl = 0, wr = 0;
-    for (int k = 0; k < wv; ++k) { wl += s_cnt[0][k]; wr += s_cnt[1][k]; }
-    if (left) nxt[nd.start + s_base[0] + wl + lo] = r;
-    if (right) nxt[nd.start + nd.count - 1 - (s_base[1] + wr + ro)] = r;
-    __syncthreads();
   }
 }
 
@@ -599,39 +900,58 @@ __global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity) {
 extern "C" int cobalt_comm_allreduce_sum_i64(void* comm, int64_t* buf, int64_t count, hipStream_t stream);
 
 struct GbdtCtx {
-  GbdtConfig cfg;
-  GbdtDev d;
-  int max_nodes, pairs_max, items_cap;
-  size_t lds_hist;
-  void* alloc_list[16];
-  int n_alloc;
+  GbdtConfig cfg{};
+  GbdtDev d{};
+  int max_nodes = 0, pairs_max = 0, items_cap = 0;
+  size_t lds_hist = 0;
+  int applied = 0;         // number of leading trees whose leaves are already in the margins
+  int grown = 0;            // number of trees grown so far
+  std::vector<void*> allocs;
 };
+
+static int pow2_clamp(int64_t v, int lo, int hi) {
+  int c = lo;
+  while (c < v && c < hi) c *= 2;
+  return c;
+}
+// Work-item sizes: the root level uses the configured chunk (~768 items of 512 threads); deeper
+// levels histogram at most ~N/2 rows -> aim for ~1536 items; partition items cover all split rows.
+static int chunk_hist(const GbdtDev& d, int level) {
+  return level == 0 ? d.chunk : pow2_clamp((d.n / 2 + 1535) / 1536, 1024, 16384);
+}
+static int chunk_part(const GbdtDev& d) { return pow2_clamp((d.n + 1535) / 1536, 1024, 16384); }
 
 static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
   CK(hipMalloc(p, bytes < 16 ? 16 : bytes));
-  c->alloc_list[c->n_alloc++] = *p;
+  c->allocs.push_back(*p);
   return 0;
 }
 
 COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if (cfg->max_depth < 1 || cfg->max_depth > 10) return -1;
   if (cfg->chunk < 64 || cfg->chunk > 16384) return -2;
-  if (cfg->row_stride % 4 != 0 || cfg->row_stride < cfg->n_feat) return -3;
+  if (cfg->row_stride % 16 != 0 || cfg->row_stride < ((cfg->n_feat + 7) / 8) * 8 + 8) return -3;
   if (cfg->feat_tile % 4 != 0 || cfg->feat_tile <= 0 || cfg->feat_tile > 64) return -4;
   if (cfg->n_rows >= (int64_t)INT32_MAX) return -5;
   GbdtCtx* c = new GbdtCtx();
-  memset(c, 0, sizeof(GbdtCtx));
   c->cfg = *cfg;
   const int F = cfg->n_feat;
   const int64_t N = cfg->n_rows;
   c->max_nodes = (1 << (cfg->max_depth + 1)) - 1;
   c->pairs_max = 1 << (cfg->max_depth - 1);
-  c->items_cap = ceil_div(N, cfg->chunk) + (1 << cfg->max_depth) + 8;
+  {
+    GbdtDev tmp{};
+    tmp.n = N;
+    tmp.chunk = cfg->chunk;
+    const int ch = std::min(chunk_hist(tmp, 0), chunk_hist(tmp, 1));
+    c->items_cap = std::max(ceil_div(N, ch), ceil_div(N, chunk_part(tmp))) + (1 << cfg->max_depth) + 8;
+  }
   GbdtDev& d = c->d;
   d.n = N;
   d.row_offset = cfg->row_offset;
   d.F = F;
   d.stride = cfg->row_stride;
+  d.goff = ((F + 7) / 8) * 8;
   d.max_depth = cfg->max_depth;
   d.max_nodes = c->max_nodes;
   d.chunk = cfg->chunk;
@@ -648,10 +968,10 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.ginv = 1.0 / cfg->gscale;
   d.hinv = 1.0 / cfg->hscale;
   d.seed = cfg->seed;
+  d.ablate = getenv("COBALT_HIST_ABLATE") ? atoi(getenv("COBALT_HIST_ABLATE")) : 0;
   c->lds_hist = (size_t)cfg->feat_tile * kMaxBins * sizeof(uint64_t);
   int rc = 0;
   const size_t hist_bytes = (size_t)c->pairs_max * d.slot_elems * sizeof(int64_t);
-  if ((rc = dev_alloc(c, (void**)&d.gpair, N * sizeof(uint64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.ridx[0], N * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.ridx[1], N * sizeof(int32_t)))) return rc;
   for (int k = 0; k < 2; ++k) {
@@ -664,14 +984,18 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.items_p, c->items_cap * sizeof(WorkItem)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.counters, 16 * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
-  if (c->lds_hist > 64 * 1024) {
-    CK(hipFuncSetAttribute((const void*)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
-  }
+  if ((rc = dev_alloc(c, (void**)&d.child_cnt, c->max_nodes * sizeof(int64_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.item_left, (size_t)c->items_cap * kPartWaves * sizeof(int32_t)))) return rc;
+  const int ntiles = ceil_div(F, cfg->feat_tile);
+  if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.tile_entries, ntiles * sizeof(int32_t)))) return rc;
   *out = c;
   return 0;
 }
 
-COBALT_API int cobalt_gbdt_set_data(void* h, const uint8_t* bins, const uint8_t* binsT, const float* cuts,
+COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT, const float* cuts,
                                     const int32_t* nbins, const float* label, const float* weight,
                                     float* margin, const uint8_t* fmask) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
@@ -683,6 +1007,31 @@ COBALT_API int cobalt_gbdt_set_data(void* h, const uint8_t* bins, const uint8_t*
   c->d.weight = weight;
   c->d.margin = margin;
   c->d.fmask = fmask;
+  // Histogram LDS layout from the per-feature bin counts (one small synchronous copy per fit).
+  const int F = c->d.F, ft = c->d.feat_tile, ntiles = ceil_div(F, ft);
+  std::vector<int32_t> nb(F);
+  CK(hipMemcpy(nb.data(), nbins, F * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::vector<int2> lay(F);
+  std::vector<int32_t> ent(ntiles, 0);
+  int max_ent = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    int off = 0;
+    for (int f = t * ft; f < std::min(F, (t + 1) * ft); ++f) {
+      const int b = std::max(1, std::min(255, nb[f]));
+      int sh = 0;
+      while (sh < 6 && (b << (sh + 1)) <= kMaxBins) ++sh;  // copies = 2^sh, nb * copies <= 256
+      lay[f] = make_int2((f - t * ft) * kMaxBins, sh);
+      off += kMaxBins;
+    }
+    ent[t] = off;
+    max_ent = std::max(max_ent, off);
+  }
+  CK(hipMemcpy(c->d.layout, lay.data(), F * sizeof(int2), hipMemcpyHostToDevice));
+  CK(hipMemcpy(c->d.tile_entries, ent.data(), ntiles * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t);
+  if (c->lds_hist > 64 * 1024) {
+    CK(hipFuncSetAttribute((const void*)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
+  }
   return 0;
 }
 
@@ -693,34 +1042,56 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
   const int D = d.max_depth;
   const int grad_grid = std::min(ceil_div(d.n, 256), 256 * 16);
   const int ftiles = ceil_div(d.F, d.feat_tile);
+  const size_t tree_lds = (size_t)c->max_nodes * 8;
+  if (t0 != c->grown) return -11;  // trees must be grown in order
   for (int t = t0; t < t0 + n_trees; ++t) {
     if (t >= c->cfg.max_trees) return -10;
     hipLaunchKernelGGL(k_init_tree, dim3(1), dim3(256), 0, stream, d);
-    hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), 0, stream, d, t);
+    const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
+    hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
+    if (apply >= 0) c->applied = t;
     CK_LAUNCH();
     for (int level = 0; level <= D; ++level) {
       const int parity = level & 1;
-      hipLaunchKernelGGL(k_plan_hist, dim3(1), dim3(256), 0, stream, d, level);
+      if (level > 0 && c->cfg.comm && c->cfg.world_size > 1) {
+        const int first = (1 << level) - 1;
+        int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.child_cnt + first, (int64_t)1 << level, stream);
+        if (rc) return rc;
+      }
+      hipLaunchKernelGGL(k_plan_hist, dim3(1), dim3(256), 0, stream, d, level, chunk_hist(d, level));
       if (level < D) {
         const int slots = level == 0 ? 1 : (1 << (level - 1));
-        const size_t hbytes = (size_t)slots * d.slot_elems * sizeof(int64_t);
-        CK(hipMemsetAsync(d.hist_b[parity], 0, hbytes, stream));
-        const int ub = ceil_div(d.n, d.chunk) + (1 << level);
-        hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(256), c->lds_hist, stream, d, parity, t);
+        const int chh = chunk_hist(d, level);
+        const int ub = ceil_div(d.n, chh) + (1 << level);
+        hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(512), c->lds_hist, stream, d, parity, t);
+        hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.F * kMaxBins + 1, 256)),
+                           dim3(256), 0, stream, d, parity);
         CK_LAUNCH();
         if (c->cfg.comm && c->cfg.world_size > 1) {
           int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
           if (rc) return rc;
         }
       }
-      hipLaunchKernelGGL(k_eval, dim3(1 << level), dim3(256), 0, stream, d, level, parity, t);
-      hipLaunchKernelGGL(k_plan_part, dim3(1), dim3(256), 0, stream, d, level);
-      const int ubp = ceil_div(d.n, d.chunk) + (1 << level);
-      hipLaunchKernelGGL(k_partition, dim3(ubp), dim3(256), 0, stream, d, parity);
+      hipLaunchKernelGGL(k_eval, dim3(1 << level), dim3(512), 0, stream, d, level, parity, t);
+      if (level < D) {
+        const int chp = chunk_part(d);
+        hipLaunchKernelGGL(k_plan_part, dim3(1), dim3(256), 0, stream, d, level, chp);
+        const int ubp = ceil_div(d.n, chp) + (1 << level);
+        hipLaunchKernelGGL(k_part_count, dim3(ubp), dim3(256), 0, stream, d, parity);
+        const int64_t zero_next = level + 1 < D ? (int64_t)(1 << level) * d.slot_elems : 0;
+        hipLaunchKernelGGL(k_part_scatter, dim3(ubp), dim3(256), 0, stream, d, parity, zero_next, chp);
+      }
       CK_LAUNCH();
     }
     CK(hipMemcpyAsync(d.trees + (size_t)t * c->max_nodes, d.nodes, c->max_nodes * sizeof(Node),
                       hipMemcpyDeviceToDevice, stream));
+    c->grown = t + 1;
+  }
+  // bring the margins up to date with the last grown tree
+  if (c->applied < c->grown) {
+    hipLaunchKernelGGL(k_apply_tree, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, c->grown - 1);
+    CK_LAUNCH();
+    c->applied = c->grown;
   }
   return 0;
 }
@@ -739,7 +1110,7 @@ COBALT_API int cobalt_gbdt_max_nodes(void* h) { return static_cast<GbdtCtx*>(h)-
 COBALT_API int cobalt_gbdt_destroy(void* h) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   if (!c) return 0;
-  for (int i = 0; i < c->n_alloc; ++i) (void)hipFree(c->alloc_list[i]);
+  for (void* p : c->allocs) (void)hipFree(p);
   delete c;
   return 0;
 }

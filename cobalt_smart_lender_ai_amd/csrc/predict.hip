@@ -82,10 +82,10 @@ COBALT_API int cobalt_predict(const float* X, int64_t n, int F, int64_t ldx, con
   const int block = 256;
   const size_t lds = kTileNodes * sizeof(uint2) + (size_t)block * (F | 1) * sizeof(float);
   if (lds > 160 * 1024) return -3;
-  static bool attr_set = false;
-  if (!attr_set) {
-    CK(hipFuncSetAttribute((const void*)k_predict, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
+  static size_t attr_set = 64 * 1024;
+  if (lds > attr_set) {
+    CK(hipFuncSetAttribute((const void*)k_predict, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_set = lds;
   }
   const int grid = ceil_div(n, block);
   hipLaunchKernelGGL(k_predict, dim3(grid), dim3(block), lds, stream, X, n, F, ldx,

@@ -45,14 +45,17 @@ assert ctypes.sizeof(GbdtConfig) == 128
 
 
 def row_stride(n_feat: int) -> int:
-    return (n_feat + 3) // 4 * 4
+    """Bytes per row record: bins padded to 8 bytes, then the packed (g, h) u64; 16-byte aligned so a
+    record is one aligned 32-byte piece of a memory sector for the 20-feature model."""
+    return ((n_feat + 7) // 8 * 8 + 8 + 15) // 16 * 16
 
 
 def pick_chunk(n_rows: int) -> int:
-    """Rows per histogram/partition work item: aim for >= 2048 root items (8 per CU), pow2 in
-    [512, 16384] (16384 keeps per-block packed sums below 2^30)."""
-    target = max(1, n_rows // 2048)
-    c = 512
+    """Rows per histogram/partition work item: ~768 root items (3 resident 512-thread blocks per CU,
+    so the root level runs in one wave of blocks), power of two in [1024, 16384] (16384 keeps the
+    per-block packed sums below 2^30)."""
+    target = max(1, -(-n_rows // 768))
+    c = 1024
     while c < target and c < 16384:
         c *= 2
     return c
@@ -64,13 +67,14 @@ def pick_feat_tile(n_feat: int) -> int:
 
 
 def bin_matrix(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-    """Quantise ``X`` [N, F] float32 (CUDA) -> (bins [N, stride] uint8, binsT [F, N] uint8)."""
+    """Quantise ``X`` [N, F] float32 (CUDA) -> (row records [N, stride] uint8 with the bins in the
+    first F bytes, binsT [F, N] uint8)."""
     if X.device.type != "cuda":
         raise ValueError("bin_matrix expects a CUDA tensor")
     X = X.contiguous()
     N, F = X.shape
     st = row_stride(F)
-    bins = torch.empty((N, st), dtype=torch.uint8, device=X.device)
+    bins = torch.zeros((N, st), dtype=torch.uint8, device=X.device)
     binsT = torch.empty((F, N), dtype=torch.uint8, device=X.device)
     lib = _native.lib()
     rc = lib.cobalt_bin_matrix(X.data_ptr(), N, F, F, cuts.contiguous().data_ptr(),
