@@ -116,7 +116,7 @@ struct GbdtDev {
   int32_t* item_left;     // [items] left-row count per partition work item
   int2* layout;           // [F] histogram LDS layout: x = cell offset within tile, y = log2(copies)
   int32_t* tile_entries;  // [n_tiles] LDS cells per feature tile
-  int64_t* child_cnt;     // [max_nodes] row counts of the current level's nodes (global under DP)
+  int32_t* child_cnt;     // [2*max_nodes] all-reduced copy of the partition cursors (DP only)
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush
@@ -227,7 +227,8 @@ __device__ __forceinline__ float tree_leaf(const GbdtDev& d, int64_t r, const ui
 // Gradient kernel. When `apply_tree >= 0` it first adds that tree's leaf value to every row's margin
 // (the prediction-cache update, done as a coalesced traversal over row-major bins instead of a
 // scatter over the leaves' row lists), then computes binary:logistic g/h in fp64, applies row
-// subsampling, quantises and packs them. Also resets ridx to the identity for the root.
+// subsampling, quantises and packs them into the row record (the root level reads rows in
+// identity order, so ridx needs no reset).
 __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tree) {
   extern __shared__ uint32_t s_tree[];
   {  // zero the root histogram slot
@@ -243,16 +244,37 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
     __syncthreads();
   }
   const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
+  const bool rec32 = d.stride == 32 && d.F <= 24;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    d.ridx[0][i] = (int32_t)i;
     float mf = d.margin[i];
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = make_uint4(0, 0, 0, 0);
+    uint4* rec = reinterpret_cast<uint4*>(d.bins + i * 32);
+    if (rec32) {
+      ra = rec[0];
+      rb = rec[1];
+    }
     if (apply_tree >= 0) {
-      mf += tree_leaf(d, i, s_meta, s_leaf);
+      if (rec32) {
+        // walk the previous tree with the record held in registers
+        int n = 0;
+        uint32_t m = s_meta[0];
+        while (m & (1u << 25)) {
+          const int f = m & 0xFFFF, q = f >> 2;
+          const uint32_t word = q == 0 ? ra.x : q == 1 ? ra.y : q == 2 ? ra.z : q == 3 ? ra.w : q == 4 ? rb.x : rb.y;
+          const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
+          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          n = 2 * n + (left ? 1 : 2);
+          m = s_meta[n];
+        }
+        mf += s_leaf[n];
+      } else {
+        mf += tree_leaf(d, i, s_meta, s_leaf);
+      }
       d.margin[i] = mf;
     }
-    const double m = (double)mf;
-    const double p = 1.0 / (1.0 + exp(-m));
+    const double mm = (double)mf;
+    const double p = 1.0 / (1.0 + exp(-mm));
     const double y = (double)d.label[i];
     const double w = (double)d.weight[i];
     double g = (p - y) * w;
@@ -265,8 +287,14 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
     int64_t hq = (int64_t)rint(h * d.hscale);
     gq = gq > 65536 ? 65536 : (gq < -65536 ? -65536 : gq);
     hq = hq > 65536 ? 65536 : (hq < 0 ? 0 : hq);
-    *reinterpret_cast<uint64_t*>(d.bins + i * d.stride + d.goff) =
-        ((uint64_t)(uint32_t)(int32_t)gq << 32) | (uint64_t)(uint32_t)hq;
+    if (rec32) {
+      rb.z = (uint32_t)hq;
+      rb.w = (uint32_t)(int32_t)gq;
+      rec[1] = rb;
+    } else {
+      *reinterpret_cast<uint64_t*>(d.bins + i * d.stride + d.goff) =
+          ((uint64_t)(uint32_t)(int32_t)gq << 32) | (uint64_t)(uint32_t)hq;
+    }
   }
 }
 
@@ -337,7 +365,7 @@ __device__ void emit_items(WorkItem* out, int total, const int32_t* s_off, int n
   }
 }
 
-__global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level, int chunk) {
+__global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level, int chunk, const int32_t* cnt_src) {
   __shared__ int32_t s_off[1024];
   __shared__ int32_t s_node[1024];
   __shared__ int32_t s_wave[8];
@@ -357,7 +385,7 @@ __global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level, int chu
         d.nodes[R].start = par.start + lc;
         d.nodes[R].count = par.count - lc;
         // histogram the child with fewer (global) rows; the sibling comes by exact subtraction
-        const bool left_small = d.child_cnt[L] <= d.child_cnt[R];
+        const bool left_small = cnt_src[2 * q] <= cnt_src[2 * q + 1];
         d.nodes[L].build = left_small ? 1 : 0;
         d.nodes[R].build = left_small ? 0 : 1;
         built = left_small ? L : R;
@@ -597,12 +625,12 @@ __device__ __forceinline__ double calc_weight(double g, double h, double lambda_
   return -t / (h + lambda_);
 }
 
-__global__ __launch_bounds__(512) void k_eval(GbdtDev d, int level, int parity, int tree) {
+__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree) {
   const int pos = blockIdx.x;
   const int n = (1 << level) - 1 + pos;
   Node* nodes = d.nodes;
   if (nodes[n].status != kActive) return;
-  __shared__ Cand s_best[8];
+  __shared__ Cand s_best[16];
   __shared__ int64_t s_GH[2];
 
   const int pair = level == 0 ? 0 : (pos >> 1);
@@ -755,8 +783,6 @@ __global__ __launch_bounds__(256) void k_plan_part(GbdtDev d, int level, int chu
   __shared__ int32_t s_node[1024];
   __shared__ int32_t s_wave[8];
   const int first = (1 << level) - 1, nlev = 1 << level;
-  // children row counts are (re)written by the partition; nodes without local rows stay 0
-  for (int i = threadIdx.x; i < 2 * nlev && level < d.max_depth; i += blockDim.x) d.child_cnt[2 * first + 1 + i] = 0;
   for (int i = threadIdx.x; i < nlev; i += blockDim.x) {
     const Node& nd = d.nodes[first + i];
     const bool live = nd.status == kSplit && nd.count > 0;
@@ -769,61 +795,27 @@ __global__ __launch_bounds__(256) void k_plan_part(GbdtDev d, int level, int chu
   emit_items(d.items_p, total, s_off, nlev, s_node, d.nodes, chunk, false);
 }
 
-// Stable, atomic-free row partition of the split nodes of a level (K18), two launches:
-//  k_part_count  : per work item, number of rows going left  -> item_left[item]
-//  k_part_scatter: per work item, base offsets = sums of the preceding items of the same node
-//                  (items of a node are contiguous and in row order), then ballot-rank scatter.
-// Left rows keep their relative order, right rows too, so every node's row list stays sorted by
-// row id (ridx starts as the identity each tree) -> histogram gathers walk memory monotonically.
-constexpr int kPartU = 4;      // rows per lane per step (memory-level parallelism)
-constexpr int kPartWaves = 4;  // partition blocks are 256 threads; each wave owns a sub-range
+// Row partition of the split nodes of a level (K18), one launch. A block takes one work item
+// (<= 8192 rows of one node); each wavefront owns a contiguous quarter and keeps its <= 32 rows per
+// lane in registers: pass 1 loads row ids + split-feature bins and counts, the block claims its
+// left range (from the node start, ascending) and right range (from the node end, descending)
+// with one atomic pair per item, pass 2 scatters with ballot ranks -- rows are read once.
+// Left rows keep their relative order inside an item; only whole items interleave, so a node's
+// row list stays sorted in 8192-row runs (the root level reads rows in identity order).
+constexpr int kPartWaves = 4;   // 256-thread blocks
+constexpr int kPartSteps = 32;  // 64-row steps per wave -> chunk_part <= 4 * 32 * 64 = 8192
 
 __device__ __forceinline__ bool goes_left(const uint8_t* col, int r, int j, bool dl) {
   const int b = col[r];
   return (b == kMissingBin) ? dl : (b <= j);
 }
 
-// Contiguous, 64-aligned sub-range [wb, we) of work item w owned by wave `wv`.
-__device__ __forceinline__ void wave_range(const WorkItem& w, int wv, int& wb, int& we) {
-  const int len = w.end - w.begin;
-  const int per = ((len + kPartWaves - 1) / kPartWaves + kWave - 1) / kWave * kWave;
-  wb = min(w.end, w.begin + wv * per);
-  we = min(w.end, wb + per);
-}
-
-__global__ __launch_bounds__(256) void k_part_count(GbdtDev d, int parity) {
-  const int item = blockIdx.x;
-  if (item >= d.counters[1]) return;
-  const WorkItem w = d.items_p[item];
-  const Node nd = d.nodes[w.node];
-  const int32_t* cur = d.ridx[parity];
-  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.n;
-  const int j = nd.bin;
-  const bool dl = nd.default_left != 0;
-  const int lane = lane_id();
-  int wb, we;
-  wave_range(w, wave_id(), wb, we);
-  int nl = 0;
-  for (int i0 = wb; i0 < we; i0 += kWave * kPartU) {
-    int r[kPartU];
-#pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
-      const int i = i0 + u * kWave + lane;
-      r[u] = i < we ? cur[i] : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < kPartU; ++u) nl += __popcll(__ballot(r[u] >= 0 && goes_left(col, r[u], j, dl)));
-  }
-  if (lane == 0) d.item_left[item * kPartWaves + wave_id()] = nl;
-}
-
-__global__ __launch_bounds__(256) void k_part_scatter(GbdtDev d, int parity, int64_t zero_next, int chunk) {
-  __shared__ int32_t s_red[2][kPartWaves];
+__global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_t zero_next) {
+  __shared__ int32_t s_cnt[2][kPartWaves];
   __shared__ int32_t s_base[2];
-  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
-  {
+  {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
     int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
-    const int64_t nz = zero_next / 2;  // int64 pairs per int4
+    const int64_t nz = zero_next / 2;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
   }
@@ -831,65 +823,57 @@ __global__ __launch_bounds__(256) void k_part_scatter(GbdtDev d, int parity, int
   if (item >= d.counters[1]) return;
   const WorkItem w = d.items_p[item];
   const Node nd = d.nodes[w.node];
-  const int c = (w.begin - nd.start) / chunk;
-  const int first = item - c;
-  const int nitems = (nd.count + chunk - 1) / chunk;
-  // left rows of the node's preceding items, and of the whole node
-  int before = 0, all = 0;
-  const int32_t* il = d.item_left + first * kPartWaves;
-  for (int k = threadIdx.x; k < nitems * kPartWaves; k += blockDim.x) {
-    const int v = il[k];
-    all += v;
-    if (k < c * kPartWaves) before += v;
-  }
-  before = wave_sum(before);
-  all = wave_sum(all);
-  if (lane_id() == 0) { s_red[0][wave_id()] = before; s_red[1][wave_id()] = all; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int b = 0, a = 0;
-    for (int k = 0; k < kPartWaves; ++k) { b += s_red[0][k]; a += s_red[1][k]; }
-    s_base[0] = b;
-    s_base[1] = a;
-    if (c == 0) {
-      d.cursors[2 * w.node] = a;  // local left child size, read by the next k_plan_hist
-      d.child_cnt[2 * w.node + 1] = a;              // local child row counts; all-reduced under
-      d.child_cnt[2 * w.node + 2] = nd.count - a;   // data parallelism before k_plan_hist
-    }
-  }
-  __syncthreads();
-  const int wv = wave_id(), lane = lane_id();
-  int wb, we;
-  wave_range(w, wv, wb, we);
-  int bl = s_base[0];
-  for (int k = 0; k < wv; ++k) bl += d.item_left[item * kPartWaves + k];
-  int br = (wb - nd.start) - bl;  // rows before this wave's range that went right
-  const int rbase = nd.start + s_base[1];
+  const bool identity = parity == 0 && w.node == 0;
   const int32_t* cur = d.ridx[parity];
   int32_t* nxt = d.ridx[parity ^ 1];
   const uint8_t* col = d.binsT + (int64_t)nd.feat * d.n;
   const int j = nd.bin;
   const bool dl = nd.default_left != 0;
-  for (int i0 = wb; i0 < we; i0 += kWave * kPartU) {
-    int r[kPartU];
-    bool lf[kPartU];
+  const int wv = wave_id(), lane = lane_id();
+  const int len = w.end - w.begin;
+  const int per = ((len + kPartWaves - 1) / kPartWaves + kWave - 1) / kWave * kWave;
+  const int wb = min(w.end, w.begin + wv * per), we = min(w.end, wb + per);
+  int r[kPartSteps];
+  uint32_t lbits = 0, vbits = 0;
+  int nl = 0, nr = 0;
 #pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
-      const int i = i0 + u * kWave + lane;
-      r[u] = i < we ? cur[i] : -1;
+  for (int k = 0; k < kPartSteps; ++k) {
+    const int i = wb + k * kWave + lane;
+    r[k] = i < we ? (identity ? i : cur[i]) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < kPartSteps; ++k) {
+    const bool valid = r[k] >= 0;
+    const bool left = valid && goes_left(col, r[k], j, dl);
+    lbits |= (uint32_t)left << k;
+    vbits |= (uint32_t)valid << k;
+    const uint64_t lm = __ballot(left), vm = __ballot(valid);
+    nl += __popcll(lm);
+    nr += __popcll(vm) - __popcll(lm);
+  }
+  if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nr; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tl = 0, tr = 0;
+    for (int k = 0; k < kPartWaves; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
+    int32_t* cursor = d.cursors + 2 * w.node;
+    s_base[0] = tl ? atomicAdd(cursor, tl) : 0;
+    s_base[1] = tr ? atomicAdd(cursor + 1, tr) : 0;
+  }
+  __syncthreads();
+  int bl = s_base[0], br = s_base[1];
+  for (int k = 0; k < wv; ++k) { bl += s_cnt[0][k]; br += s_cnt[1][k]; }
+  const int rend = nd.start + nd.count - 1;
+#pragma unroll
+  for (int k = 0; k < kPartSteps; ++k) {
+    const bool valid = (vbits >> k) & 1u, left = (lbits >> k) & 1u;
+    const uint64_t lm = __ballot(valid && left), rm = __ballot(valid && !left);
+    if (valid) {
+      if (left) nxt[nd.start + bl + mask_rank(lm)] = r[k];
+      else nxt[rend - (br + mask_rank(rm))] = r[k];
     }
-#pragma unroll
-    for (int u = 0; u < kPartU; ++u) lf[u] = r[u] >= 0 && goes_left(col, r[u], j, dl);
-#pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
-      const uint64_t lm = __ballot(lf[u]), rm = __ballot(r[u] >= 0 && !lf[u]);
-      if (r[u] >= 0) {
-        if (lf[u]) nxt[nd.start + bl + mask_rank(lm)] = r[u];
-        else nxt[rbase + br + mask_rank(rm)] = r[u];
-      }
-      bl += __popcll(lm);
-      br += __popcll(rm);
-    }
+    bl += __popcll(lm);
+    br += __popcll(rm);
   }
 }
 
@@ -898,6 +882,7 @@ __global__ __launch_bounds__(256) void k_part_scatter(GbdtDev d, int parity, int
 // ------------------------------------------------------------------------------------------
 // RCCL all-reduce hook implemented in comm.cpp
 extern "C" int cobalt_comm_allreduce_sum_i64(void* comm, int64_t* buf, int64_t count, hipStream_t stream);
+extern "C" int cobalt_comm_allreduce(void* comm, void* buf, int64_t count, int dtype, int op, hipStream_t stream);
 
 struct GbdtCtx {
   GbdtConfig cfg{};
@@ -919,7 +904,7 @@ static int pow2_clamp(int64_t v, int lo, int hi) {
 static int chunk_hist(const GbdtDev& d, int level) {
   return level == 0 ? d.chunk : pow2_clamp((d.n / 2 + 1535) / 1536, 1024, 16384);
 }
-static int chunk_part(const GbdtDev& d) { return pow2_clamp((d.n + 1535) / 1536, 1024, 16384); }
+static int chunk_part(const GbdtDev& d) { return pow2_clamp((d.n + 1535) / 1536, 1024, 8192); }
 
 static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
   CK(hipMalloc(p, bytes < 16 ? 16 : bytes));
@@ -984,7 +969,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.items_p, c->items_cap * sizeof(WorkItem)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.counters, 16 * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&d.child_cnt, c->max_nodes * sizeof(int64_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.child_cnt, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.item_left, (size_t)c->items_cap * kPartWaves * sizeof(int32_t)))) return rc;
@@ -1053,12 +1038,18 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
     CK_LAUNCH();
     for (int level = 0; level <= D; ++level) {
       const int parity = level & 1;
-      if (level > 0 && c->cfg.comm && c->cfg.world_size > 1) {
-        const int first = (1 << level) - 1;
-        int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.child_cnt + first, (int64_t)1 << level, stream);
+      const int32_t* cnt_src = d.cursors;
+      if (level > 0 && level < D && c->cfg.comm && c->cfg.world_size > 1) {
+        // global child row counts decide which child is histogrammed (identically on every rank)
+        const int pfirst = (1 << (level - 1)) - 1, np = 1 << (level - 1);
+        CK(hipMemcpyAsync(d.child_cnt + 2 * pfirst, d.cursors + 2 * pfirst, 2 * np * sizeof(int32_t),
+                          hipMemcpyDeviceToDevice, stream));
+        int rc = cobalt_comm_allreduce(c->cfg.comm, d.child_cnt + 2 * pfirst, 2 * np, 2 /*int32*/, 0 /*sum*/, stream);
         if (rc) return rc;
+        cnt_src = d.child_cnt;
       }
-      hipLaunchKernelGGL(k_plan_hist, dim3(1), dim3(256), 0, stream, d, level, chunk_hist(d, level));
+      if (level < D)
+        hipLaunchKernelGGL(k_plan_hist, dim3(1), dim3(256), 0, stream, d, level, chunk_hist(d, level), cnt_src);
       if (level < D) {
         const int slots = level == 0 ? 1 : (1 << (level - 1));
         const int chh = chunk_hist(d, level);
@@ -1072,14 +1063,13 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
           if (rc) return rc;
         }
       }
-      hipLaunchKernelGGL(k_eval, dim3(1 << level), dim3(512), 0, stream, d, level, parity, t);
-      if (level < D) {
+      hipLaunchKernelGGL(k_eval, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t);
+      if (level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         hipLaunchKernelGGL(k_plan_part, dim3(1), dim3(256), 0, stream, d, level, chp);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
-        hipLaunchKernelGGL(k_part_count, dim3(ubp), dim3(256), 0, stream, d, parity);
-        const int64_t zero_next = level + 1 < D ? (int64_t)(1 << level) * d.slot_elems : 0;
-        hipLaunchKernelGGL(k_part_scatter, dim3(ubp), dim3(256), 0, stream, d, parity, zero_next, chp);
+        const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;
+        hipLaunchKernelGGL(k_partition, dim3(ubp), dim3(256), 0, stream, d, parity, zero_next);
       }
       CK_LAUNCH();
     }
