@@ -1,0 +1,113 @@
+"""Command-line entry point: ``python -m cobalt_smart_lender_ai_amd <command>``.
+
+Commands mirror the reference's scripts:
+
+  synth     write a synthetic LendingClub-shaped raw CSV into the store (offline stand-in for the
+            Kaggle download, reference README "Data" section)
+  clean     stage 1 (clean_data.py; ``--full`` = ``python clean_data.py full``)
+  features  stage 2 (feature_engineering.py)
+  train     tree model training (model_tree_train_test.py)
+  serve     FastAPI scoring service (cobalt_fast_api.py, uvicorn)
+
+The artifact store is ``--store`` or ``$COBALT_ARTIFACT_URI`` (a local directory or ``s3://bucket``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import sys
+
+
+def _store(args):
+    from .dataio.artifacts import get_store
+
+    return get_store(args.store)
+
+
+def cmd_synth(args) -> int:
+    from .config import RAW_DATA_KEY_FULL, RAW_DATA_KEY_SAMPLE
+    from .dataio.synth_raw import make_raw_lendingclub
+
+    st = _store(args)
+    df = make_raw_lendingclub(args.rows, seed=args.seed)
+    st.write_csv(df, RAW_DATA_KEY_FULL if args.full else RAW_DATA_KEY_SAMPLE)
+    if args.both:
+        st.write_csv(df, RAW_DATA_KEY_SAMPLE if args.full else RAW_DATA_KEY_FULL)
+    print(f"[INFO] wrote {len(df)} synthetic raw rows")
+    return 0
+
+
+def cmd_clean(args) -> int:
+    from .pipeline.prep_flow import run_clean
+
+    run_clean(_store(args), use_sample=not args.full, device=args.device, preset=args.preset)
+    return 0
+
+
+def cmd_features(args) -> int:
+    from .pipeline.prep_flow import run_features
+
+    run_features(_store(args), device=args.device, reference_date=args.reference_date)
+    return 0
+
+
+def cmd_train(args) -> int:
+    from .config import TrainConfig
+    from .pipeline.train_tree import run_training
+
+    st = _store(args)
+    cfg = TrainConfig(device=args.device)
+    if args.n_iter is not None:
+        cfg.search_n_iter = args.n_iter
+    if args.gpus is not None:
+        cfg.fits_in_parallel = args.gpus
+    df = st.read_csv(cfg.input_key)
+    m = run_training(df, cfg, store=st, local_dir=args.local_dir, device=args.device)
+    print(json.dumps({k: m[k] for k in ("auc", "best_params", "timing_s", "selected_features")}, indent=2))
+    return 0
+
+
+def cmd_serve(args) -> int:
+    import uvicorn
+
+    from .serve.app import create_app
+
+    uvicorn.run(create_app(), host=args.host, port=args.port)
+    return 0
+
+
+def main(argv: list[str] | None = None) -> int:
+    logging.basicConfig(level=logging.INFO, format="[%(levelname)s] %(message)s")
+    p = argparse.ArgumentParser(prog="cobalt_smart_lender_ai_amd")
+    p.add_argument("--store", default=None, help="artifact store (dir or s3://bucket)")
+    p.add_argument("--device", default=None, help="cuda:N or cpu (default: cuda:0 when available)")
+    sub = p.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("synth")
+    s.add_argument("--rows", type=int, default=100_000)
+    s.add_argument("--seed", type=int, default=0)
+    s.add_argument("--full", action="store_true")
+    s.add_argument("--both", action="store_true", help="write the same frame under sample and full keys")
+    s.set_defaults(fn=cmd_synth)
+    s = sub.add_parser("clean")
+    s.add_argument("--full", action="store_true")
+    s.add_argument("--preset", default="script", choices=["script", "notebook"])
+    s.set_defaults(fn=cmd_clean)
+    s = sub.add_parser("features")
+    s.add_argument("--reference-date", default=None)
+    s.set_defaults(fn=cmd_features)
+    s = sub.add_parser("train")
+    s.add_argument("--local-dir", default="models")
+    s.add_argument("--n-iter", type=int, default=None)
+    s.add_argument("--gpus", type=int, default=None)
+    s.set_defaults(fn=cmd_train)
+    s = sub.add_parser("serve")
+    s.add_argument("--host", default="0.0.0.0")
+    s.add_argument("--port", type=int, default=8000)
+    s.set_defaults(fn=cmd_serve)
+    args = p.parse_args(argv)
+    return args.fn(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

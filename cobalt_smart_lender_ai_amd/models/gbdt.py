@@ -110,6 +110,67 @@ def feature_masks(n_trees: int, n_feat: int, colsample: float, seed: int) -> np.
     return m
 
 
+@dataclass
+class BinnedData:
+    """A quantised training matrix: cuts + bins, reusable across fits on the same rows (RFE steps,
+    search candidates). GPU: row records [N, stride] + feature-major bins [F, N]; host: uint8 [N, F]."""
+    device: torch.device
+    n_rows: int
+    n_rows_global: int
+    n_features: int
+    row_offset: int
+    cuts: torch.Tensor
+    nbins: torch.Tensor
+    records: torch.Tensor | None = None
+    binsT: torch.Tensor | None = None
+    bins_host: np.ndarray | None = None
+    t_sketch: float = 0.0
+    t_bin: float = 0.0
+
+
+def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int = 1 << 18, device=None, dist=None,
+                n_rows_global: int | None = None, row_offset: int = 0) -> BinnedData:
+    """Quantile sketch (K12) on a global strided sample + binning (K13)."""
+    dev = _resolve_device(device, X)
+    world = dist.world if dist is not None else 1
+    Xt = _to_tensor(X, dev)
+    N, F = Xt.shape
+    n_glob = n_rows_global if n_rows_global is not None else (
+        int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
+    ts = time.perf_counter()
+    stride = sketch.sample_stride(n_glob, sketch_rows)
+    samp = sketch.local_sample(Xt, row_offset, stride)
+    if world > 1:
+        samp = dist.allgather_rows(samp)
+    cuts, nbins = sketch.compute_cuts(samp, max_bin)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t_sketch = time.perf_counter() - ts
+    tb = time.perf_counter()
+    bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
+    if dev.type == "cuda":
+        from ..ops import gbdt_ops
+
+        bd.records, bd.binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
+        torch.cuda.synchronize(dev)
+    else:
+        bd.bins_host = sketch.bin_matrix_host(Xt.cpu().numpy(), cuts.cpu().numpy(), nbins.cpu().numpy())
+    bd.t_bin = time.perf_counter() - tb
+    return bd
+
+
+def subset_rows(bd: BinnedData, rows: np.ndarray) -> BinnedData:
+    """Rows ``rows`` of a binned matrix with the same cuts (CV folds re-use one binning)."""
+    idx = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=bd.device)
+    out = BinnedData(bd.device, len(rows), len(rows), bd.n_features, 0, bd.cuts, bd.nbins)
+    if bd.records is not None:
+        out.records = bd.records.index_select(0, idx).contiguous()
+        out.binsT = bd.binsT.index_select(1, idx).contiguous()
+    else:
+        out.bins_host = bd.bins_host[np.asarray(rows)]
+    return out
+
+
 def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, device=None,
           feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
           dist=None, n_rows_global: int | None = None, row_offset: int = 0,
@@ -120,16 +181,31 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
         params = GBDTParams()
     elif isinstance(params, dict):
         params = GBDTParams.from_kwargs(**params)
-    dev = _resolve_device(device, X)
-    world = dist.world if dist is not None else 1
     t0 = time.perf_counter()
-    Xt = _to_tensor(X, dev)
+    bd = bin_dataset(X, max_bin=params.max_bin, sketch_rows=params.sketch_rows, device=device, dist=dist,
+                     n_rows_global=n_rows_global, row_offset=row_offset)
+    bst = train_binned(bd, y, params, sample_weight=sample_weight, feature_names=feature_names,
+                       feature_types=feature_types, dist=dist, report=report)
+    if report is not None:
+        report.t_total = time.perf_counter() - t0
+    return bst
+
+
+def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, sample_weight=None,
+                 feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
+                 feature_mask: np.ndarray | None = None, dist=None, report: FitReport | None = None) -> Booster:
+    """Boost on pre-binned data. ``feature_mask`` (bool [F]) restricts the fit to a feature subset
+    (the trees still index the full feature space, so a subset fit costs no re-binning)."""
+    if params is None:
+        params = GBDTParams()
+    elif isinstance(params, dict):
+        params = GBDTParams.from_kwargs(**params)
+    dev = bd.device
+    world = dist.world if dist is not None else 1
+    N, F = bd.n_rows, bd.n_features
     yt = _to_tensor(y, dev).reshape(-1)
-    N, F = Xt.shape
     if yt.shape[0] != N:
         raise ValueError("X and y row counts differ")
-    n_glob = n_rows_global if n_rows_global is not None else (
-        int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
     wt = _to_tensor(sample_weight, dev).reshape(-1) if sample_weight is not None else torch.ones(N, device=dev)
     spw = float(params.scale_pos_weight if params.scale_pos_weight is not None else 1.0)
     wt = wt * torch.where(yt == 1.0, torch.tensor(spw, device=dev), torch.tensor(1.0, device=dev))
@@ -146,40 +222,30 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
     else:
         base_score = float(params.base_score)
     base_score = float(np.float32(base_score))
-    booster_shell = Booster([], base_score=base_score, num_feature=F)
-    base_margin = booster_shell.base_margin
+    base_margin = Booster([], base_score=base_score, num_feature=F).base_margin
 
     wmax = float(wt.max()) if N else 1.0
     if world > 1:
         wmax = dist.allreduce_scalar(wmax, "max", dev)
     gscale, hscale = gbdt_host.quant_scales(wmax)
 
-    # ---- K12 quantile sketch on a global strided sample
-    ts = time.perf_counter()
-    stride = sketch.sample_stride(n_glob, params.sketch_rows)
-    samp = sketch.local_sample(Xt, row_offset, stride)
-    if world > 1:
-        samp = dist.allgather_rows(samp)
-    cuts, nbins = sketch.compute_cuts(samp, params.max_bin)
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-    t_sketch = time.perf_counter() - ts
-
     T = int(params.n_estimators)
     fmask_np = feature_masks(T, F, float(params.colsample_bytree), int(params.random_state))
+    if feature_mask is not None:
+        fm_sub = np.asarray(feature_mask, dtype=bool)
+        active = np.nonzero(fm_sub)[0]
+        fmask_np = np.zeros((T, F), dtype=np.uint8)
+        sub = feature_masks(T, len(active), float(params.colsample_bytree), int(params.random_state))
+        fmask_np[:, active] = sub
     hp = gbdt_host.HostGbdtParams(max_depth=int(params.max_depth), eta=float(params.learning_rate),
                                   reg_lambda=float(params.reg_lambda), reg_alpha=float(params.reg_alpha),
                                   gamma=float(params.gamma), min_child_weight=float(params.min_child_weight),
                                   subsample=float(params.subsample), seed=int(params.random_state),
                                   gscale=gscale, hscale=hscale)
+    tb = time.perf_counter()
     if dev.type == "cuda":
         from ..ops import gbdt_ops
 
-        tb = time.perf_counter()
-        bins, binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
-        torch.cuda.synchronize(dev)
-        t_bin = time.perf_counter() - tb
-        tb = time.perf_counter()
         margin = torch.full((N,), base_margin, dtype=torch.float32, device=dev)
         comm = dist.native_comm if (dist is not None and world > 1) else None
         if world > 1 and comm is None:
@@ -188,21 +254,16 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
                                      reg_lambda=hp.reg_lambda, reg_alpha=hp.reg_alpha, gamma=hp.gamma,
                                      min_child_weight=hp.min_child_weight, subsample=hp.subsample,
                                      gscale=gscale, hscale=hscale, base_margin=base_margin,
-                                     seed=hp.seed, row_offset=row_offset, world_size=world, comm=comm)
+                                     seed=hp.seed, row_offset=bd.row_offset, world_size=world, comm=comm)
         fm = torch.as_tensor(fmask_np, device=dev).contiguous()
-        tr.set_data(bins, binsT, cuts.contiguous(), nbins.to(torch.int32).contiguous(), yt.contiguous(), wt,
-                    margin, fm)
+        tr.set_data(bd.records, bd.binsT, bd.cuts.contiguous(), bd.nbins.to(torch.int32).contiguous(),
+                    yt.contiguous(), wt, margin, fm)
         tr.grow(0, T)
         nodes = tr.fetch(0, T)
         tr.close()
-        t_boost = time.perf_counter() - tb
     else:
-        tb = time.perf_counter()
-        cuts_np = cuts.cpu().numpy()
-        nb_np = nbins.cpu().numpy()
-        bins_np = sketch.bin_matrix_host(Xt.cpu().numpy(), cuts_np, nb_np)
-        t_bin = time.perf_counter() - tb
-        tb = time.perf_counter()
+        cuts_np = bd.cuts.cpu().numpy()
+        nb_np = bd.nbins.cpu().numpy()
         margin_np = np.full(N, np.float32(base_margin), dtype=np.float32)
         y_np = yt.cpu().numpy()
         w_np = wt.cpu().numpy()
@@ -214,12 +275,12 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
                 return t.numpy()
         recs = []
         for t in range(T):
-            gq, hq = gbdt_host.gradients_host(margin_np, y_np, w_np, hp, t, row_offset)
-            recs.append(gbdt_host.grow_tree_host(bins_np, cuts_np, nb_np, gq, hq, margin_np, hp, fmask_np[t],
+            gq, hq = gbdt_host.gradients_host(margin_np, y_np, w_np, hp, t, bd.row_offset)
+            recs.append(gbdt_host.grow_tree_host(bd.bins_host, cuts_np, nb_np, gq, hq, margin_np, hp, fmask_np[t],
                                                  allreduce))
         nodes = np.stack(recs) if recs else np.zeros((0, (1 << (hp.max_depth + 1)) - 1),
                                                       dtype=gbdt_host.NODE_DTYPE)
-        t_boost = time.perf_counter() - tb
+    t_boost = time.perf_counter() - tb
     trees = trees_from_heap_nodes(nodes, hp.max_depth)
     names = list(feature_names) if feature_names is not None else None
     ftypes = list(feature_types) if feature_types is not None else None
@@ -230,12 +291,11 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
                                     colsample_bytree=float(params.colsample_bytree), max_bin=int(params.max_bin),
                                     scale_pos_weight=spw, seed=hp.seed))
     if report is not None:
-        report.n_rows, report.n_rows_global, report.n_features, report.n_trees = N, n_glob, F, T
+        report.n_rows, report.n_rows_global, report.n_features, report.n_trees = N, bd.n_rows_global, F, T
         report.device, report.world = str(dev), world
-        report.t_sketch, report.t_bin, report.t_boost = t_sketch, t_bin, t_boost
-        report.t_total = time.perf_counter() - t0
-        report.extra["cuts"] = cuts
-        report.extra["nbins"] = nbins
+        report.t_sketch, report.t_bin, report.t_boost = bd.t_sketch, bd.t_bin, t_boost
+        report.extra["cuts"] = bd.cuts
+        report.extra["nbins"] = bd.nbins
     return bst
 
 

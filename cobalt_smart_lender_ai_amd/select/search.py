@@ -1,0 +1,110 @@
+"""Randomized hyper-parameter search with stratified K-fold ROC-AUC scoring (K28).
+
+Reference: ``RandomizedSearchCV(XGBClassifier(eval_metric='logloss', scale_pos_weight=spw,
+random_state=78), param_distributions, n_iter=20, scoring='roc_auc', cv=StratifiedKFold(3),
+n_jobs=-1, random_state=22)`` (src/model_train_test/model_tree_train_test.py:132-164) = 60 fits +
+1 refit spread over CPU worker processes.
+
+Here: the candidate list comes from scikit-learn's ``ParameterSampler`` (same ``random_state`` ->
+same 20 candidates); each fold's training rows are sketched + binned once and reused by all 20
+candidates; fits run on the GPU, sequentially on one device or task-parallel with one worker
+process per GPU (``n_gpus``). The best candidate (highest mean AUC, first on ties -- sklearn's
+``rank_test_score`` argmin) is refit on all training rows.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..metrics.auc import roc_auc
+from ..models import gbdt
+from ..models.booster import Booster
+from .split import stratified_kfold_indices
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class SearchResult:
+    best_params_: dict
+    best_score_: float
+    best_index_: int
+    best_estimator_: Booster
+    cv_results_: dict = field(default_factory=dict)
+
+
+def sample_candidates(param_distributions: dict, n_iter: int, random_state: int | None) -> list[dict]:
+    from sklearn.model_selection import ParameterSampler
+
+    return [dict(p) for p in ParameterSampler(param_distributions, n_iter=n_iter, random_state=random_state)]
+
+
+def _fold_scores(X, y, folds, base: dict, candidates: list[dict], device) -> np.ndarray:
+    """[n_candidates, n_folds] AUC matrix; one binning per fold."""
+    Xn = X if isinstance(X, (np.ndarray, torch.Tensor)) else np.asarray(X, dtype=np.float32)
+    yn = np.asarray(y, dtype=np.float32)
+    scores = np.zeros((len(candidates), len(folds)))
+    for k, (tr, va) in enumerate(folds):
+        params0 = gbdt.GBDTParams.from_kwargs(**base)
+        bd = gbdt.bin_dataset(Xn[tr], max_bin=params0.max_bin, sketch_rows=params0.sketch_rows, device=device)
+        for i, cand in enumerate(candidates):
+            p = gbdt.GBDTParams.from_kwargs(**{**base, **cand})
+            bst = gbdt.train_binned(bd, yn[tr], p)
+            prob = bst.predict_proba(Xn[va], device=str(bd.device))
+            scores[i, k] = roc_auc(yn[va], prob)
+    return scores
+
+
+def _worker(args):
+    X, y, folds, base, cands, gpu = args
+    if gpu is not None and torch.cuda.is_available():
+        torch.cuda.set_device(gpu)
+        dev = f"cuda:{gpu}"
+    else:
+        dev = "cpu"
+    return _fold_scores(X, y, folds, base, cands, dev)
+
+
+def randomized_search(X, y, param_distributions: dict, base_params: dict, n_iter: int = 20, cv: int = 3,
+                      random_state: int | None = 22, device=None, n_gpus: int = 1) -> SearchResult:
+    X = np.asarray(X, dtype=np.float32)
+    y = np.asarray(y, dtype=np.float32)
+    cands = sample_candidates(param_distributions, n_iter, random_state)
+    folds = stratified_kfold_indices(y, cv)
+    t0 = time.perf_counter()
+    ngpu = min(n_gpus, torch.cuda.device_count()) if torch.cuda.is_available() else 0
+    if ngpu > 1:
+        import multiprocessing as mp
+
+        shards = [list(range(i, len(cands), ngpu)) for i in range(ngpu)]
+        ctx = mp.get_context("spawn")
+        with ctx.Pool(ngpu) as pool:
+            parts = pool.map(_worker, [(X, y, folds, base_params, [cands[j] for j in sh], g)
+                                       for g, sh in enumerate(shards)])
+        scores = np.zeros((len(cands), len(folds)))
+        for sh, part in zip(shards, parts):
+            scores[sh] = part
+    else:
+        scores = _fold_scores(X, y, folds, base_params, cands, device)
+    mean = scores.mean(1)
+    # sklearn ranks with method="min": equal scores share the best rank
+    order = np.argsort(-mean, kind="stable")
+    ranks = np.empty(len(mean), dtype=np.int64)
+    prev, r = None, 0
+    for pos, i in enumerate(order):
+        if prev is None or mean[i] != prev:
+            r = pos + 1
+            prev = mean[i]
+        ranks[i] = r
+    best = int(np.argmin(ranks))
+    best_params = cands[best]
+    bst = gbdt.train(X, y, gbdt.GBDTParams.from_kwargs(**{**base_params, **best_params}), device=device)
+    res = {"params": cands, "mean_test_score": mean, "std_test_score": scores.std(1), "rank_test_score": ranks,
+           "search_seconds": time.perf_counter() - t0}
+    for k in range(scores.shape[1]):
+        res[f"split{k}_test_score"] = scores[:, k]
+    return SearchResult(best_params, float(mean[best]), best, bst, res)

@@ -1,0 +1,193 @@
+"""FastAPI scoring service with the reference's REST contract (src/api/cobalt_fast_api.py).
+
+Routes (identical paths, request schemas, response keys and error codes):
+
+* ``POST /predict``                 -- one borrower (20 fields, two of them via the aliases
+  ``"application_type_Joint App"`` / ``"hardship_status_No Hardship"``) ->
+  ``{prob_default, shap_values[20], base_value, features[20], input_row}``; micro-batched onto the
+  GPU engine (hipGraph replay of predictor + TreeSHAP).
+* ``POST /predict_bulk_csv``        -- multipart field ``file`` with a CSV of the 20 columns ->
+  ``{"predictions": [row + prob_default]}`` with NaN/inf rendered ``"null"``; errors -> 500
+  ``"Bulk prediction failed: ..."``.
+* ``POST /feature_importance_bulk`` -- ``{"data": [...]}`` -> top-10 average-gain features; empty
+  -> 400 ``"No data provided."``.
+* ``GET /health``                   -- additive: model / device / batcher statistics.
+
+Model loading mirrors the reference lifespan (load at startup, fail fast with ``RuntimeError``) but
+reads the checkpoint with the static, non-executing pickle decoder and takes the path from
+``COBALT_MODEL_PATH`` (or S3 via ``COBALT_SOURCE=s3`` when boto3 is available).
+"""
+from __future__ import annotations
+
+import io
+import os
+import re
+from contextlib import asynccontextmanager
+from pathlib import Path
+from typing import Dict, List
+
+import numpy as np
+import pandas as pd
+from fastapi import FastAPI, HTTPException, Request
+from pydantic import BaseModel, ConfigDict, Field
+
+from ..config import ServeConfig, from_env
+from ..models.booster import Booster, load_pickle_bytes
+from .batcher import MicroBatcher
+from .engine import ScoringEngine
+
+
+class SingleInput(BaseModel):
+    # Aliases are required for the two fields with spaces: the reference's pydantic-v1
+    # ``allow_population_by_field_name`` is ignored under pydantic v2, so the
+    # underscore spellings are rejected with 422 there too.
+    model_config = ConfigDict(populate_by_name=False)
+
+    loan_amnt: float
+    term: float
+    installment: float
+    fico_range_low: float
+    last_fico_range_high: float
+    open_il_12m: float
+    open_il_24m: float
+    max_bal_bc: float
+    num_rev_accts: float
+    pub_rec_bankruptcies: float
+    emp_length_num: float
+    earliest_cr_line_days: float
+    grade_E: int
+    home_ownership_MORTGAGE: int
+    verification_status_Verified: int
+    application_type_Joint_App: int = Field(alias="application_type_Joint App")
+    hardship_status_BROKEN: int
+    hardship_status_COMPLETE: int
+    hardship_status_COMPLETED: int
+    hardship_status_No_Hardship: int = Field(alias="hardship_status_No Hardship")
+
+
+class BulkInput(BaseModel):
+    data: List[Dict]
+
+
+def parse_multipart(body: bytes, content_type: str) -> dict[str, tuple[str | None, bytes]]:
+    """Minimal RFC 7578 multipart/form-data parser -> {field name: (filename, payload)}."""
+    m = re.search(r'boundary="?([^";]+)"?', content_type or "")
+    if not m:
+        raise ValueError("multipart request without boundary")
+    boundary = b"--" + m.group(1).encode("latin-1")
+    out: dict[str, tuple[str | None, bytes]] = {}
+    for part in body.split(boundary)[1:]:
+        if part.startswith(b"--"):
+            break
+        part = part[2:] if part.startswith(b"\r\n") else part
+        head, sep, payload = part.partition(b"\r\n\r\n")
+        if not sep:
+            continue
+        if payload.endswith(b"\r\n"):
+            payload = payload[:-2]
+        headers = head.decode("latin-1")
+        nm = re.search(r'name="([^"]*)"', headers)
+        fn = re.search(r'filename="([^"]*)"', headers)
+        if nm:
+            out[nm.group(1)] = (fn.group(1) if fn else None, payload)
+    return out
+
+
+def load_model(cfg: ServeConfig) -> Booster:
+    if cfg.source == "s3":
+        from ..dataio.artifacts import S3Store
+
+        data = S3Store(cfg.s3_bucket).get_bytes(cfg.s3_model_key)
+    else:
+        p = Path(cfg.model_path)
+        if not p.exists():
+            raise FileNotFoundError(p)
+        data = p.read_bytes()
+    if data[:1] == b"\x80":
+        return load_pickle_bytes(data)[1]
+    return Booster.load_raw(data)
+
+
+def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -> FastAPI:
+    cfg = cfg or from_env(ServeConfig)
+    state: dict = {}
+
+    @asynccontextmanager
+    async def lifespan(app: FastAPI):
+        try:
+            bst = booster if booster is not None else load_model(cfg)
+            engine = ScoringEngine(bst, device=cfg.device, use_graphs=cfg.use_graphs)
+            batcher = MicroBatcher(engine, max_batch=cfg.max_batch, max_wait_ms=cfg.max_wait_ms)
+            await batcher.start()
+            state.update(booster=bst, engine=engine, batcher=batcher,
+                         features=list(bst.feature_names or [f"f{i}" for i in range(bst.num_feature)]))
+            print(f"[INFO] Model and SHAP engine ready on {engine.device} ({bst.num_trees} trees).")
+        except Exception as e:  # noqa: BLE001
+            print(f"[ERROR] Model load failed: {e}")
+            raise RuntimeError("Failed to load model.") from e
+        yield
+        await state["batcher"].stop()
+
+    app = FastAPI(title="Cobalt XGBoost Inference API", lifespan=lifespan)
+    app.state.cobalt = state
+
+    @app.post("/predict")
+    async def predict_single(input_data: SingleInput):
+        row = input_data.model_dump(by_alias=True)
+        feats = state["features"]
+        x = np.array([float(row[f]) for f in feats], dtype=np.float32)
+        prob, phi = await state["batcher"].submit(x)
+        return {
+            "prob_default": float(prob),
+            "shap_values": [float(v) for v in phi],
+            "base_value": float(state["engine"].expected_value),
+            "features": feats,
+            "input_row": {f: float(row[f]) for f in feats},
+        }
+
+    @app.post("/predict_bulk_csv")
+    async def predict_bulk_csv(request: Request):
+        try:
+            ctype = request.headers.get("content-type", "")
+            parts = parse_multipart(await request.body(), ctype)
+            if "file" not in parts:
+                raise ValueError("multipart field 'file' is required")
+            df = pd.read_csv(io.BytesIO(parts["file"][1]))
+            feats = state["features"]
+            if list(df.columns) != feats:
+                raise ValueError(f"feature_names mismatch: expected {feats}, got {list(df.columns)}")
+            X = df.to_numpy(dtype=np.float32, na_value=np.nan)
+            df["prob_default"] = state["engine"].predict_proba(X)
+            df_clean = df.replace([np.inf, -np.inf], np.nan).astype(object).where(
+                df.replace([np.inf, -np.inf], np.nan).notna(), "null")
+            return {"predictions": df_clean.to_dict(orient="records")}
+        except Exception as e:  # noqa: BLE001
+            print(f"[ERROR] Bulk prediction failed: {e}")
+            raise HTTPException(status_code=500, detail=f"Bulk prediction failed: {e}")
+
+    @app.post("/feature_importance_bulk")
+    def feature_importance_bulk(data: BulkInput):
+        if not data.data:
+            raise HTTPException(status_code=400, detail="No data provided.")
+        try:
+            imp = state["booster"].get_score(importance_type="gain")
+            top = sorted(imp.items(), key=lambda kv: kv[1], reverse=True)[:10]
+            return {"top_features": [{"feature": k, "importance": v} for k, v in top]}
+        except Exception as e:  # noqa: BLE001
+            raise HTTPException(status_code=500, detail=f"Feature importance computation failed: {e}")
+
+    @app.get("/health")
+    def health():
+        eng = state.get("engine")
+        b = state.get("batcher")
+        return {
+            "status": "ok" if eng is not None else "loading",
+            "device": str(eng.device) if eng else None,
+            "trees": state["booster"].num_trees if "booster" in state else None,
+            "graphs": bool(eng.use_graphs) if eng else None,
+            "batches": b.stats.batches if b else 0,
+            "rows": b.stats.rows if b else 0,
+            "max_batch_seen": b.stats.max_batch_seen if b else 0,
+        }
+
+    return app

@@ -1,0 +1,57 @@
+"""GPU preprocessing kernels == host path (run with -m gpu)."""
+import warnings
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from cobalt_smart_lender_ai_amd.dataio.synth_raw import make_raw_lendingclub
+from cobalt_smart_lender_ai_amd.ops import prep_ops
+from cobalt_smart_lender_ai_amd.prep import clean, features
+
+pytestmark = pytest.mark.gpu
+
+
+def _eq(a, b):
+    pd.testing.assert_frame_equal(a.reset_index(drop=True), b.reset_index(drop=True), check_dtype=False,
+                                  check_exact=False, rtol=1e-14)
+
+
+def test_pipeline_gpu_equals_cpu():
+    raw = make_raw_lendingclub(20000, seed=3)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        g1 = clean.clean_data_flow(raw, device="cuda")
+        c1 = clean.clean_data_flow(raw, device="cpu")
+        _eq(g1, c1)
+        g2 = features.clean_lending_data(g1, reference_date="2025-07-04", device="cuda")
+        c2 = features.clean_lending_data(c1, reference_date="2025-07-04", device="cpu")
+        _eq(g2, c2)
+        gt, gn = features.feature_engineer_lending_data(g2, device="cuda")
+        ct, cn = features.feature_engineer_lending_data(c2, device="cpu")
+    _eq(gt, ct)
+    _eq(gn, cn)
+
+
+def test_prep_kernels_match_host():
+    rng = np.random.default_rng(0)
+    a = rng.standard_normal((7, 100_003))
+    a[rng.random(a.shape) < 0.1] = np.nan
+    a[3, :50] = a[3, 50:100]  # some duplicate structure
+    X = torch.from_numpy(a)
+    Xg = X.cuda()
+    assert torch.equal(prep_ops.col_null_counts(Xg).cpu(), prep_ops.col_null_counts(X))
+    assert torch.equal(prep_ops.row_null_counts(Xg).cpu(), prep_ops.row_null_counts(X))
+    assert torch.equal(prep_ops.row_hash(Xg).cpu(), prep_ops.row_hash(X))
+    mg, mc = prep_ops.col_moments(Xg).cpu(), prep_ops.col_moments(X)
+    torch.testing.assert_close(mg, mc, rtol=1e-12, atol=1e-9)
+    Yg, Yc = Xg.clone(), X.clone()
+    prep_ops.masked_log1p_(Yg, [0, 2, 5])
+    prep_ops.masked_log1p_(Yc, [0, 2, 5])
+    torch.testing.assert_close(Yg.cpu(), Yc, rtol=2e-16, atol=0, equal_nan=True)
+    ig = prep_ops.fill_with_indicator_(Yg, [1, 4], [0.5, -1.0])
+    ic = prep_ops.fill_with_indicator_(Yc, [1, 4], [0.5, -1.0])
+    assert torch.equal(ig.cpu(), ic)
+    codes = torch.from_numpy(rng.integers(-1, 6, 10_000).astype(np.int32))
+    assert torch.equal(prep_ops.onehot(codes.cuda(), 6).cpu(), prep_ops.onehot(codes, 6))
