@@ -65,7 +65,7 @@ def main() -> None:
                              random_state=78)
 
     def fit():
-        rep = gbdt.FitReport()
+        rep = gbdt.FitReport(sync_phases=a.profile_fit)
         b = gbdt.train(X, y, params, device=dev, dist=ctx if world > 1 else None, n_rows_global=n_global,
                        row_offset=start, report=rep, feature_names=synth.FEATURES,
                        feature_types=synth.FEATURE_TYPES)
@@ -98,7 +98,8 @@ def main() -> None:
     if a.profile_fit and rank == 0:
         for r in reps:
             print(f"[bench] sketch {r.t_sketch*1e3:.1f} ms  bin {r.t_bin*1e3:.1f} ms  boost {r.t_boost*1e3:.1f} ms"
-                  f"  total {r.t_total*1e3:.1f} ms", file=sys.stderr)
+                  f"  total {r.t_total*1e3:.1f} ms  phases "
+                  + " ".join(f"{k}={v*1e3:.1f}" for k, v in r.phases.items()), file=sys.stderr)
     if rank == 0:
         out = {
             "metric": "rows/sec GBDT train on 10M-row LendingClub-shaped tabular; AUC parity",

@@ -103,28 +103,36 @@ struct PathElem {
 };
 static_assert(sizeof(PathElem) == 24, "PathElem");
 
+// One block = (path chunk, row). Each thread walks its paths in a fixed order and accumulates into a
+// private LDS column s_part[f][tid]; a fixed-shape tree reduction then sums the columns. The result
+// of every block goes to its own slab slot (or straight to phi when there is one chunk), and
+// k_shap_reduce sums the chunk slots in ascending order -- no floating-point atomics. The chunk size
+// depends only on the forest and F (never on the batch size), so a row's SHAP values are
+// bit-identical run to run and whether it is scored alone or inside a bulk batch.
+// P = path register capacity (max unique features on a path + 1): 8 covers depth <= 7 trees without
+// paying for the predicated iterations of a 16/32-slot path.
+template <int P>
 __global__ __launch_bounds__(256) void k_treeshap(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
                                                   const PathElem* __restrict__ elems,
                                                   const int32_t* __restrict__ path_ptr,
-                                                  const double* __restrict__ path_val, int n_paths,
-                                                  double* __restrict__ phi) {
-  extern __shared__ double s_phi[];  // [F]
+                                                  const double* __restrict__ path_val, int n_paths, int chunk,
+                                                  int nchunks, double* __restrict__ out) {
+  extern __shared__ double s_part[];  // [F][blockDim.x]
+  const int B = blockDim.x, tid = threadIdx.x;
   const int64_t row = blockIdx.y;
-  for (int f = threadIdx.x; f < F; f += blockDim.x) s_phi[f] = 0.0;
-  __syncthreads();
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < n_paths) {
+  for (int f = 0; f < F; ++f) s_part[f * B + tid] = 0.0;
+  const int p_end = min(n_paths, (int)(blockIdx.x + 1) * chunk);
+  const float* x = X + row * ldx;
+  for (int p = blockIdx.x * chunk + tid; p < p_end; p += B) {
     const int e0 = path_ptr[p], k = path_ptr[p + 1] - e0;  // k unique features (bias excluded)
-    const float* x = X + row * ldx;
-    double z[kMaxPath], o[kMaxPath], w[kMaxPath];
-    int feat[kMaxPath];
-    // bias element
+    double z[P], o[P], w[P];
+    int feat[P];
     z[0] = 1.0; o[0] = 1.0; w[0] = 1.0; feat[0] = -1;
 #pragma unroll
-    for (int i = 1; i < kMaxPath; ++i) { z[i] = 0.0; o[i] = 0.0; w[i] = 0.0; feat[i] = -1; }
+    for (int i = 1; i < P; ++i) { z[i] = 0.0; o[i] = 0.0; w[i] = 0.0; feat[i] = -1; }
     // EXTEND each element
 #pragma unroll
-    for (int l = 1; l < kMaxPath; ++l) {
+    for (int l = 1; l < P; ++l) {
       if (l <= k) {
         const PathElem e = elems[e0 + l - 1];
         const float v = x[e.feat];
@@ -132,7 +140,7 @@ __global__ __launch_bounds__(256) void k_treeshap(const float* __restrict__ X, i
         z[l] = e.zero; o[l] = one; feat[l] = e.feat;
         w[l] = 0.0;
 #pragma unroll
-        for (int j = kMaxPath - 2; j >= 0; --j) {
+        for (int j = P - 2; j >= 0; --j) {
           if (j <= l - 1) {
             w[j + 1] += one * w[j] * (double)(j + 1) / (double)(l + 1);
             w[j] = e.zero * w[j] * (double)(l - j) / (double)(l + 1);
@@ -143,14 +151,14 @@ __global__ __launch_bounds__(256) void k_treeshap(const float* __restrict__ X, i
     const double leaf = path_val[p];
     // UNWOUND sum per element
 #pragma unroll
-    for (int i = 1; i < kMaxPath; ++i) {
+    for (int i = 1; i < P; ++i) {
       if (i <= k) {
         const double one = o[i], zero = z[i];
         double total = 0.0;
         if (one != 0.0) {
           double next = w[k];
 #pragma unroll
-          for (int j = kMaxPath - 2; j >= 0; --j) {
+          for (int j = P - 2; j >= 0; --j) {
             if (j <= k - 1) {
               const double tmp = next / ((double)(j + 1) * one);
               total += tmp;
@@ -159,31 +167,87 @@ __global__ __launch_bounds__(256) void k_treeshap(const float* __restrict__ X, i
           }
         } else {
 #pragma unroll
-          for (int j = kMaxPath - 2; j >= 0; --j) {
+          for (int j = P - 2; j >= 0; --j) {
             if (j <= k - 1) total += w[j] / (zero * (double)(k - j));
           }
         }
         total *= (double)(k + 1);
-        atomicAdd(&s_phi[feat[i]], total * (one - zero) * leaf);
+        s_part[feat[i] * B + tid] += total * (one - zero) * leaf;
       }
     }
   }
   __syncthreads();
-  for (int f = threadIdx.x; f < F; f += blockDim.x) {
-    const double v = s_phi[f];
-    if (v != 0.0) atomicAdd(&phi[row * F + f], v);
+  for (int stride = B >> 1; stride >= 1; stride >>= 1) {
+    for (int idx = tid; idx < F * stride; idx += B) {
+      const int f = idx / stride, j = idx - f * stride;
+      s_part[f * B + j] += s_part[f * B + j + stride];
+    }
+    __syncthreads();
   }
+  for (int f = tid; f < F; f += B) out[(row * nchunks + blockIdx.x) * F + f] = s_part[f * B];
+}
+
+__global__ void k_shap_reduce(const double* __restrict__ slab, int64_t n, int F, int nchunks,
+                              double* __restrict__ phi) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * F) return;
+  const int64_t row = i / F;
+  const int f = (int)(i - row * F);
+  const double* src = slab + row * nchunks * F + f;
+  double acc = 0.0;
+  for (int c = 0; c < nchunks; ++c) acc += src[(int64_t)c * F];
+  phi[i] = acc;
+}
+
+constexpr int kShapPathsPerThread = 2;
+
+static int shap_block(int F) {
+  // LDS column store: F * block * 8 bytes must fit the 160 KB of a CU
+  int b = 256;
+  while (b > 64 && (int64_t)F * b * 8 > 160 * 1024) b >>= 1;
+  return ((int64_t)F * b * 8 > 160 * 1024) ? 0 : b;
+}
+
+// Number of path chunks (and so slab slots per row) the launch for n rows uses; the caller sizes
+// the workspace as n * chunks * F doubles when chunks > 1.
+COBALT_API int cobalt_treeshap_chunks(int64_t n, int F, int n_paths) {
+  const int B = shap_block(F);
+  if (B == 0 || n <= 0 || n_paths <= 0) return 1;
+  (void)n;
+  return (int)ceil_div((int64_t)n_paths, (int64_t)B * kShapPathsPerThread);
 }
 
 COBALT_API int cobalt_treeshap(const float* X, int64_t n, int F, int64_t ldx, const void* elems, const int32_t* path_ptr,
-                               const double* path_val, int n_paths, int max_len, double* phi, hipStream_t stream) {
+                               const double* path_val, int n_paths, int max_len, double* phi, double* work,
+                               int nchunks, hipStream_t stream) {
   if (n <= 0 || n_paths <= 0) return 0;
   if (max_len + 1 > kMaxPath) return -3;
   if (n > 65535) return -4;  // grid.y limit; the caller batches rows
-  const int block = 256;
-  dim3 grid(ceil_div(n_paths, block), (unsigned)n);
-  hipLaunchKernelGGL(k_treeshap, grid, dim3(block), F * sizeof(double), stream, X, n, F, ldx,
-                     static_cast<const PathElem*>(elems), path_ptr, path_val, n_paths, phi);
+  const int B = shap_block(F);
+  if (B == 0) return -5;
+  if (nchunks < 1) return -6;
+  if (nchunks > 1 && work == nullptr) return -7;
+  if (nchunks != cobalt_treeshap_chunks(n, F, n_paths)) return -8;
+  const int chunk = B * kShapPathsPerThread;
+  const size_t lds = (size_t)F * B * sizeof(double);
+  dim3 grid((unsigned)nchunks, (unsigned)n);
+  const PathElem* pe = static_cast<const PathElem*>(elems);
+  double* dst = nchunks > 1 ? work : phi;
+  if (max_len + 1 <= 8) {
+    if (lds > 64 * 1024) CK(hipFuncSetAttribute((const void*)k_treeshap<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_treeshap<8>, grid, dim3(B), lds, stream, X, n, F, ldx, pe, path_ptr, path_val, n_paths, chunk,
+                       nchunks, dst);
+  } else {
+    if (lds > 64 * 1024) CK(hipFuncSetAttribute((const void*)k_treeshap<kMaxPath>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_treeshap<kMaxPath>, grid, dim3(B), lds, stream, X, n, F, ldx, pe, path_ptr, path_val, n_paths,
+                       chunk, nchunks, dst);
+  }
   CK_LAUNCH();
+  if (nchunks > 1) {
+    const int64_t tot = n * F;
+    hipLaunchKernelGGL(k_shap_reduce, dim3((unsigned)ceil_div(tot, (int64_t)256)), dim3(256), 0, stream, work, n, F,
+                       nchunks, phi);
+    CK_LAUNCH();
+  }
   return 0;
 }

@@ -119,6 +119,8 @@ class Booster:
     objective: str = "binary:logistic"
     train_params: dict[str, Any] = field(default_factory=dict)
     attributes: dict[str, str] = field(default_factory=dict)
+    # the "Config" section of a loaded model, re-emitted verbatim while the forest is unchanged
+    source_config: dict[str, Any] | None = field(default=None, repr=False, compare=False)
 
     # --------------------------------------------------------------------------------- basics
     @property
@@ -219,7 +221,7 @@ class Booster:
         f = _fmt_float
         return {
             "learner": {
-                "generic_param": {"device": "cuda:0", "fail_on_invalid_gpu_id": "0", "n_jobs": "0", "nthread": "0",
+                "generic_param": {"device": "cpu", "fail_on_invalid_gpu_id": "0", "n_jobs": "0", "nthread": "0",
                                   "random_state": str(int(p["seed"])), "seed": str(int(p["seed"])),
                                   "seed_per_iteration": "0", "validate_parameters": "1"},
                 "gradient_booster": {
@@ -286,7 +288,11 @@ class Booster:
             },
             "version": [3, 0, 0],
         }
-        return {"Config": self._config_doc(), "Model": model}
+        cfg = self.source_config
+        if cfg is None or cfg.get("learner", {}).get("gradient_booster", {}).get("gbtree_model_param", {}).get(
+                "num_trees") != str(self.num_trees):
+            cfg = self._config_doc()
+        return {"Config": cfg, "Model": model}
 
     @classmethod
     def from_doc(cls, doc: dict[str, Any]) -> "Booster":
@@ -316,10 +322,11 @@ class Booster:
         return cls(trees=trees,
                    feature_names=list(lrn.get("feature_names") or []) or None,
                    feature_types=list(lrn.get("feature_types") or []) or None,
-                   base_score=float(lmp.get("base_score", "0.5")),
+                   base_score=float(np.float32(lmp.get("base_score", "0.5"))),
                    num_feature=int(lmp.get("num_feature", "0")),
                    objective=obj, train_params=params,
-                   attributes=dict(lrn.get("attributes") or {}))
+                   attributes=dict(lrn.get("attributes") or {}),
+                   source_config=doc.get("Config"))
 
     # --------------------------------------------------------------------------- file I/O
     def save_raw(self, fmt: str = "ubj") -> bytes:
@@ -537,47 +544,36 @@ def iter_leaf_paths(t: Tree) -> Iterable[tuple[int, list[tuple[int, int, bool]]]
 def trees_from_heap_nodes(nodes: np.ndarray, max_depth: int) -> list[Tree]:
     """Convert heap-ordered node records (NODE_DTYPE, [T, 2^(D+1)-1]) of the trainer into XGBoost
     trees, numbering nodes in XGBoost's depthwise creation order (children allocated in pairs)."""
-    out: list[Tree] = []
-    for rec in nodes:
-        status = rec["status"]
-        order: list[int] = []
-        level = [0]
-        while level:
-            nxt = []
-            for h in level:
-                if status[h] in (2, 3):
-                    order.append(h)
-                    if status[h] == 2:
-                        nxt += [2 * h + 1, 2 * h + 2]
-            level = nxt
-        new_id = {h: i for i, h in enumerate(order)}
-        n = len(order)
-        lc = np.full(n, -1, np.int32)
-        rc = np.full(n, -1, np.int32)
-        par = np.full(n, ROOT_PARENT, np.int32)
-        si = np.zeros(n, np.int32)
-        sc = np.zeros(n, np.float32)
-        dl = np.zeros(n, np.uint8)
-        bw = np.zeros(n, np.float32)
-        lo = np.zeros(n, np.float32)
-        sh = np.zeros(n, np.float32)
-        for h, i in new_id.items():
-            r = rec[h]
-            bw[i] = r["base_weight"]
-            sh[i] = r["sum_hess"]
-            if r["status"] == 2:
-                lc[i] = new_id[2 * h + 1]
-                rc[i] = new_id[2 * h + 2]
-                par[lc[i]] = i
-                par[rc[i]] = i
-                si[i] = r["feat"]
-                sc[i] = r["split_cond"]
-                dl[i] = r["default_left"]
-                lo[i] = r["loss_chg"]
-            else:
-                sc[i] = r["leaf_value"]
-        out.append(Tree(lc, rc, par, si, sc, dl, bw, lo, sh))
-    return out
+    # Heap indices of one level are contiguous and children are allocated in parent order, so the
+    # depthwise creation order is simply ascending heap index over the live nodes.
+    # Everything is computed for all trees at once and split per tree at the end.
+    if nodes.ndim != 2 or nodes.shape[0] == 0:
+        return []
+    T, M = nodes.shape
+    status = nodes["status"]
+    live = (status == 2) | (status == 3)
+    new_id = (np.cumsum(live, axis=1) - 1).astype(np.int32)       # per-tree position of each live node
+    counts = live.sum(1)
+    split_full = status == 2
+    kid = np.minimum(2 * np.arange(M) + 1, M - 2)
+    lc_full = np.where(split_full, new_id[:, kid], -1).astype(np.int32)
+    rc_full = np.where(split_full, new_id[:, kid + 1], -1).astype(np.int32)
+    par_full = np.full((T, M), ROOT_PARENT, np.int32)
+    parent_heap = (np.arange(M) - 1) // 2
+    has_par = np.arange(M) > 0
+    par_full[:, has_par] = new_id[:, parent_heap[has_par]]
+    r = nodes[live]
+    split = r["status"] == 2
+    lc, rc, par = lc_full[live], rc_full[live], par_full[live]
+    si = np.where(split, r["feat"], 0).astype(np.int32)
+    sc = np.where(split, r["split_cond"], r["leaf_value"]).astype(np.float32)
+    dl = np.where(split, r["default_left"], 0).astype(np.uint8)
+    lo = np.where(split, r["loss_chg"], 0).astype(np.float32)
+    bw = r["base_weight"].astype(np.float32)
+    sh = r["sum_hess"].astype(np.float32)
+    cuts = np.cumsum(counts)[:-1]
+    cols = [np.split(a, cuts) for a in (lc, rc, par, si, sc, dl, bw, lo, sh)]
+    return [Tree(*parts) for parts in zip(*cols)]
 
 
 NODE_DTYPE = np.dtype([

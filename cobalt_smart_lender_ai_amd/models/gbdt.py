@@ -75,7 +75,19 @@ class FitReport:
     t_bin: float = 0.0
     t_boost: float = 0.0
     t_total: float = 0.0
+    phases: dict[str, float] = field(default_factory=dict)   # filled when ``sync_phases`` is set
+    sync_phases: bool = False
     extra: dict[str, Any] = field(default_factory=dict)
+
+    def mark(self, name: str, t_prev: float, dev: torch.device) -> float:
+        """Record the wall time since ``t_prev`` under ``name`` (device-synchronised when profiling)."""
+        if not self.sync_phases:
+            return t_prev
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        now = time.perf_counter()
+        self.phases[name] = self.phases.get(name, 0.0) + (now - t_prev)
+        return now
 
 
 def _to_tensor(X, device, dtype=torch.float32) -> torch.Tensor:
@@ -203,6 +215,8 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     dev = bd.device
     world = dist.world if dist is not None else 1
     N, F = bd.n_rows, bd.n_features
+    rep = report if report is not None else FitReport()
+    tp = rep.mark("pre", time.perf_counter(), dev)
     yt = _to_tensor(y, dev).reshape(-1)
     if yt.shape[0] != N:
         raise ValueError("X and y row counts differ")
@@ -242,6 +256,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                                   gamma=float(params.gamma), min_child_weight=float(params.min_child_weight),
                                   subsample=float(params.subsample), seed=int(params.random_state),
                                   gscale=gscale, hscale=hscale)
+    tp = rep.mark("labels_weights", tp, dev)
     tb = time.perf_counter()
     if dev.type == "cuda":
         from ..ops import gbdt_ops
@@ -258,9 +273,12 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         fm = torch.as_tensor(fmask_np, device=dev).contiguous()
         tr.set_data(bd.records, bd.binsT, bd.cuts.contiguous(), bd.nbins.to(torch.int32).contiguous(),
                     yt.contiguous(), wt, margin, fm)
+        tp = rep.mark("trainer_setup", tp, dev)
         tr.grow(0, T)
+        tp = rep.mark("grow", tp, dev)
         nodes = tr.fetch(0, T)
         tr.close()
+        tp = rep.mark("fetch", tp, dev)
     else:
         cuts_np = bd.cuts.cpu().numpy()
         nb_np = bd.nbins.cpu().numpy()
@@ -280,8 +298,10 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                                                  allreduce))
         nodes = np.stack(recs) if recs else np.zeros((0, (1 << (hp.max_depth + 1)) - 1),
                                                       dtype=gbdt_host.NODE_DTYPE)
+        rep.extra["margin"] = margin_np
     t_boost = time.perf_counter() - tb
     trees = trees_from_heap_nodes(nodes, hp.max_depth)
+    tp = rep.mark("to_trees", tp, dev)
     names = list(feature_names) if feature_names is not None else None
     ftypes = list(feature_types) if feature_types is not None else None
     bst = Booster(trees=trees, feature_names=names, feature_types=ftypes, base_score=base_score, num_feature=F,

@@ -22,7 +22,9 @@ _native.register("cobalt_predict", ctypes.c_int,
                   ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
 _native.register("cobalt_treeshap", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p])
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                  ctypes.c_void_p])
+_native.register("cobalt_treeshap_chunks", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int])
 
 PATH_ELEM = np.dtype([("lo", "<f4"), ("hi", "<f4"), ("feat", "<i4"), ("nan_ok", "<i4"), ("zero", "<f8")])
 
@@ -193,15 +195,18 @@ def predict_gpu(b: Booster, X: torch.Tensor, n_trees: int | None = None, out_mar
 
 
 def treeshap_gpu(b: Booster, X: torch.Tensor, phi: torch.Tensor) -> None:
-    """Accumulate TreeSHAP values into ``phi`` [N, F] float64 (must be zeroed) on the current stream."""
+    """Write TreeSHAP values into ``phi`` [N, F] float64 on the current stream (deterministic: no
+    floating-point atomics; partial sums are combined in a fixed order)."""
     gf = gpu_forest(b, X.device, None, with_shap=True)
     N, F = X.shape
     lib = _native.lib()
     for s in range(0, N, 65535):
         e = min(N, s + 65535)
+        nch = int(lib.cobalt_treeshap_chunks(e - s, F, gf.n_paths))
+        work = torch.empty((e - s) * nch * F, dtype=torch.float64, device=X.device) if nch > 1 else None
         rc = lib.cobalt_treeshap(X[s:e].data_ptr(), e - s, F, X.stride(0), gf.elems.data_ptr(), gf.path_ptr.data_ptr(),
                                  gf.path_val.data_ptr(), gf.n_paths, gf.max_len, phi[s:e].data_ptr(),
-                                 _native.stream_handle())
+                                 work.data_ptr() if work is not None else None, nch, _native.stream_handle())
         _native.check(rc, "cobalt_treeshap")
 
 

@@ -2,8 +2,8 @@
 
 The reference scores one HTTP request at a time with ``xgb_model.predict_proba`` and
 ``shap.TreeExplainer.shap_values`` (src/api/cobalt_fast_api.py:90-108). Here a request batch is
-padded to a bucket size (1, 8, 64, 512, 4096) whose whole pipeline -- predictor kernel + zeroing of
-the SHAP accumulator + TreeSHAP kernel -- was captured once into a hipGraph (``torch.cuda.CUDAGraph``
+padded to a bucket size (1, 8, 64, 512, 4096) whose whole pipeline -- predictor kernel + TreeSHAP kernel
+(+ its fixed-order chunk reduction) -- was captured once into a hipGraph (``torch.cuda.CUDAGraph``
 over the library's own launches on the capture stream). Serving a batch is then: one H2D copy into
 the bucket's static input, one graph replay, one D2H copy. Larger batches are split into bucket
 sized pieces. On a CPU-only host the engine runs the NumPy reference path instead.
@@ -60,7 +60,6 @@ class ScoringEngine:
 
     def _run_full(self, bk: _Bucket) -> None:
         self._ops.predict_gpu(self.booster, bk.x, None, out_prob=bk.prob)
-        bk.phi.zero_()
         self._ops.treeshap_gpu(self.booster, bk.x, bk.phi)
 
     def _make_bucket(self, size: int) -> _Bucket:

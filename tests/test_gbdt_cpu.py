@@ -1,0 +1,119 @@
+"""GBDT host path, model formats and the data-parallel protocol on CPU (gloo).
+
+* the host oracle's training margin equals re-scoring the converted model (tree conversion + bin ->
+  threshold semantics);
+* the shipped checkpoint round-trips byte-exactly through our UBJSON and static-pickle codecs;
+* quantile cuts / binning agree with a searchsorted oracle;
+* 2-rank data-parallel training (gloo, row shards) yields exactly the single-process model.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from cobalt_smart_lender_ai_amd.dataio import safe_pickle, ubjson
+from cobalt_smart_lender_ai_amd.models import gbdt, sketch
+from cobalt_smart_lender_ai_amd.models.booster import Booster, load_pickle_bytes, predict_margin_host
+
+
+def _data(n=3000, f=6, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, f)).astype(np.float32)
+    X[:, 1] = np.round(X[:, 1] * 2)           # low-cardinality column
+    X[rng.random((n, f)) < 0.07] = np.nan
+    z = 1.2 * np.nan_to_num(X[:, 0]) - np.nan_to_num(X[:, 1]) + np.isnan(X[:, 3]) * 1.5 - 1.5
+    y = (rng.random(n) < 1 / (1 + np.exp(-z))).astype(np.float32)
+    return X, y
+
+
+PARAMS = dict(n_estimators=8, max_depth=4, learning_rate=0.3, gamma=0.5, reg_lambda=1.0, min_child_weight=1.0,
+              scale_pos_weight=3.0, random_state=7)
+
+
+def test_training_margin_equals_model_prediction():
+    X, y = _data()
+    rep = gbdt.FitReport()
+    b = gbdt.train(X, y, PARAMS, device="cpu", report=rep)
+    assert b.num_trees == 8
+    m_train = rep.extra["margin"]
+    np.testing.assert_array_equal(predict_margin_host(b, X), m_train)
+    # XGBoost JSON round trip keeps the model exactly
+    b2 = Booster.load_raw(b.save_raw("ubj"))
+    np.testing.assert_array_equal(predict_margin_host(b2, X), m_train)
+    b3 = Booster.load_raw(b.save_raw("json"))
+    np.testing.assert_array_equal(predict_margin_host(b3, X), m_train)
+
+
+@pytest.mark.parametrize("extra", [dict(subsample=0.7), dict(colsample_bytree=0.5), dict(reg_alpha=0.5),
+                                   dict(min_child_weight=20.0)])
+def test_training_margin_equals_prediction_with_sampling_and_regularisation(extra):
+    X, y = _data(seed=1)
+    rep = gbdt.FitReport()
+    b = gbdt.train(X, y, {**PARAMS, **extra}, device="cpu", report=rep)
+    np.testing.assert_array_equal(predict_margin_host(b, X), rep.extra["margin"])
+
+
+def test_reference_checkpoint_round_trips_bytes(reference_model_bytes):
+    st, raw = safe_pickle.read_xgb_classifier_pickle(reference_model_bytes)
+    doc = ubjson.loads(raw)
+    assert ubjson.dumps(doc) == raw
+    b = Booster.load_raw(raw)
+    assert b.save_raw("ubj") == raw
+    assert b.num_trees == 300 and b.num_feature == 20
+    st2, b2 = load_pickle_bytes(reference_model_bytes)
+    assert st2["n_estimators"] == 300 and st2["max_depth"] == 7
+    assert b2.expected_value() == pytest.approx(-0.0027751700, abs=1e-9)
+
+
+def test_cuts_and_binning_oracle():
+    X, _ = _data(n=5000)
+    Xt = torch.from_numpy(X)
+    cuts, nb = sketch.compute_cuts(sketch.local_sample(Xt, 0, 1), 256)
+    cuts, nb = cuts.numpy(), nb.numpy()
+    bins = sketch.bin_matrix_host(X, cuts, nb)
+    for f in range(X.shape[1]):
+        c = cuts[f, : nb[f]]
+        assert np.all(np.diff(c) > 0)
+        col = X[:, f]
+        ok = ~np.isnan(col)
+        ref = np.minimum(np.searchsorted(c, col[ok], side="right"), nb[f] - 1)
+        np.testing.assert_array_equal(bins[ok, f], ref)
+        assert np.all(bins[~ok, f] == sketch.MAX_BINS_U8)
+    col = X[:, 1]
+    assert nb[1] == len(np.unique(col[~np.isnan(col)]))  # low cardinality: one bin per distinct value
+
+
+# ------------------------------------------------------------------------------ data parallel
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from cobalt_smart_lender_ai_amd.parallel import dist as pdist
+
+    ctx = pdist.init_from_env(backend="gloo", native=False)
+    X, y = _data(n=4001, seed=2)
+    s, e = pdist.shard_range(len(X), rank, world)
+    params = {**PARAMS, "subsample": 0.8}
+    b = gbdt.train(X[s:e], y[s:e], params, device="cpu", dist=ctx, n_rows_global=len(X), row_offset=s)
+    if rank == 0:
+        with open(os.path.join(out_dir, "dp.ubj"), "wb") as fh:
+            fh.write(b.save_raw("ubj"))
+    pdist.shutdown()
+
+
+def test_data_parallel_gloo_matches_single_process(tmp_path):
+    import torch.multiprocessing as mp
+
+    X, y = _data(n=4001, seed=2)
+    ref = gbdt.train(X, y, {**PARAMS, "subsample": 0.8}, device="cpu")
+    mp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    dp = Booster.load_raw((tmp_path / "dp.ubj").read_bytes())
+    np.testing.assert_array_equal(predict_margin_host(dp, X), predict_margin_host(ref, X))
+    assert dp.save_raw("ubj") == ref.save_raw("ubj")

@@ -49,7 +49,7 @@ def test_prep_kernels_match_host():
     Yg, Yc = Xg.clone(), X.clone()
     prep_ops.masked_log1p_(Yg, [0, 2, 5])
     prep_ops.masked_log1p_(Yc, [0, 2, 5])
-    torch.testing.assert_close(Yg.cpu(), Yc, rtol=2e-16, atol=0, equal_nan=True)
+    torch.testing.assert_close(Yg.cpu(), Yc, rtol=1e-15, atol=0, equal_nan=True)  # device log1p vs libm: <=2 ulp
     ig = prep_ops.fill_with_indicator_(Yg, [1, 4], [0.5, -1.0])
     ic = prep_ops.fill_with_indicator_(Yc, [1, 4], [0.5, -1.0])
     assert torch.equal(ig.cpu(), ic)
