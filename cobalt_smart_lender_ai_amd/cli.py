@@ -7,6 +7,7 @@ Commands mirror the reference's scripts:
   clean     stage 1 (clean_data.py; ``--full`` = ``python clean_data.py full``)
   features  stage 2 (feature_engineering.py)
   train     tree model training (model_tree_train_test.py)
+  train-nn  NN challenger (notebook 04 cells 31-44)
   serve     FastAPI scoring service (cobalt_fast_api.py, uvicorn)
 
 The artifact store is ``--store`` or ``$COBALT_ARTIFACT_URI`` (a local directory or ``s3://bucket``).
@@ -68,6 +69,18 @@ def cmd_train(args) -> int:
     return 0
 
 
+def cmd_train_nn(args) -> int:
+    from .config import CLEAN_DATA_KEY_NN
+    from .nn.mlp import MLPConfig
+    from .pipeline.train_nn import NNTrainConfig, run_nn_training
+
+    st = _store(args)
+    cfg = NNTrainConfig(reproduce_reference=not args.use_smote, mlp=MLPConfig(epochs=args.epochs))
+    m = run_nn_training(st.read_csv(CLEAN_DATA_KEY_NN), cfg, store=st, local_dir=args.local_dir, device=args.device)
+    print(json.dumps({k: m[k] for k in ("auc", "auc_thresholded", "selected_features", "train_seconds")}, indent=2))
+    return 0
+
+
 def cmd_serve(args) -> int:
     import uvicorn
 
@@ -101,6 +114,11 @@ def main(argv: list[str] | None = None) -> int:
     s.add_argument("--n-iter", type=int, default=None)
     s.add_argument("--gpus", type=int, default=None)
     s.set_defaults(fn=cmd_train)
+    s = sub.add_parser("train-nn")
+    s.add_argument("--local-dir", default="models")
+    s.add_argument("--epochs", type=int, default=50)
+    s.add_argument("--use-smote", action="store_true", help="train on the SMOTE-resampled, scaled rows")
+    s.set_defaults(fn=cmd_train_nn)
     s = sub.add_parser("serve")
     s.add_argument("--host", default="0.0.0.0")
     s.add_argument("--port", type=int, default=8000)

@@ -1,0 +1,363 @@
+// Fused MLP challenger (K31): the notebook's Dense 128-32-16-1 ReLU/sigmoid network
+// (notebooks/04_model_training.ipynb cell 39 `build_and_train_nn`).
+//
+// Training (k_mlp_train): sequential mini-batch SGD is a chain of tiny dependent steps (batch 32,
+// 7,361 parameters), so instead of ~20 library launches per step the WHOLE epoch runs inside one
+// workgroup: weights, AdamW moments and the batch activations live in LDS (~140 KB at F = 20) and
+// every step is forward -> backward -> AdamW with workgroup barriers only. One workgroup trains one
+// model; a launch with G workgroups trains G independent models (seeds / hyper-parameters) on G
+// CUs at the cost of one.
+//
+// Semantics follow the Keras model the reference builds:
+//   * loss = mean BCE computed from the logit (Keras uses the sigmoid's logit when present),
+//     gradient (p - y) / batch_rows; last partial batch = its own mean;
+//   * L2 kernel regulariser lambda * sum(W^2) on the three hidden Dense layers (not the output
+//     layer, not biases) -> + 2 * lambda * W;
+//   * AdamW (Keras 3): p -= lr * wd * p, then m += (g - m)(1 - b1), v += (g^2 - v)(1 - b2),
+//     p -= lr * sqrt(1 - b2^t) / (1 - b1^t) * m / (sqrt(v) + eps), t = step + 1;
+//   * ExponentialDecay(staircase): lr = lr0 * rate^floor(step / decay_steps).
+// Parameter layout per model (floats): W1[F][128] b1[128] W2[128][32] b2[32] W3[32][16] b3[16]
+// W4[16] b4[1]  (P = 128 F + 4801).
+//
+// Inference (k_mlp_forward): 32-row tiles per workgroup iteration with the same LDS-resident
+// forward code; writes sigmoid probabilities (and optionally logits).
+#include "common.h"
+
+namespace {
+constexpr int H1 = 128, H2 = 32, H3 = 16, MB = 32, NT = 256;
+constexpr int kMaxF = 32;
+
+struct MlpHyper {
+  float lr0, decay_rate;
+  int32_t decay_steps, staircase;
+  float weight_decay, beta1, beta2, eps;
+  float l2;
+  int32_t batch;
+  int32_t pad[2];
+};
+static_assert(sizeof(MlpHyper) == 48, "MlpHyper layout mirrored in nn/mlp.py");
+
+__host__ __device__ constexpr int mlp_params(int F) { return F * H1 + H1 + H1 * H2 + H2 + H2 * H3 + H3 + H3 + 1; }
+__host__ __device__ constexpr int act_floats(int F) {
+  (void)F;
+  return MB * kMaxF + MB + 2 * MB * H1 + 2 * MB * H2 + 2 * MB * H3 + MB + 64;
+}
+
+struct Views {
+  float *W1, *b1, *W2, *b2, *W3, *b3, *W4, *b4;
+};
+__device__ __forceinline__ Views views(float* base, int F) {
+  Views v;
+  v.W1 = base;
+  v.b1 = v.W1 + F * H1;
+  v.W2 = v.b1 + H1;
+  v.b2 = v.W2 + H1 * H2;
+  v.W3 = v.b2 + H2;
+  v.b3 = v.W3 + H2 * H3;
+  v.W4 = v.b3 + H3;
+  v.b4 = v.W4 + H3;
+  return v;
+}
+
+struct Acts {
+  float *xb, *yb, *h1, *d1, *h2, *d2, *h3, *d3, *d4, *red;
+};
+__device__ __forceinline__ Acts acts(float* base) {
+  Acts a;
+  a.xb = base;
+  a.yb = a.xb + MB * kMaxF;
+  a.h1 = a.yb + MB;
+  a.d1 = a.h1 + MB * H1;
+  a.h2 = a.d1 + MB * H1;
+  a.d2 = a.h2 + MB * H2;
+  a.h3 = a.d2 + MB * H2;
+  a.d3 = a.h3 + MB * H3;
+  a.d4 = a.d3 + MB * H3;
+  a.red = a.d4 + MB;
+  return a;
+}
+
+// Forward of one 32-row tile held in a.xb (rows >= bs are zero). Leaves ReLU outputs in h1/h2/h3
+// and the logits in d4 (overwritten by the backward pass in training).
+__device__ __forceinline__ void forward_tile(const Views& w, const Acts& a, int F) {
+  const int t = threadIdx.x;
+  {  // layer 1: thread -> hidden j, 16 rows
+    const int j = t & (H1 - 1), r0 = (t >> 7) * 16;
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = w.b1[j];
+    for (int k = 0; k < F; ++k) {
+      const float wk = w.W1[k * H1 + j];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = fmaf(a.xb[(r0 + i) * kMaxF + k], wk, acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a.h1[(r0 + i) * H1 + j] = fmaxf(acc[i], 0.0f);
+  }
+  __syncthreads();
+  {  // layer 2: thread -> j in 32, 4 rows
+    const int j = t & (H2 - 1), r0 = (t >> 5) * 4;
+    float acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = w.b2[j];
+    for (int k = 0; k < H1; ++k) {
+      const float wk = w.W2[k * H2 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = fmaf(a.h1[(r0 + i) * H1 + k], wk, acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a.h2[(r0 + i) * H2 + j] = fmaxf(acc[i], 0.0f);
+  }
+  __syncthreads();
+  {  // layer 3: thread -> j in 16, 2 rows
+    const int j = t & (H3 - 1), r0 = (t >> 4) * 2;
+    float acc[2] = {w.b3[j], w.b3[j]};
+    for (int k = 0; k < H2; ++k) {
+      const float wk = w.W3[k * H3 + j];
+      acc[0] = fmaf(a.h2[r0 * H2 + k], wk, acc[0]);
+      acc[1] = fmaf(a.h2[(r0 + 1) * H2 + k], wk, acc[1]);
+    }
+    a.h3[r0 * H3 + j] = fmaxf(acc[0], 0.0f);
+    a.h3[(r0 + 1) * H3 + j] = fmaxf(acc[1], 0.0f);
+  }
+  __syncthreads();
+  if (t < MB) {  // output logit
+    float z = w.b4[0];
+    for (int k = 0; k < H3; ++k) z = fmaf(a.h3[t * H3 + k], w.W4[k], z);
+    a.d4[t] = z;
+  }
+  __syncthreads();
+}
+
+struct AdamStep {
+  float lr, lr_t, wd, b1, b2, eps, l2;
+};
+
+__device__ __forceinline__ void adam(float* p, float* m, float* v, float g, bool reg, const AdamStep& s) {
+  float w = *p;
+  if (reg) g = fmaf(2.0f * s.l2, w, g);
+  w -= s.lr * s.wd * w;
+  float mm = *m, vv = *v;
+  mm += (g - mm) * (1.0f - s.b1);
+  vv += (g * g - vv) * (1.0f - s.b2);
+  w -= s.lr_t * mm / (sqrtf(vv) + s.eps);
+  *p = w;
+  *m = mm;
+  *v = vv;
+}
+
+__global__ __launch_bounds__(NT) void k_mlp_train(const float* __restrict__ X, int64_t ldx, const float* __restrict__ y,
+                                                  int64_t n, int F, const int32_t* __restrict__ perm,
+                                                  float* __restrict__ params, float* __restrict__ mom1,
+                                                  float* __restrict__ mom2, int64_t* __restrict__ steps,
+                                                  MlpHyper hp, float* __restrict__ loss_out) {
+  extern __shared__ float sm[];
+  const int P = mlp_params(F);
+  const int model = blockIdx.x;
+  const int t = threadIdx.x;
+  float* Wb = sm;
+  float* Mb = Wb + P;
+  float* Vb = Mb + P;
+  const Acts a = acts(Vb + P);
+  const Views w = views(Wb, F), m = views(Mb, F), v = views(Vb, F);
+  float* gp = params + (int64_t)model * P;
+  float* gm = mom1 + (int64_t)model * P;
+  float* gv = mom2 + (int64_t)model * P;
+  for (int i = t; i < P; i += NT) {
+    Wb[i] = gp[i];
+    Mb[i] = gm[i];
+    Vb[i] = gv[i];
+  }
+  for (int i = t; i < MB * kMaxF; i += NT) a.xb[i] = 0.0f;
+  int64_t step = steps[model];
+  const int32_t* pm = perm + (int64_t)model * n;
+  const int B = hp.batch;
+  const int64_t nb = (n + B - 1) / B;
+  float loss_acc = 0.0f;  // thread 0 only
+  __syncthreads();
+  for (int64_t b = 0; b < nb; ++b) {
+    const int bs = (int)min((int64_t)B, n - b * B);
+    for (int i = t; i < MB * F; i += NT) {
+      const int r = i / F, k = i - r * F;
+      a.xb[r * kMaxF + k] = r < bs ? X[(int64_t)pm[b * B + r] * ldx + k] : 0.0f;
+    }
+    if (t < MB) a.yb[t] = t < bs ? y[pm[b * B + t]] : 0.0f;
+    __syncthreads();
+    forward_tile(w, a, F);
+    // schedule + bias correction for this step
+    AdamStep s;
+    {
+      const float e = hp.staircase ? floorf((float)step / (float)hp.decay_steps) : (float)step / (float)hp.decay_steps;
+      s.lr = hp.lr0 * powf(hp.decay_rate, e);
+      const float tt = (float)(step + 1);
+      s.lr_t = s.lr * sqrtf(1.0f - powf(hp.beta2, tt)) / (1.0f - powf(hp.beta1, tt));
+      s.wd = hp.weight_decay;
+      s.b1 = hp.beta1;
+      s.b2 = hp.beta2;
+      s.eps = hp.eps;
+      s.l2 = hp.l2;
+    }
+    if (t < MB) {  // BCE from the logit; gradient (p - y) / bs
+      const float z = a.d4[t];
+      const float yy = a.yb[t];
+      const float p = 1.0f / (1.0f + expf(-z));
+      const float l = fmaxf(z, 0.0f) - z * yy + log1pf(expf(-fabsf(z)));
+      a.red[t] = t < bs ? l : 0.0f;
+      a.d4[t] = t < bs ? (p - yy) / (float)bs : 0.0f;
+    }
+    __syncthreads();
+    if (t == 0) {
+      float sl = 0.0f;
+      for (int r = 0; r < bs; ++r) sl += a.red[r];
+      loss_acc += sl / (float)bs;
+    }
+    // phase A: delta3 = d4 * W4 * relu'(h3)
+    for (int e = t; e < MB * H3; e += NT) {
+      const int r = e / H3, k = e - r * H3;
+      a.d3[e] = a.h3[e] > 0.0f ? a.d4[r] * w.W4[k] : 0.0f;
+    }
+    __syncthreads();
+    // phase B: update W4/b4; delta2 = (d3 W3^T) * relu'(h2)
+    if (t < H3) {
+      float g = 0.0f;
+      for (int r = 0; r < MB; ++r) g = fmaf(a.h3[r * H3 + t], a.d4[r], g);
+      adam(&w.W4[t], &m.W4[t], &v.W4[t], g, false, s);
+    } else if (t == H3) {
+      float g = 0.0f;
+      for (int r = 0; r < MB; ++r) g += a.d4[r];
+      adam(&w.b4[0], &m.b4[0], &v.b4[0], g, false, s);
+    }
+    for (int e = t; e < MB * H2; e += NT) {
+      const int r = e / H2, k = e - r * H2;
+      float acc = 0.0f;
+      if (a.h2[e] > 0.0f)
+        for (int j = 0; j < H3; ++j) acc = fmaf(a.d3[r * H3 + j], w.W3[k * H3 + j], acc);
+      a.d2[e] = acc;
+    }
+    __syncthreads();
+    // phase C: update W3/b3; delta1 = (d2 W2^T) * relu'(h1)
+    for (int e = t; e < H2 * H3 + H3; e += NT) {
+      if (e < H2 * H3) {
+        const int k = e / H3, j = e - k * H3;
+        float g = 0.0f;
+        for (int r = 0; r < MB; ++r) g = fmaf(a.h2[r * H2 + k], a.d3[r * H3 + j], g);
+        adam(&w.W3[e], &m.W3[e], &v.W3[e], g, true, s);
+      } else {
+        const int j = e - H2 * H3;
+        float g = 0.0f;
+        for (int r = 0; r < MB; ++r) g += a.d3[r * H3 + j];
+        adam(&w.b3[j], &m.b3[j], &v.b3[j], g, false, s);
+      }
+    }
+    for (int e = t; e < MB * H1; e += NT) {
+      const int r = e / H1, k = e - r * H1;
+      float acc = 0.0f;
+      if (a.h1[e] > 0.0f)
+        for (int j = 0; j < H2; ++j) acc = fmaf(a.d2[r * H2 + j], w.W2[k * H2 + j], acc);
+      a.d1[e] = acc;
+    }
+    __syncthreads();
+    // phase D: update W2/b2 and W1/b1
+    for (int e = t; e < H1 * H2 + H2; e += NT) {
+      if (e < H1 * H2) {
+        const int k = e / H2, j = e - k * H2;
+        float g = 0.0f;
+        for (int r = 0; r < MB; ++r) g = fmaf(a.h1[r * H1 + k], a.d2[r * H2 + j], g);
+        adam(&w.W2[e], &m.W2[e], &v.W2[e], g, true, s);
+      } else {
+        const int j = e - H1 * H2;
+        float g = 0.0f;
+        for (int r = 0; r < MB; ++r) g += a.d2[r * H2 + j];
+        adam(&w.b2[j], &m.b2[j], &v.b2[j], g, false, s);
+      }
+    }
+    for (int e = t; e < F * H1 + H1; e += NT) {
+      if (e < F * H1) {
+        const int k = e / H1, j = e - k * H1;
+        float g = 0.0f;
+        for (int r = 0; r < MB; ++r) g = fmaf(a.xb[r * kMaxF + k], a.d1[r * H1 + j], g);
+        adam(&w.W1[e], &m.W1[e], &v.W1[e], g, true, s);
+      } else {
+        const int j = e - F * H1;
+        float g = 0.0f;
+        for (int r = 0; r < MB; ++r) g += a.d1[r * H1 + j];
+        adam(&w.b1[j], &m.b1[j], &v.b1[j], g, false, s);
+      }
+    }
+    ++step;
+    __syncthreads();
+  }
+  for (int i = t; i < P; i += NT) {
+    gp[i] = Wb[i];
+    gm[i] = Mb[i];
+    gv[i] = Vb[i];
+  }
+  if (t == 0) {
+    steps[model] = step;
+    loss_out[model] = loss_acc;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_mlp_forward(const float* __restrict__ X, int64_t ldx, int64_t n, int F,
+                                                    const float* __restrict__ params, float* __restrict__ prob,
+                                                    float* __restrict__ logit) {
+  extern __shared__ float sm[];
+  const int P = mlp_params(F);
+  const int t = threadIdx.x;
+  float* Wb = sm;
+  const Acts a = acts(Wb + P);
+  const Views w = views(Wb, F);
+  for (int i = t; i < P; i += NT) Wb[i] = params[i];
+  for (int i = t; i < MB * kMaxF; i += NT) a.xb[i] = 0.0f;
+  __syncthreads();
+  const int64_t tiles = (n + MB - 1) / MB;
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * MB;
+    const int bs = (int)min((int64_t)MB, n - r0);
+    for (int i = t; i < MB * F; i += NT) {
+      const int r = i / F, k = i - r * F;
+      a.xb[r * kMaxF + k] = r < bs ? X[(r0 + r) * ldx + k] : 0.0f;
+    }
+    __syncthreads();
+    forward_tile(w, a, F);
+    if (t < bs) {
+      const float z = a.d4[t];
+      prob[r0 + t] = 1.0f / (1.0f + expf(-z));
+      if (logit) logit[r0 + t] = z;
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+COBALT_API int cobalt_mlp_num_params(int F) { return mlp_params(F); }
+
+COBALT_API int cobalt_mlp_train_epoch(const float* X, int64_t ldx, const float* y, int64_t n, int F,
+                                      const int32_t* perm, float* params, float* m, float* v, int64_t* steps,
+                                      const void* hyper, int n_models, float* loss_out, hipStream_t stream) {
+  if (F < 1 || F > kMaxF) return -1;
+  if (n < 1 || n_models < 1) return 0;
+  MlpHyper hp = *static_cast<const MlpHyper*>(hyper);
+  if (hp.batch < 1 || hp.batch > MB || hp.decay_steps < 1) return -2;
+  const size_t lds = ((size_t)3 * mlp_params(F) + act_floats(F)) * sizeof(float);
+  if (lds > 160 * 1024) return -3;
+  CK(hipFuncSetAttribute((const void*)k_mlp_train, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_mlp_train, dim3(n_models), dim3(NT), lds, stream, X, ldx, y, n, F, perm, params, m, v, steps,
+                     hp, loss_out);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_mlp_forward(const float* X, int64_t ldx, int64_t n, int F, const float* params, float* prob,
+                                  float* logit, hipStream_t stream) {
+  if (F < 1 || F > kMaxF) return -1;
+  if (n < 1) return 0;
+  const size_t lds = ((size_t)mlp_params(F) + act_floats(F)) * sizeof(float);
+  if (lds > 64 * 1024)
+    CK(hipFuncSetAttribute((const void*)k_mlp_forward, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int64_t tiles = (n + MB - 1) / MB;
+  const int grid = (int)std::min<int64_t>(tiles, 2048);
+  hipLaunchKernelGGL(k_mlp_forward, dim3(grid), dim3(NT), lds, stream, X, ldx, n, F, params, prob, logit);
+  CK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,1 @@
+"""NN challenger (notebook 04): fused MLP trainer/inference, SMOTE, MinMaxScaler."""
