@@ -24,7 +24,7 @@
 #include "common.h"
 
 namespace {
-constexpr int H1 = 128, H2 = 32, H3 = 16, MB = 32, NT = 256;
+constexpr int H1 = 128, H2 = 32, H3 = 16, MB = 32, NT = 1024;  // 16 waves: 4 per SIMD hide LDS latency
 constexpr int kMaxF = 32;
 
 struct MlpHyper {
@@ -36,6 +36,8 @@ struct MlpHyper {
   int32_t pad[2];
 };
 static_assert(sizeof(MlpHyper) == 48, "MlpHyper layout mirrored in nn/mlp.py");
+static_assert(NT == 1024, "forward_tile thread maps assume 1024 threads");
+static_assert(MB * kMaxF <= NT, "one batch element per thread");
 
 __host__ __device__ constexpr int mlp_params(int F) { return F * H1 + H1 + H1 * H2 + H2 + H2 * H3 + H3 + H3 + 1; }
 __host__ __device__ constexpr int act_floats(int F) {
@@ -81,44 +83,32 @@ __device__ __forceinline__ Acts acts(float* base) {
 // and the logits in d4 (overwritten by the backward pass in training).
 __device__ __forceinline__ void forward_tile(const Views& w, const Acts& a, int F) {
   const int t = threadIdx.x;
-  {  // layer 1: thread -> hidden j, 16 rows
-    const int j = t & (H1 - 1), r0 = (t >> 7) * 16;
-    float acc[16];
+  {  // layer 1: thread -> hidden j, 4 rows
+    const int j = t & (H1 - 1), r0 = (t >> 7) * 4;
+    float acc[4];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = w.b1[j];
+    for (int i = 0; i < 4; ++i) acc[i] = w.b1[j];
     for (int k = 0; k < F; ++k) {
       const float wk = w.W1[k * H1 + j];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = fmaf(a.xb[(r0 + i) * kMaxF + k], wk, acc[i]);
+      for (int i = 0; i < 4; ++i) acc[i] = fmaf(a.xb[(r0 + i) * kMaxF + k], wk, acc[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) a.h1[(r0 + i) * H1 + j] = fmaxf(acc[i], 0.0f);
+    for (int i = 0; i < 4; ++i) a.h1[(r0 + i) * H1 + j] = fmaxf(acc[i], 0.0f);
   }
   __syncthreads();
-  {  // layer 2: thread -> j in 32, 4 rows
-    const int j = t & (H2 - 1), r0 = (t >> 5) * 4;
-    float acc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = w.b2[j];
-    for (int k = 0; k < H1; ++k) {
-      const float wk = w.W2[k * H2 + j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = fmaf(a.h1[(r0 + i) * H1 + k], wk, acc[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a.h2[(r0 + i) * H2 + j] = fmaxf(acc[i], 0.0f);
+  {  // layer 2: thread -> (row, j)
+    const int j = t & (H2 - 1), r = t >> 5;
+    float acc = w.b2[j];
+    for (int k = 0; k < H1; ++k) acc = fmaf(a.h1[r * H1 + k], w.W2[k * H2 + j], acc);
+    a.h2[r * H2 + j] = fmaxf(acc, 0.0f);
   }
   __syncthreads();
-  {  // layer 3: thread -> j in 16, 2 rows
-    const int j = t & (H3 - 1), r0 = (t >> 4) * 2;
-    float acc[2] = {w.b3[j], w.b3[j]};
-    for (int k = 0; k < H2; ++k) {
-      const float wk = w.W3[k * H3 + j];
-      acc[0] = fmaf(a.h2[r0 * H2 + k], wk, acc[0]);
-      acc[1] = fmaf(a.h2[(r0 + 1) * H2 + k], wk, acc[1]);
-    }
-    a.h3[r0 * H3 + j] = fmaxf(acc[0], 0.0f);
-    a.h3[(r0 + 1) * H3 + j] = fmaxf(acc[1], 0.0f);
+  if (t < MB * H3) {  // layer 3: thread -> (row, j)
+    const int j = t & (H3 - 1), r = t >> 4;
+    float acc = w.b3[j];
+    for (int k = 0; k < H2; ++k) acc = fmaf(a.h2[r * H2 + k], w.W3[k * H3 + j], acc);
+    a.h3[r * H3 + j] = fmaxf(acc, 0.0f);
   }
   __syncthreads();
   if (t < MB) {  // output logit
@@ -150,10 +140,21 @@ __global__ __launch_bounds__(NT) void k_mlp_train(const float* __restrict__ X, i
                                                   int64_t n, int F, const int32_t* __restrict__ perm,
                                                   float* __restrict__ params, float* __restrict__ mom1,
                                                   float* __restrict__ mom2, int64_t* __restrict__ steps,
-                                                  MlpHyper hp, float* __restrict__ loss_out) {
+                                                  MlpHyper hp, float* __restrict__ loss_out,
+                                                  uint64_t* __restrict__ prof) {
   extern __shared__ float sm[];
   const int P = mlp_params(F);
   const int model = blockIdx.x;
+  // optional phase timer (thread 0 of model 0, s_memrealtime ticks): prof[0..6]
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph_last = 0;
+  const bool timing = prof != nullptr && model == 0 && threadIdx.x == 0;
+#define MLP_PHASE(i)                      \
+  if (timing) {                           \
+    const uint64_t now = wall_clock64();  \
+    ph[i] += now - ph_last;               \
+    ph_last = now;                        \
+  }
   const int t = threadIdx.x;
   float* Wb = sm;
   float* Mb = Wb + P;
@@ -175,15 +176,26 @@ __global__ __launch_bounds__(NT) void k_mlp_train(const float* __restrict__ X, i
   const int64_t nb = (n + B - 1) / B;
   float loss_acc = 0.0f;  // thread 0 only
   __syncthreads();
+  // Batch b + 1 is fetched into registers while step b computes (MB * F <= NT: one element per
+  // thread), hiding the dependent perm -> X global-load latency behind the step.
+  const int xr = t / F, xk = t - (t / F) * F;
+  auto fetch = [&](int64_t bb, float& xv, float& yv) {
+    const int bsz = (int)min((int64_t)B, n - bb * B);
+    xv = (t < MB * F && xr < bsz) ? X[(int64_t)pm[bb * B + xr] * ldx + xk] : 0.0f;
+    yv = (t < bsz) ? y[pm[bb * B + t]] : 0.0f;
+  };
+  float nx = 0.0f, ny = 0.0f;
+  if (nb > 0) fetch(0, nx, ny);
   for (int64_t b = 0; b < nb; ++b) {
     const int bs = (int)min((int64_t)B, n - b * B);
-    for (int i = t; i < MB * F; i += NT) {
-      const int r = i / F, k = i - r * F;
-      a.xb[r * kMaxF + k] = r < bs ? X[(int64_t)pm[b * B + r] * ldx + k] : 0.0f;
-    }
-    if (t < MB) a.yb[t] = t < bs ? y[pm[b * B + t]] : 0.0f;
+    if (t < MB * F) a.xb[xr * kMaxF + xk] = nx;
+    if (t < MB) a.yb[t] = ny;
+    if (timing) ph_last = wall_clock64();
     __syncthreads();
+    MLP_PHASE(0)
+    if (b + 1 < nb) fetch(b + 1, nx, ny);
     forward_tile(w, a, F);
+    MLP_PHASE(1)
     // schedule + bias correction for this step
     AdamStep s;
     {
@@ -211,12 +223,14 @@ __global__ __launch_bounds__(NT) void k_mlp_train(const float* __restrict__ X, i
       for (int r = 0; r < bs; ++r) sl += a.red[r];
       loss_acc += sl / (float)bs;
     }
+    MLP_PHASE(2)
     // phase A: delta3 = d4 * W4 * relu'(h3)
     for (int e = t; e < MB * H3; e += NT) {
       const int r = e / H3, k = e - r * H3;
       a.d3[e] = a.h3[e] > 0.0f ? a.d4[r] * w.W4[k] : 0.0f;
     }
     __syncthreads();
+    MLP_PHASE(3)
     // phase B: update W4/b4; delta2 = (d3 W3^T) * relu'(h2)
     if (t < H3) {
       float g = 0.0f;
@@ -230,11 +244,15 @@ __global__ __launch_bounds__(NT) void k_mlp_train(const float* __restrict__ X, i
     for (int e = t; e < MB * H2; e += NT) {
       const int r = e / H2, k = e - r * H2;
       float acc = 0.0f;
-      if (a.h2[e] > 0.0f)
-        for (int j = 0; j < H3; ++j) acc = fmaf(a.d3[r * H3 + j], w.W3[k * H3 + j], acc);
+      if (a.h2[e] > 0.0f)  // rotated j: lanes (consecutive k) hit different banks of the W3 rows
+        for (int jj = 0; jj < H3; ++jj) {
+          const int j = (jj + k) & (H3 - 1);
+          acc = fmaf(a.d3[r * H3 + j], w.W3[k * H3 + j], acc);
+        }
       a.d2[e] = acc;
     }
     __syncthreads();
+    MLP_PHASE(4)
     // phase C: update W3/b3; delta1 = (d2 W2^T) * relu'(h1)
     for (int e = t; e < H2 * H3 + H3; e += NT) {
       if (e < H2 * H3) {
@@ -252,11 +270,15 @@ __global__ __launch_bounds__(NT) void k_mlp_train(const float* __restrict__ X, i
     for (int e = t; e < MB * H1; e += NT) {
       const int r = e / H1, k = e - r * H1;
       float acc = 0.0f;
-      if (a.h1[e] > 0.0f)
-        for (int j = 0; j < H2; ++j) acc = fmaf(a.d2[r * H2 + j], w.W2[k * H2 + j], acc);
+      if (a.h1[e] > 0.0f)  // rotated j (see above): W2 rows are 32 floats apart
+        for (int jj = 0; jj < H2; ++jj) {
+          const int j = (jj + k) & (H2 - 1);
+          acc = fmaf(a.d2[r * H2 + j], w.W2[k * H2 + j], acc);
+        }
       a.d1[e] = acc;
     }
     __syncthreads();
+    MLP_PHASE(5)
     // phase D: update W2/b2 and W1/b1
     for (int e = t; e < H1 * H2 + H2; e += NT) {
       if (e < H1 * H2) {
@@ -286,7 +308,11 @@ __global__ __launch_bounds__(NT) void k_mlp_train(const float* __restrict__ X, i
     }
     ++step;
     __syncthreads();
+    MLP_PHASE(6)
   }
+#undef MLP_PHASE
+  if (timing)
+    for (int i = 0; i < 7; ++i) prof[i] += ph[i];
   for (int i = t; i < P; i += NT) {
     gp[i] = Wb[i];
     gm[i] = Mb[i];
@@ -334,7 +360,8 @@ COBALT_API int cobalt_mlp_num_params(int F) { return mlp_params(F); }
 
 COBALT_API int cobalt_mlp_train_epoch(const float* X, int64_t ldx, const float* y, int64_t n, int F,
                                       const int32_t* perm, float* params, float* m, float* v, int64_t* steps,
-                                      const void* hyper, int n_models, float* loss_out, hipStream_t stream) {
+                                      const void* hyper, int n_models, float* loss_out, uint64_t* prof,
+                                      hipStream_t stream) {
   if (F < 1 || F > kMaxF) return -1;
   if (n < 1 || n_models < 1) return 0;
   MlpHyper hp = *static_cast<const MlpHyper*>(hyper);
@@ -343,7 +370,7 @@ COBALT_API int cobalt_mlp_train_epoch(const float* X, int64_t ldx, const float* 
   if (lds > 160 * 1024) return -3;
   CK(hipFuncSetAttribute((const void*)k_mlp_train, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_mlp_train, dim3(n_models), dim3(NT), lds, stream, X, ldx, y, n, F, perm, params, m, v, steps,
-                     hp, loss_out);
+                     hp, loss_out, prof);
   CK_LAUNCH();
   return 0;
 }

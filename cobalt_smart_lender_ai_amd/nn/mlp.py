@@ -96,7 +96,7 @@ _native.register("cobalt_mlp_num_params", ctypes.c_int, [ctypes.c_int])
 _native.register("cobalt_mlp_train_epoch", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                  ctypes.c_void_p, ctypes.c_void_p])
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
 _native.register("cobalt_mlp_forward", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_void_p])
@@ -278,7 +278,7 @@ def fit_many(X_train, y_train, X_val=None, y_val=None, cfg: MLPConfig | None = N
             permd = torch.as_tensor(perms, device=dev)
             rc = lib.cobalt_mlp_train_epoch(Xd.data_ptr(), F, yd.data_ptr(), N, F, permd.data_ptr(), pd_.data_ptr(),
                                             md.data_ptr(), vd.data_ptr(), steps.data_ptr(), ctypes.byref(hp), G,
-                                            loss.data_ptr(), _native.stream_handle())
+                                            loss.data_ptr(), None, _native.stream_handle())
             _native.check(rc, "cobalt_mlp_train_epoch")
             losses = (loss / nb).cpu().numpy()
             cur = pd_.cpu().numpy()
