@@ -43,6 +43,7 @@ _SIGS: dict[str, tuple] = {
     "cobalt_gbdt_grow": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "cobalt_gbdt_fetch_trees": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "cobalt_gbdt_max_nodes": (c_int, [c_void_p]),
+    "cobalt_gbdt_set_start": (c_int, [c_void_p, c_int]),
     "cobalt_gbdt_destroy": (c_int, [c_void_p]),
     "cobalt_bin_matrix": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int,
                                   c_void_p, c_void_p]),

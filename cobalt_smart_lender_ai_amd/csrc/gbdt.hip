@@ -1097,6 +1097,17 @@ COBALT_API int cobalt_gbdt_fetch_trees(void* h, int t0, int n, void* host_out, h
 
 COBALT_API int cobalt_gbdt_max_nodes(void* h) { return static_cast<GbdtCtx*>(h)->max_nodes; }
 
+// Resume: the margins passed to set_data already contain trees [0, t0) (re-predicted from a
+// checkpoint); boosting continues at global tree index t0, so row sampling and column masks -- both
+// keyed by the global tree index -- follow the uninterrupted run exactly.
+COBALT_API int cobalt_gbdt_set_start(void* h, int t0) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  if (t0 < 0 || t0 > c->cfg.max_trees || c->grown != 0) return -12;
+  c->grown = t0;
+  c->applied = t0;
+  return 0;
+}
+
 COBALT_API int cobalt_gbdt_destroy(void* h) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   if (!c) return 0;

@@ -16,7 +16,10 @@ histogram trees (K14-K20). See ``csrc/gbdt.hip`` for the device design.
 """
 from __future__ import annotations
 
+import json
+import logging
 import math
+import os
 import time
 from dataclasses import asdict, dataclass, field
 from typing import Any, Sequence
@@ -26,6 +29,8 @@ import torch
 
 from . import gbdt_host, sketch
 from .booster import Booster, dump_pickle_bytes, sigmoid32, trees_from_heap_nodes
+
+log = logging.getLogger(__name__)
 
 XGB_DEFAULTS = dict(n_estimators=100, max_depth=6, learning_rate=0.3, gamma=0.0, min_child_weight=1.0,
                     reg_lambda=1.0, reg_alpha=0.0, subsample=1.0, colsample_bytree=1.0, max_bin=256,
@@ -186,18 +191,43 @@ def subset_rows(bd: BinnedData, rows: np.ndarray) -> BinnedData:
 def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, device=None,
           feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
           dist=None, n_rows_global: int | None = None, row_offset: int = 0,
-          report: FitReport | None = None) -> Booster:
+          report: FitReport | None = None, init_booster: Booster | None = None,
+          checkpoint_path: str | None = None, checkpoint_every: int = 0, resume: bool = True) -> Booster:
     """Fit a binary:logistic GBDT. With ``dist`` (a :class:`~..parallel.dist.DistContext`) each rank
-    passes its local row shard (``row_offset`` = global index of its first row)."""
+    passes its local row shard (``row_offset`` = global index of its first row).
+
+    ``init_booster`` continues boosting from an existing model for ``n_estimators`` MORE trees
+    (XGBoost's ``xgb_model=``). ``checkpoint_path`` + ``checkpoint_every`` write the model every that
+    many trees (atomic replace, rank 0); with ``resume`` an existing checkpoint there is loaded and
+    training continues to ``n_estimators`` trees in total -- bit-identical to an uninterrupted fit,
+    because sampling is keyed by the global tree index and the margins are re-predicted in tree order."""
     if params is None:
         params = GBDTParams()
     elif isinstance(params, dict):
         params = GBDTParams.from_kwargs(**params)
     t0 = time.perf_counter()
+    ckpt = Checkpointer(checkpoint_path, checkpoint_every, params, dist) if checkpoint_path else None
+    total = None
+    if ckpt is not None and resume and init_booster is None:
+        init_booster = ckpt.load()
+        if init_booster is not None:
+            total = int(params.n_estimators)
+            log.info("resuming from %s at tree %d of %d", checkpoint_path, init_booster.num_trees, total)
+    dev = _resolve_device(device, X)
+    init_margin = None
+    if init_booster is not None:
+        from ..ops import predict_ops
+
+        Xt = _to_tensor(X, dev)
+        init_margin = predict_ops.predict_margin(init_booster, Xt, dev)
+        if not isinstance(init_margin, torch.Tensor):
+            init_margin = torch.as_tensor(init_margin)
+        init_margin = init_margin.to(dev, torch.float32).contiguous()
     bd = bin_dataset(X, max_bin=params.max_bin, sketch_rows=params.sketch_rows, device=device, dist=dist,
                      n_rows_global=n_rows_global, row_offset=row_offset)
     bst = train_binned(bd, y, params, sample_weight=sample_weight, feature_names=feature_names,
-                       feature_types=feature_types, dist=dist, report=report)
+                       feature_types=feature_types, dist=dist, report=report, init_booster=init_booster,
+                       init_margin=init_margin, total_trees=total, checkpoint=ckpt)
     if report is not None:
         report.t_total = time.perf_counter() - t0
     return bst
@@ -205,9 +235,13 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
 
 def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, sample_weight=None,
                  feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
-                 feature_mask: np.ndarray | None = None, dist=None, report: FitReport | None = None) -> Booster:
+                 feature_mask: np.ndarray | None = None, dist=None, report: FitReport | None = None,
+                 init_booster: Booster | None = None, init_margin: torch.Tensor | None = None,
+                 total_trees: int | None = None, checkpoint: "Checkpointer | None" = None) -> Booster:
     """Boost on pre-binned data. ``feature_mask`` (bool [F]) restricts the fit to a feature subset
-    (the trees still index the full feature space, so a subset fit costs no re-binning)."""
+    (the trees still index the full feature space, so a subset fit costs no re-binning).
+    ``init_booster`` + ``init_margin`` (its margins on these rows) continue an existing model: grow
+    ``total_trees - init_booster.num_trees`` trees (default ``n_estimators`` more)."""
     if params is None:
         params = GBDTParams()
     elif isinstance(params, dict):
@@ -225,8 +259,13 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     wt = wt * torch.where(yt == 1.0, torch.tensor(spw, device=dev), torch.tensor(1.0, device=dev))
     wt = wt.to(torch.float32).contiguous()
 
+    T0 = init_booster.num_trees if init_booster is not None else 0
+    if init_booster is not None and init_margin is None:
+        raise ValueError("init_booster needs init_margin (its margins on the training rows)")
     # base score = weighted label mean (XGBoost boost_from_average for binary:logistic)
-    if params.base_score is None:
+    if init_booster is not None:
+        base_score = float(init_booster.base_score)
+    elif params.base_score is None:
         sw = float(wt.double().sum())
         swy = float((wt.double() * yt.double()).sum())
         if world > 1:
@@ -243,7 +282,10 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         wmax = dist.allreduce_scalar(wmax, "max", dev)
     gscale, hscale = gbdt_host.quant_scales(wmax)
 
-    T = int(params.n_estimators)
+    T_new = (int(total_trees) - T0) if total_trees is not None else int(params.n_estimators)
+    if T_new < 0:
+        raise ValueError("the initial model already has more trees than requested")
+    T = T0 + T_new  # global tree indices [T0, T) are grown; masks/RNG are keyed by the global index
     fmask_np = feature_masks(T, F, float(params.colsample_bytree), int(params.random_state))
     if feature_mask is not None:
         fm_sub = np.asarray(feature_mask, dtype=bool)
@@ -251,6 +293,30 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         fmask_np = np.zeros((T, F), dtype=np.uint8)
         sub = feature_masks(T, len(active), float(params.colsample_bytree), int(params.random_state))
         fmask_np[:, active] = sub
+    seg = checkpoint.every if checkpoint is not None and checkpoint.every > 0 else max(T_new, 1)
+    trees_so_far = list(init_booster.trees) if init_booster is not None else []
+    names = list(feature_names) if feature_names is not None else (
+        list(init_booster.feature_names) if init_booster is not None and init_booster.feature_names else None)
+    ftypes = list(feature_types) if feature_types is not None else (
+        list(init_booster.feature_types) if init_booster is not None and init_booster.feature_types else None)
+
+    def make_booster(trees):
+        return Booster(trees=list(trees), feature_names=names, feature_types=ftypes, base_score=base_score,
+                       num_feature=F,
+                       train_params=dict(eta=hp.eta, gamma=hp.gamma, max_depth=hp.max_depth,
+                                         min_child_weight=hp.min_child_weight, reg_lambda=hp.reg_lambda,
+                                         reg_alpha=hp.reg_alpha, subsample=hp.subsample,
+                                         colsample_bytree=float(params.colsample_bytree),
+                                         max_bin=int(params.max_bin), scale_pos_weight=spw, seed=hp.seed))
+
+    def segment_done(new_nodes: np.ndarray, end: int) -> None:
+        trees_so_far.extend(trees_from_heap_nodes(new_nodes, hp.max_depth))
+        if checkpoint is not None:
+            checkpoint.save(make_booster(trees_so_far))
+        fault_after = int(os.environ.get("COBALT_FAULT_AFTER_TREES", "0") or 0)
+        fault_rank = int(os.environ.get("COBALT_FAULT_RANK", "-1") or -1)
+        if fault_after and end >= fault_after and end < T and (fault_rank < 0 or fault_rank == (dist.rank if dist else 0)):
+            raise InjectedFault(f"injected fault after tree {end}")
     hp = gbdt_host.HostGbdtParams(max_depth=int(params.max_depth), eta=float(params.learning_rate),
                                   reg_lambda=float(params.reg_lambda), reg_alpha=float(params.reg_alpha),
                                   gamma=float(params.gamma), min_child_weight=float(params.min_child_weight),
@@ -261,7 +327,8 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     if dev.type == "cuda":
         from ..ops import gbdt_ops
 
-        margin = torch.full((N,), base_margin, dtype=torch.float32, device=dev)
+        margin = (init_margin.to(dev, torch.float32).clone().contiguous() if init_margin is not None
+                  else torch.full((N,), base_margin, dtype=torch.float32, device=dev))
         comm = dist.native_comm if (dist is not None and world > 1) else None
         if world > 1 and comm is None:
             raise RuntimeError("data-parallel GPU training needs the native RCCL communicator")
@@ -274,15 +341,23 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         tr.set_data(bd.records, bd.binsT, bd.cuts.contiguous(), bd.nbins.to(torch.int32).contiguous(),
                     yt.contiguous(), wt, margin, fm)
         tp = rep.mark("trainer_setup", tp, dev)
-        tr.grow(0, T)
-        tp = rep.mark("grow", tp, dev)
-        nodes = tr.fetch(0, T)
-        tr.close()
-        tp = rep.mark("fetch", tp, dev)
+        try:
+            if T0:
+                tr.set_start(T0)
+            for s0 in range(T0, T, seg):
+                s1 = min(T, s0 + seg)
+                tr.grow(s0, s1 - s0)
+                tp = rep.mark("grow", tp, dev)
+                seg_nodes = tr.fetch(s0, s1 - s0)
+                tp = rep.mark("fetch", tp, dev)
+                segment_done(seg_nodes, s1)
+        finally:
+            tr.close()
     else:
         cuts_np = bd.cuts.cpu().numpy()
         nb_np = bd.nbins.cpu().numpy()
-        margin_np = np.full(N, np.float32(base_margin), dtype=np.float32)
+        margin_np = (init_margin.cpu().numpy().astype(np.float32).copy() if init_margin is not None
+                     else np.full(N, np.float32(base_margin), dtype=np.float32))
         y_np = yt.cpu().numpy()
         w_np = wt.cpu().numpy()
         allreduce = None
@@ -291,25 +366,18 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                 t = torch.from_numpy(np.ascontiguousarray(a))
                 dist.allreduce(t, "sum")
                 return t.numpy()
-        recs = []
-        for t in range(T):
-            gq, hq = gbdt_host.gradients_host(margin_np, y_np, w_np, hp, t, bd.row_offset)
-            recs.append(gbdt_host.grow_tree_host(bd.bins_host, cuts_np, nb_np, gq, hq, margin_np, hp, fmask_np[t],
-                                                 allreduce))
-        nodes = np.stack(recs) if recs else np.zeros((0, (1 << (hp.max_depth + 1)) - 1),
-                                                      dtype=gbdt_host.NODE_DTYPE)
+        for s0 in range(T0, T, seg):
+            s1 = min(T, s0 + seg)
+            recs = []
+            for t in range(s0, s1):
+                gq, hq = gbdt_host.gradients_host(margin_np, y_np, w_np, hp, t, bd.row_offset)
+                recs.append(gbdt_host.grow_tree_host(bd.bins_host, cuts_np, nb_np, gq, hq, margin_np, hp,
+                                                     fmask_np[t], allreduce))
+            segment_done(np.stack(recs), s1)
         rep.extra["margin"] = margin_np
     t_boost = time.perf_counter() - tb
-    trees = trees_from_heap_nodes(nodes, hp.max_depth)
     tp = rep.mark("to_trees", tp, dev)
-    names = list(feature_names) if feature_names is not None else None
-    ftypes = list(feature_types) if feature_types is not None else None
-    bst = Booster(trees=trees, feature_names=names, feature_types=ftypes, base_score=base_score, num_feature=F,
-                  train_params=dict(eta=hp.eta, gamma=hp.gamma, max_depth=hp.max_depth,
-                                    min_child_weight=hp.min_child_weight, reg_lambda=hp.reg_lambda,
-                                    reg_alpha=hp.reg_alpha, subsample=hp.subsample,
-                                    colsample_bytree=float(params.colsample_bytree), max_bin=int(params.max_bin),
-                                    scale_pos_weight=spw, seed=hp.seed))
+    bst = make_booster(trees_so_far)
     if report is not None:
         report.n_rows, report.n_rows_global, report.n_features, report.n_trees = N, bd.n_rows_global, F, T
         report.device, report.world = str(dev), world
@@ -317,6 +385,55 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         report.extra["cuts"] = bd.cuts
         report.extra["nbins"] = bd.nbins
     return bst
+
+
+class InjectedFault(RuntimeError):
+    """Raised by the fault-injection hook (``COBALT_FAULT_AFTER_TREES`` [+ ``COBALT_FAULT_RANK``])."""
+
+
+class Checkpointer:
+    """Periodic model checkpoints of a fit (checkpoint-per-N-trees + resume).
+
+    The checkpoint is the XGBoost UBJSON model of the trees grown so far (loadable by any consumer
+    of the format) plus a JSON sidecar with the fit parameters; both are replaced atomically
+    (write + ``os.replace``). Only rank 0 writes under data parallelism; every rank reads on resume."""
+
+    def __init__(self, path: str, every: int, params: GBDTParams, dist=None):
+        self.path = str(path)
+        self.every = int(every)
+        self.params = params
+        self.rank = dist.rank if dist is not None else 0
+
+    def _meta(self, n_trees: int) -> dict:
+        keys = ("max_depth", "learning_rate", "gamma", "min_child_weight", "reg_lambda", "reg_alpha", "subsample",
+                "colsample_bytree", "max_bin", "scale_pos_weight", "random_state", "n_estimators")
+        return {"n_trees": n_trees, "params": {k: getattr(self.params, k) for k in keys}}
+
+    def save(self, booster: Booster) -> None:
+        if self.rank != 0:
+            return
+        tmp = self.path + ".tmp"
+        with open(tmp, "wb") as fh:
+            fh.write(booster.save_raw("ubj"))
+        os.replace(tmp, self.path)
+        with open(tmp + ".json", "w") as fh:
+            json.dump(self._meta(booster.num_trees), fh)
+        os.replace(tmp + ".json", self.path + ".json")
+
+    def load(self) -> Booster | None:
+        if not os.path.exists(self.path):
+            return None
+        meta_p = self.path + ".json"
+        if os.path.exists(meta_p):
+            with open(meta_p) as fh:
+                meta = json.load(fh)
+            want = self._meta(meta["n_trees"])["params"]
+            diff = {k: (meta["params"].get(k), v) for k, v in want.items()
+                    if k != "n_estimators" and meta["params"].get(k) != v}
+            if diff:
+                raise ValueError(f"checkpoint {self.path} was written with different parameters: {diff}")
+        with open(self.path, "rb") as fh:
+            return Booster.load_raw(fh.read())
 
 
 def _feature_info(X) -> tuple[list[str] | None, list[str] | None]:
@@ -389,8 +506,26 @@ class GBDTClassifier:
         kw = {k: v for k, v in self.get_params().items() if v is not None}
         return GBDTParams.from_kwargs(**{k: v for k, v in {**XGB_DEFAULTS, **kw}.items()})
 
-    def fit(self, X, y, sample_weight=None, **_):
+    def fit(self, X, y, sample_weight=None, xgb_model=None, **_):
+        """``xgb_model`` (a Booster, a fitted classifier or a model/pickle path) continues boosting
+        from that model for ``n_estimators`` more trees, as XGBoost's ``fit(xgb_model=...)``."""
         names, types = _feature_info(X)
+        init = None
+        if xgb_model is not None:
+            if isinstance(xgb_model, Booster):
+                init = xgb_model
+            elif hasattr(xgb_model, "get_booster"):
+                init = xgb_model.get_booster()
+            else:
+                from pathlib import Path
+
+                raw = Path(xgb_model).read_bytes()
+                if raw[:1] == b"\x80":
+                    from .booster import load_pickle_bytes
+
+                    init = load_pickle_bytes(raw)[1]
+                else:
+                    init = Booster.load_raw(raw)
         y_np = np.asarray(y.to_numpy() if hasattr(y, "to_numpy") else y).reshape(-1)
         self.classes_ = np.unique(y_np)
         if len(self.classes_) > 2:
@@ -399,7 +534,7 @@ class GBDTClassifier:
         yb = (y_np == self.classes_[-1]).astype(np.float32) if len(self.classes_) == 2 else y_np.astype(np.float32)
         rep = FitReport()
         self._Booster = train(X, yb, self._train_params(), sample_weight=sample_weight, device=self.device,
-                              feature_names=names, feature_types=types, report=rep)
+                              feature_names=names, feature_types=types, report=rep, init_booster=init)
         self.fit_report_ = rep
         self.n_features_in_ = self._Booster.num_feature
         if names is not None:

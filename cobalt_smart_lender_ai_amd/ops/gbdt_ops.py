@@ -129,6 +129,10 @@ class GpuGbdtTrainer:
         rc = self.lib.cobalt_gbdt_set_data(self.h, *[t.data_ptr() for t in ts])
         _native.check(rc, "cobalt_gbdt_set_data")
 
+    def set_start(self, t0: int) -> None:
+        """Continue boosting at global tree index ``t0`` (margins already hold trees < t0)."""
+        _native.check(self.lib.cobalt_gbdt_set_start(self.h, t0), "cobalt_gbdt_set_start")
+
     def grow(self, t0: int, n_trees: int) -> None:
         rc = self.lib.cobalt_gbdt_grow(self.h, t0, n_trees, _native.stream_handle())
         if rc != 0 and self.cfg.comm:

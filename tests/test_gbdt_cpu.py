@@ -117,3 +117,32 @@ def test_data_parallel_gloo_matches_single_process(tmp_path):
     dp = Booster.load_raw((tmp_path / "dp.ubj").read_bytes())
     np.testing.assert_array_equal(predict_margin_host(dp, X), predict_margin_host(ref, X))
     assert dp.save_raw("ubj") == ref.save_raw("ubj")
+
+
+# ------------------------------------------------------------------------------ checkpoint / resume
+def test_checkpoint_resume_after_injected_fault_is_bit_identical(tmp_path, monkeypatch):
+    X, y = _data(seed=4)
+    params = {**PARAMS, "n_estimators": 9, "subsample": 0.8, "colsample_bytree": 0.5}
+    ref = gbdt.train(X, y, params, device="cpu")
+    ck = str(tmp_path / "ckpt.ubj")
+    monkeypatch.setenv("COBALT_FAULT_AFTER_TREES", "5")
+    with pytest.raises(gbdt.InjectedFault):
+        gbdt.train(X, y, params, device="cpu", checkpoint_path=ck, checkpoint_every=3)
+    assert Booster.load_raw(open(ck, "rb").read()).num_trees == 6
+    monkeypatch.delenv("COBALT_FAULT_AFTER_TREES")
+    resumed = gbdt.train(X, y, params, device="cpu", checkpoint_path=ck, checkpoint_every=3)
+    assert resumed.num_trees == 9
+    assert resumed.save_raw("ubj") == ref.save_raw("ubj")
+    # a checkpoint written with other parameters is refused
+    with pytest.raises(ValueError):
+        gbdt.train(X, y, {**params, "max_depth": 3}, device="cpu", checkpoint_path=ck, checkpoint_every=3)
+
+
+def test_continue_training_from_model_equals_longer_fit():
+    X, y = _data(seed=5)
+    p8 = {**PARAMS, "n_estimators": 8, "subsample": 0.9}
+    full = gbdt.train(X, y, p8, device="cpu")
+    first = gbdt.train(X, y, {**p8, "n_estimators": 5}, device="cpu")
+    clf = gbdt.GBDTClassifier(device="cpu", **{**p8, "n_estimators": 3})
+    clf.fit(X, y, xgb_model=first)
+    assert clf.get_booster().save_raw("ubj") == full.save_raw("ubj")

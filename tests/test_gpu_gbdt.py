@@ -111,3 +111,21 @@ def test_gpu_auc_parity_with_cpu_oracle():
     ac = roc_auc(yte, bc.predict_proba(Xte.numpy(), device="cpu"))
     assert abs(ag - ac) <= 0.002
     assert ag > 0.9
+
+
+def test_gpu_checkpoint_resume_bit_identical(tmp_path, monkeypatch):
+    X, y = _data(300_000, seed=9)
+    params = dict(n_estimators=12, max_depth=6, learning_rate=0.1, gamma=1.0, subsample=0.8, colsample_bytree=0.8,
+                  random_state=3, scale_pos_weight=4.0)
+    ref = gbdt.train(X, y, params, device="cuda")
+    ck = str(tmp_path / "ck.ubj")
+    monkeypatch.setenv("COBALT_FAULT_AFTER_TREES", "7")
+    with pytest.raises(gbdt.InjectedFault):
+        gbdt.train(X, y, params, device="cuda", checkpoint_path=ck, checkpoint_every=4)
+    monkeypatch.delenv("COBALT_FAULT_AFTER_TREES")
+    resumed = gbdt.train(X, y, params, device="cuda", checkpoint_path=ck, checkpoint_every=4)
+    assert resumed.save_raw("ubj") == ref.save_raw("ubj")
+    # xgb_model-style continuation: 5 + 7 trees == 12 trees
+    first = gbdt.train(X, y, {**params, "n_estimators": 5}, device="cuda")
+    cont = gbdt.GBDTClassifier(device="cuda", **{**params, "n_estimators": 7}).fit(X, y, xgb_model=first)
+    assert cont.get_booster().save_raw("ubj") == ref.save_raw("ubj")
