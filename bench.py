@@ -8,9 +8,11 @@ binary:logistic, 20 features). One step = one complete fit (quantile sketch + bi
 boosting rounds + model fetch), i.e. BASELINE.md's ``rows_per_s = N_train_rows / wall_seconds(fit)``.
 
 Data: synthetic LendingClub-shaped rows (no dataset download is possible) generated on each GPU for
-its own shard by global row index, so the global dataset is identical for any GPU count. Scaling
-mode "strong" (default) keeps the 10M global rows fixed and shards them over the ranks; "weak"
-gives every rank 10M rows.
+its own shard by global row index. Scaling mode "weak" (default) gives every rank a 10M-row shard
+(N GPUs train one model on N x 10M rows: per-GPU work fixed, sized for 288 GB HBM -- the
+data-parallel deployment shape); "strong" keeps 10M global rows and shards them over the ranks.
+Strong scaling of a 300-tree x 7-level boosting run is bounded by its 2,100 sequential level steps
+(each needs two collectives under DP), see docs/PERF.md for both curves.
 
 Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
 Rank 0 prints one JSON line.
@@ -37,7 +39,7 @@ def main() -> None:
     ap.add_argument("--test-rows", type=int, default=1_000_000)
     ap.add_argument("--trees", type=int, default=300)
     ap.add_argument("--depth", type=int, default=7)
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--profile-fit", action="store_true", help="print per-phase timings to stderr")
     a = ap.parse_args()
@@ -116,8 +118,10 @@ def main() -> None:
             "precision": "fp32 features, fp64 gradients, exact int64 fixed-point histogram sums",
             "data": "synthetic LendingClub-shaped (20 deployed features, 12.9% positives), generated on device",
             "config": {
-                "model": "GBDT binary:logistic, 300 trees depth 7 eta 0.05 gamma 5 lambda 1 max_bin 256 spw=neg/pos",
+                "model": f"GBDT binary:logistic, {a.trees} trees depth {a.depth} eta 0.05 gamma 5 lambda 1 max_bin 256 "
+                         "spw=neg/pos",
                 "global_batch": n_global,
+                "rows_per_gpu": end - start,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "n_features": len(synth.FEATURES),

@@ -107,19 +107,20 @@ struct GbdtDev {
   int32_t* ridx[2];       // [N] x2
   int64_t* hist_b[2];     // [pairs][F+1][256][2]
   int64_t* hist_s[2];
-  Node* nodes;            // [max_nodes]
+  Node* nodes;            // [max_nodes] the tree being grown (one of nodes_buf, alternating per tree)
+  Node* prev_nodes;       // [max_nodes] the previous tree (the other buffer), applied + archived by k_grad
+  Node* nodes_buf[2];
   Node* trees;            // [max_trees][max_nodes]
-  WorkItem* items_h;      // histogram work list
-  WorkItem* items_p;      // partition work list
-  int32_t* counters;      // [0] = #hist items, [1] = #partition items
+  WorkItem* items_h;      // histogram work list (written by the histogram blocks for the reduce pass)
+  int32_t* counters;      // [0] = #hist items of the current level
   int32_t* cursors;       // [max_nodes][2]
-  int32_t* item_left;     // [items] left-row count per partition work item
   int2* layout;           // [F] histogram LDS layout: x = cell offset within tile, y = log2(copies)
   int32_t* tile_entries;  // [n_tiles] LDS cells per feature tile
   int32_t* child_cnt;     // [2*max_nodes] all-reduced copy of the partition cursors (DP only)
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush
+  int32_t dp;             // data parallel: partition also accumulates child_cnt for the all-reduce
   int64_t n;
   int64_t row_offset;
   int32_t F, stride, max_depth, max_nodes, chunk, feat_tile;
@@ -179,7 +180,8 @@ __global__ __launch_bounds__(256) void k_bin(const float* __restrict__ X, int64_
 // ------------------------------------------------------------------------------------------
 // Per-tree initialisation + binary:logistic gradients (K14)
 // ------------------------------------------------------------------------------------------
-__global__ void k_init_tree(GbdtDev d) {
+// Reset the node table of a new tree (root active with all local rows) and the per-node counters.
+__device__ void init_tree_block(const GbdtDev& d) {
   for (int i = threadIdx.x; i < d.max_nodes; i += blockDim.x) {
     Node nd = {};
     if (i == 0) {
@@ -193,13 +195,14 @@ __global__ void k_init_tree(GbdtDev d) {
     d.nodes[i] = nd;
     d.cursors[2 * i] = 0;
     d.cursors[2 * i + 1] = 0;
+    d.child_cnt[2 * i] = 0;
+    d.child_cnt[2 * i + 1] = 0;
   }
 }
 
 // Stage tree `t` (heap-ordered node records) into LDS as {meta, leaf value}:
 // meta = feat | bin << 16 | default_left << 24 | is_split << 25.
-__device__ __forceinline__ void stage_tree(const GbdtDev& d, int t, uint32_t* s_meta, float* s_leaf) {
-  const Node* tr = d.trees + (int64_t)t * d.max_nodes;
+__device__ __forceinline__ void stage_tree(const GbdtDev& d, const Node* tr, uint32_t* s_meta, float* s_leaf) {
   for (int i = threadIdx.x; i < d.max_nodes; i += blockDim.x) {
     const Node nd = tr[i];
     const uint32_t split = nd.status == kSplit ? 1u : 0u;
@@ -240,9 +243,15 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
   uint32_t* s_meta = s_tree;
   float* s_leaf = reinterpret_cast<float*>(s_tree + d.max_nodes);
   if (apply_tree >= 0) {
-    stage_tree(d, apply_tree, s_meta, s_leaf);
+    stage_tree(d, d.prev_nodes, s_meta, s_leaf);
+    // archive the previous tree (its node table is the other buffer, untouched by this tree)
+    const int4* src = reinterpret_cast<const int4*>(d.prev_nodes);
+    int4* dst = reinterpret_cast<int4*>(d.trees + (int64_t)apply_tree * d.max_nodes);
+    const int nv = d.max_nodes * (int)(sizeof(Node) / sizeof(int4));
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nv; e += gridDim.x * blockDim.x) dst[e] = src[e];
     __syncthreads();
   }
+  if (blockIdx.x == 0) init_tree_block(d);  // the new tree's node table (no other block reads it)
   const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
   const bool rec32 = d.stride == 32 && d.F <= 24;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n;
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
   extern __shared__ uint32_t s_tree[];
   uint32_t* s_meta = s_tree;
   float* s_leaf = reinterpret_cast<float*>(s_tree + d.max_nodes);
-  stage_tree(d, t, s_meta, s_leaf);
+  stage_tree(d, d.trees + (int64_t)t * d.max_nodes, s_meta, s_leaf);
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -315,113 +324,105 @@ __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
 // emit histogram work items. One block; work items are emitted by all threads in parallel.
 // ------------------------------------------------------------------------------------------
 // Exclusive scan of v[0..n) (n <= 1024) in LDS by a 256-thread block; returns the total.
-__device__ int block_excl_scan_1024(int32_t* v, int n, int32_t* s_wave) {
-  // each thread owns 4 consecutive entries
-  const int t = threadIdx.x;
-  int a[4], tot = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = t * 4 + k;
-    a[k] = i < n ? v[i] : 0;
-    tot += a[k];
-  }
-  const int incl = wave_incl_scan(tot);
-  if (lane_id() == kWave - 1) s_wave[wave_id()] = incl;
-  __syncthreads();
-  int wbase = 0, all = 0;
-  for (int w = 0; w < (int)(blockDim.x / kWave); ++w) {
-    if (w < wave_id()) wbase += s_wave[w];
-    all += s_wave[w];
-  }
-  int run = wbase + incl - tot;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = t * 4 + k;
-    if (i < n) v[i] = run;
-    run += a[k];
-  }
-  __syncthreads();
-  return all;
-}
+// Self-planning work lists. A pass over the rows of several nodes is cut into items of at most
+// `chunk` rows; item i of the pass belongs to the entry (node) e with off[e] <= i < off[e+1], where
+// off is the exclusive scan of ceil(rows(e) / chunk). Every block of the pass computes this plan for
+// itself with wave 0 (a 64-wide scan over the <= 2^level entries, looping for deeper trees) from the
+// node table written by the previous kernels -- no separate planning kernel and no kernel boundary.
+struct PlanEntry {
+  int node, slot, start, count;
+};
+struct PlanOut {
+  int node, slot, begin, end, total;
+};
 
-// Emit `total` work items: item i belongs to slot p with off[p] <= i < off[p+1].
-__device__ void emit_items(WorkItem* out, int total, const int32_t* s_off, int nslots, const int32_t* s_node,
-                           const Node* nodes, int chunk, bool slot_is_pair) {
-  for (int i = threadIdx.x; i < total; i += blockDim.x) {
-    int lo = 0, hi = nslots - 1;
-    while (lo < hi) {  // largest p with s_off[p] <= i
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] <= i) lo = mid; else hi = mid - 1;
-    }
-    const int p = lo;
-    const int nd = s_node[p];
-    const int c = i - s_off[p];
-    WorkItem w;
-    w.node = nd;
-    w.slot = slot_is_pair ? p : 0;
-    w.begin = nodes[nd].start + c * chunk;
-    w.end = min(nodes[nd].start + nodes[nd].count, w.begin + chunk);
-    out[i] = w;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_plan_hist(GbdtDev d, int level, int chunk, const int32_t* cnt_src) {
-  __shared__ int32_t s_off[1024];
-  __shared__ int32_t s_node[1024];
-  __shared__ int32_t s_wave[8];
-  const int npairs = level == 0 ? 1 : (1 << (level - 1));
-  for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
-    int built = -1;
-    if (level == 0) {
-      built = 0;
-    } else {
-      const int q = (1 << (level - 1)) - 1 + p;  // parent
-      Node& par = d.nodes[q];
-      if (par.status == kSplit) {
-        const int L = 2 * q + 1, R = 2 * q + 2;
-        const int lc = d.cursors[2 * q];
-        d.nodes[L].start = par.start;
-        d.nodes[L].count = lc;
-        d.nodes[R].start = par.start + lc;
-        d.nodes[R].count = par.count - lc;
-        // histogram the child with fewer (global) rows; the sibling comes by exact subtraction
-        const bool left_small = cnt_src[2 * q] <= cnt_src[2 * q + 1];
-        d.nodes[L].build = left_small ? 1 : 0;
-        d.nodes[R].build = left_small ? 0 : 1;
-        built = left_small ? L : R;
+template <class EntryFn>
+__device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int* s_out) {
+  if (wave_id() == 0) {
+    const int lane = lane_id();
+    if (lane == 0) s_out[0] = -1;
+    int carry = 0;
+    for (int base = 0; base < n_ent; base += kWave) {
+      const int e = base + lane;
+      PlanEntry en{-1, 0, 0, 0};
+      if (e < n_ent) en = entry(e);
+      const int nch = (en.node >= 0 && en.count > 0) ? (en.count + chunk - 1) / chunk : 0;
+      const int incl = wave_incl_scan(nch) + carry;
+      const int excl = incl - nch;
+      if (nch > 0 && item >= excl && item < incl) {
+        const int b = en.start + (item - excl) * chunk;
+        s_out[0] = en.node;
+        s_out[1] = en.slot;
+        s_out[2] = b;
+        s_out[3] = min(en.start + en.count, b + chunk);
       }
+      carry = __shfl(incl, kWave - 1, kWave);
     }
-    s_node[p] = built;
-    s_off[p] = built >= 0 ? (d.nodes[built].count + chunk - 1) / chunk : 0;
+    if (lane == 0) s_out[4] = carry;
   }
-  // reset partition cursors of this level's nodes
+  __syncthreads();
+  return PlanOut{s_out[0], s_out[1], s_out[2], s_out[3], s_out[4]};
+}
+
+// Histogram pass of `level`: entries are the node pairs; the built child of a split parent is the
+// one with fewer GLOBAL rows (cnt_src: partition cursors, or their all-reduced copy under DP); the
+// sibling comes by exact subtraction.
+__device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, const int32_t* cnt_src, int p) {
+  if (level == 0) return PlanEntry{0, 0, 0, (int)d.n};
+  const int q = (1 << (level - 1)) - 1 + p;
+  const Node& par = d.nodes[q];
+  if (par.status != kSplit) return PlanEntry{-1, p, 0, 0};
+  const int lc = d.cursors[2 * q];
+  const bool left_small = cnt_src[2 * q] <= cnt_src[2 * q + 1];
+  return left_small ? PlanEntry{2 * q + 1, p, par.start, lc} : PlanEntry{2 * q + 2, p, par.start + lc, par.count - lc};
+}
+
+// Block (0, 0) of the histogram pass publishes the level's node ranges / build flags for the
+// evaluation and partition kernels, resets the level's partition counters and the item count.
+__device__ void publish_level(const GbdtDev& d, int level, const int32_t* cnt_src, int total) {
+  if (threadIdx.x == 0) d.counters[0] = total;
+  if (level == 0) return;
+  const int npairs = 1 << (level - 1);
+  for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
+    const int q = npairs - 1 + p;
+    const Node& par = d.nodes[q];
+    if (par.status != kSplit) continue;
+    const int L = 2 * q + 1, R = 2 * q + 2;
+    const int lc = d.cursors[2 * q];
+    const bool left_small = cnt_src[2 * q] <= cnt_src[2 * q + 1];
+    d.nodes[L].start = par.start;
+    d.nodes[L].count = lc;
+    d.nodes[R].start = par.start + lc;
+    d.nodes[R].count = par.count - lc;
+    d.nodes[L].build = left_small ? 1 : 0;
+    d.nodes[R].build = left_small ? 0 : 1;
+  }
   const int first = (1 << level) - 1, nlev = 1 << level;
   for (int i = threadIdx.x; i < nlev; i += blockDim.x) {
     d.cursors[2 * (first + i)] = 0;
     d.cursors[2 * (first + i) + 1] = 0;
+    d.child_cnt[2 * (first + i)] = 0;
+    d.child_cnt[2 * (first + i) + 1] = 0;
   }
-  __syncthreads();
-  const int total = block_excl_scan_1024(s_off, npairs, s_wave);
-  if (threadIdx.x == 0) d.counters[0] = total;
-  emit_items(d.items_h, total, s_off, npairs, s_node, d.nodes, chunk, true);
 }
 
-// ------------------------------------------------------------------------------------------
-// Histogram build (K15): LDS-privatised packed-u64 histograms, one work item per block,
-// blockIdx.y = feature tile. LDS layout is bin-count aware: feature f occupies nb_f * K_f cells
-// where K_f = min(64, 2^floor(log2(256/nb_f))) lane-private copies (lane l adds into copy
-// l % K_f), so a 2-bin dummy feature gets 64 copies and its 64 lanes never collide on one LDS
-// address, while a 255-bin quantile feature (naturally spread) keeps one copy. Flush sums the
-// copies and issues one int64 global atomic per non-zero (feature, bin, stat) per block.
-// ------------------------------------------------------------------------------------------
-constexpr int kMaxTileWords = 8;   // feature tile <= 32 features (8 dwords of bins)
-
-__global__ __launch_bounds__(512) void k_hist(GbdtDev d, int parity, int tree) {
+__global__ __launch_bounds__(512) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk,
+                                              const int32_t* __restrict__ cnt_src) {
   extern __shared__ uint64_t s_hist[];
   __shared__ int64_t s_tot[2][8];
+  __shared__ int s_plan[5];
   const int item = blockIdx.x;
-  if (item >= d.counters[0]) return;
-  const WorkItem w = d.items_h[item];
+  const int n_ent = level == 0 ? 1 : (1 << (level - 1));
+  const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, cnt_src, p); },
+                                s_plan);
+  if (item == 0 && blockIdx.y == 0) publish_level(d, level, cnt_src, pl.total);
+  if (pl.node < 0) return;
+  WorkItem w;
+  w.node = pl.node;
+  w.slot = pl.slot;
+  w.begin = pl.begin;
+  w.end = pl.end;
+  if (blockIdx.y == 0 && threadIdx.x == 0) d.items_h[item] = w;
   const int f0 = blockIdx.y * d.feat_tile;
   if (f0 >= d.F) return;
   const int ft = min(d.feat_tile, d.F - f0);
@@ -759,6 +760,19 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       Node& R = nodes[2 * n + 2];
       L.status = kActive; L.G = best.gl; L.H = best.hl;
       R.status = kActive; R.G = G - best.gl; R.H = H - best.hl;
+      if (level + 1 == d.max_depth) {  // children are at max depth: finalise them as leaves here
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          Node& ch = c == 0 ? L : R;
+          const double cg = (double)ch.G * d.ginv, chh = (double)ch.H * d.hinv;
+          const double cw = calc_weight(cg, chh, d.lambda_, d.alpha, d.mcw);
+          ch.sum_hess = (float)chh;
+          ch.base_weight = (float)(cw * d.eta);
+          ch.status = kLeaf;
+          ch.leaf_value = (float)(cw * d.eta);
+          ch.split_cond = ch.leaf_value;
+        }
+      }
     } else {
       nd.status = kLeaf;
       nd.leaf_value = (float)(wgt * d.eta);
@@ -778,23 +792,6 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 // ------------------------------------------------------------------------------------------
 // Partition planning + row partition (K18) + leaf margin update (K19)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_plan_part(GbdtDev d, int level, int chunk) {
-  __shared__ int32_t s_off[1024];
-  __shared__ int32_t s_node[1024];
-  __shared__ int32_t s_wave[8];
-  const int first = (1 << level) - 1, nlev = 1 << level;
-  for (int i = threadIdx.x; i < nlev; i += blockDim.x) {
-    const Node& nd = d.nodes[first + i];
-    const bool live = nd.status == kSplit && nd.count > 0;
-    s_off[i] = live ? (nd.count + chunk - 1) / chunk : 0;
-    s_node[i] = first + i;
-  }
-  __syncthreads();
-  const int total = block_excl_scan_1024(s_off, nlev, s_wave);
-  if (threadIdx.x == 0) d.counters[1] = total;
-  emit_items(d.items_p, total, s_off, nlev, s_node, d.nodes, chunk, false);
-}
-
 // Row partition of the split nodes of a level (K18), one launch. A block takes one work item
 // (<= 8192 rows of one node); each wavefront owns a contiguous quarter and keeps its <= 32 rows per
 // lane in registers: pass 1 loads row ids + split-feature bins and counts, the block claims its
@@ -810,9 +807,10 @@ __device__ __forceinline__ bool goes_left(const uint8_t* col, int r, int j, bool
   return (b == kMissingBin) ? dl : (b <= j);
 }
 
-__global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_t zero_next) {
+__global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_t zero_next, int level, int chunk) {
   __shared__ int32_t s_cnt[2][kPartWaves];
   __shared__ int32_t s_base[2];
+  __shared__ int s_plan[5];
   {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
     int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
     const int64_t nz = zero_next / 2;
@@ -820,8 +818,17 @@ __global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_
       zp[e] = make_int4(0, 0, 0, 0);
   }
   const int item = blockIdx.x;
-  if (item >= d.counters[1]) return;
-  const WorkItem w = d.items_p[item];
+  const int first = (1 << level) - 1;
+  const PlanOut pl = block_plan(1 << level, chunk, item, [&](int e) {
+    const Node& n = d.nodes[first + e];
+    return (n.status == kSplit && n.count > 0) ? PlanEntry{first + e, 0, n.start, n.count} : PlanEntry{-1, 0, 0, 0};
+  }, s_plan);
+  if (pl.node < 0) return;
+  WorkItem w;
+  w.node = pl.node;
+  w.slot = 0;
+  w.begin = pl.begin;
+  w.end = pl.end;
   const Node nd = d.nodes[w.node];
   const bool identity = parity == 0 && w.node == 0;
   const int32_t* cur = d.ridx[parity];
@@ -859,6 +866,10 @@ __global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_
     int32_t* cursor = d.cursors + 2 * w.node;
     s_base[0] = tl ? atomicAdd(cursor, tl) : 0;
     s_base[1] = tr ? atomicAdd(cursor + 1, tr) : 0;
+    if (d.dp) {  // global child counts: all-reduced before the next histogram pass
+      if (tl) atomicAdd(d.child_cnt + 2 * w.node, tl);
+      if (tr) atomicAdd(d.child_cnt + 2 * w.node + 1, tr);
+    }
   }
   __syncthreads();
   int bl = s_base[0], br = s_base[1];
@@ -963,16 +974,17 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
     if ((rc = dev_alloc(c, (void**)&d.hist_b[k], hist_bytes))) return rc;
     if ((rc = dev_alloc(c, (void**)&d.hist_s[k], hist_bytes))) return rc;
   }
-  if ((rc = dev_alloc(c, (void**)&d.nodes, c->max_nodes * sizeof(Node)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.nodes_buf[0], c->max_nodes * sizeof(Node)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.nodes_buf[1], c->max_nodes * sizeof(Node)))) return rc;
+  d.nodes = d.nodes_buf[0];
+  d.prev_nodes = d.nodes_buf[1];
   if ((rc = dev_alloc(c, (void**)&d.trees, (size_t)cfg->max_trees * c->max_nodes * sizeof(Node)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.items_h, c->items_cap * sizeof(WorkItem)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&d.items_p, c->items_cap * sizeof(WorkItem)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.counters, 16 * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.child_cnt, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&d.item_left, (size_t)c->items_cap * kPartWaves * sizeof(int32_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.tile_entries, ntiles * sizeof(int32_t)))) return rc;
@@ -1029,53 +1041,56 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
   const int ftiles = ceil_div(d.F, d.feat_tile);
   const size_t tree_lds = (size_t)c->max_nodes * 8;
   if (t0 != c->grown) return -11;  // trees must be grown in order
+  // any native communicator turns on the data-parallel protocol (a 1-rank one exercises it on 1 GPU)
+  const bool dp = c->cfg.comm != nullptr;
+  d.dp = dp ? 1 : 0;
+  // Per tree: grad (+ node-table init, + archive/apply of the previous tree), then per level
+  // hist (self-planned) -> reduce -> [RCCL histogram all-reduce] -> eval -> partition (self-planned)
+  // [-> RCCL child-count all-reduce]; the last split level's children are finalised by eval.
   for (int t = t0; t < t0 + n_trees; ++t) {
     if (t >= c->cfg.max_trees) return -10;
-    hipLaunchKernelGGL(k_init_tree, dim3(1), dim3(256), 0, stream, d);
+    d.nodes = d.nodes_buf[t & 1];
+    d.prev_nodes = d.nodes_buf[(t + 1) & 1];
     const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
     hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
     if (apply >= 0) c->applied = t;
     CK_LAUNCH();
-    for (int level = 0; level <= D; ++level) {
+    for (int level = 0; level < D; ++level) {
       const int parity = level & 1;
-      const int32_t* cnt_src = d.cursors;
-      if (level > 0 && level < D && c->cfg.comm && c->cfg.world_size > 1) {
+      const int32_t* cnt_src = dp ? d.child_cnt : d.cursors;
+      if (level > 0 && dp) {
         // global child row counts decide which child is histogrammed (identically on every rank)
         const int pfirst = (1 << (level - 1)) - 1, np = 1 << (level - 1);
-        CK(hipMemcpyAsync(d.child_cnt + 2 * pfirst, d.cursors + 2 * pfirst, 2 * np * sizeof(int32_t),
-                          hipMemcpyDeviceToDevice, stream));
         int rc = cobalt_comm_allreduce(c->cfg.comm, d.child_cnt + 2 * pfirst, 2 * np, 2 /*int32*/, 0 /*sum*/, stream);
         if (rc) return rc;
-        cnt_src = d.child_cnt;
       }
-      if (level < D)
-        hipLaunchKernelGGL(k_plan_hist, dim3(1), dim3(256), 0, stream, d, level, chunk_hist(d, level), cnt_src);
-      if (level < D) {
-        const int slots = level == 0 ? 1 : (1 << (level - 1));
-        const int chh = chunk_hist(d, level);
-        const int ub = ceil_div(d.n, chh) + (1 << level);
-        hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(512), c->lds_hist, stream, d, parity, t);
-        hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.F * kMaxBins + 1, 256)),
-                           dim3(256), 0, stream, d, parity);
-        CK_LAUNCH();
-        if (c->cfg.comm && c->cfg.world_size > 1) {
-          int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
-          if (rc) return rc;
-        }
+      const int slots = level == 0 ? 1 : (1 << (level - 1));
+      const int chh = chunk_hist(d, level);
+      const int ub = ceil_div(d.n, chh) + (1 << level);
+      hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(512), c->lds_hist, stream, d, parity, t, level, chh, cnt_src);
+      hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.F * kMaxBins + 1, 256)),
+                         dim3(256), 0, stream, d, parity);
+      CK_LAUNCH();
+      if (dp) {
+        int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
+        if (rc) return rc;
       }
       hipLaunchKernelGGL(k_eval, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t);
       if (level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
-        hipLaunchKernelGGL(k_plan_part, dim3(1), dim3(256), 0, stream, d, level, chp);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
         const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;
-        hipLaunchKernelGGL(k_partition, dim3(ubp), dim3(256), 0, stream, d, parity, zero_next);
+        hipLaunchKernelGGL(k_partition, dim3(ubp), dim3(256), 0, stream, d, parity, zero_next, level, chp);
       }
       CK_LAUNCH();
     }
-    CK(hipMemcpyAsync(d.trees + (size_t)t * c->max_nodes, d.nodes, c->max_nodes * sizeof(Node),
-                      hipMemcpyDeviceToDevice, stream));
     c->grown = t + 1;
+  }
+  // archive the last tree of this call (later trees are archived by the next tree's k_grad)
+  if (c->grown > t0) {
+    const int last = c->grown - 1;
+    CK(hipMemcpyAsync(d.trees + (size_t)last * c->max_nodes, d.nodes_buf[last & 1], c->max_nodes * sizeof(Node),
+                      hipMemcpyDeviceToDevice, stream));
   }
   // bring the margins up to date with the last grown tree
   if (c->applied < c->grown) {

@@ -329,7 +329,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
 
         margin = (init_margin.to(dev, torch.float32).clone().contiguous() if init_margin is not None
                   else torch.full((N,), base_margin, dtype=torch.float32, device=dev))
-        comm = dist.native_comm if (dist is not None and world > 1) else None
+        comm = dist.native_comm if dist is not None else None
         if world > 1 and comm is None:
             raise RuntimeError("data-parallel GPU training needs the native RCCL communicator")
         tr = gbdt_ops.GpuGbdtTrainer(n_rows=N, n_feat=F, max_depth=hp.max_depth, max_trees=T, eta=hp.eta,

@@ -129,3 +129,27 @@ def test_gpu_checkpoint_resume_bit_identical(tmp_path, monkeypatch):
     first = gbdt.train(X, y, {**params, "n_estimators": 5}, device="cuda")
     cont = gbdt.GBDTClassifier(device="cuda", **{**params, "n_estimators": 7}).fit(X, y, xgb_model=first)
     assert cont.get_booster().save_raw("ubj") == ref.save_raw("ubj")
+
+
+def test_gpu_data_parallel_protocol_with_one_rank_rccl():
+    """The DP code path (RCCL child-count + histogram all-reduces, child_cnt accumulation) on a
+    1-rank RCCL communicator must give exactly the single-GPU trees."""
+    import ctypes
+
+    from cobalt_smart_lender_ai_amd import _native
+    from cobalt_smart_lender_ai_amd.parallel.dist import DistContext
+
+    lib = _native.lib()
+    assert lib.cobalt_comm_load(_native.rccl_path().encode()) == 0
+    uid = (ctypes.c_uint8 * 128)()
+    assert lib.cobalt_comm_unique_id(uid) == 0
+    h = ctypes.c_void_p()
+    assert lib.cobalt_comm_init(uid, 1, 0, ctypes.byref(h)) == 0
+    ctx = DistContext(rank=0, world=1, local_rank=0, backend="none", native_comm=h.value)
+    X, y = _data(400_000, seed=11)
+    params = dict(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9, random_state=5,
+                  scale_pos_weight=6.0)
+    ref = gbdt.train(X, y, params, device="cuda")
+    dp = gbdt.train(X, y, params, device="cuda", dist=ctx)
+    assert dp.save_raw("ubj") == ref.save_raw("ubj")
+    lib.cobalt_comm_destroy(h, 0)
