@@ -799,15 +799,21 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 // with one atomic pair per item, pass 2 scatters with ballot ranks -- rows are read once.
 // Left rows keep their relative order inside an item; only whole items interleave, so a node's
 // row list stays sorted in 8192-row runs (the root level reads rows in identity order).
-constexpr int kPartWaves = 4;   // 256-thread blocks
-constexpr int kPartSteps = 32;  // 64-row steps per wave -> chunk_part <= 4 * 32 * 64 = 8192
+// Block size is a template parameter: the per-item cursor claim is a pair of same-address
+// device-scope atomics, whose latency/serialisation across the 8 XCDs dominates a level when items
+// are many and small (measured: removing the claims took a 10M-row level from 58 to 24 us). Small
+// row counts therefore use 1024-thread blocks (fewer, bigger items: ~150 at 1.25M rows); large ones
+// 256-thread blocks with 8192-row items, which keep more independent blocks in flight per CU.
+constexpr int kPartSteps = 32;  // 64-row steps per wave
 
 __device__ __forceinline__ bool goes_left(const uint8_t* col, int r, int j, bool dl) {
   const int b = col[r];
   return (b == kMissingBin) ? dl : (b <= j);
 }
 
-__global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_t zero_next, int level, int chunk) {
+template <int kPartWaves>
+__global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int parity, int64_t zero_next, int level,
+                                                               int chunk) {
   __shared__ int32_t s_cnt[2][kPartWaves];
   __shared__ int32_t s_base[2];
   __shared__ int s_plan[5];
@@ -841,6 +847,7 @@ __global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_
   const int per = ((len + kPartWaves - 1) / kPartWaves + kWave - 1) / kWave * kWave;
   const int wb = min(w.end, w.begin + wv * per), we = min(w.end, wb + per);
   int r[kPartSteps];
+  static_assert(kPartSteps <= 32, "step bit masks are 32-bit");
   uint32_t lbits = 0, vbits = 0;
   int nl = 0, nr = 0;
 #pragma unroll
@@ -851,7 +858,7 @@ __global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_
 #pragma unroll
   for (int k = 0; k < kPartSteps; ++k) {
     const bool valid = r[k] >= 0;
-    const bool left = valid && goes_left(col, r[k], j, dl);
+    const bool left = valid && (d.ablate == 11 ? ((r[k] & 1) != 0) : goes_left(col, r[k], j, dl));
     lbits |= (uint32_t)left << k;
     vbits |= (uint32_t)valid << k;
     const uint64_t lm = __ballot(left), vm = __ballot(valid);
@@ -864,8 +871,12 @@ __global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_
     int tl = 0, tr = 0;
     for (int k = 0; k < kPartWaves; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
     int32_t* cursor = d.cursors + 2 * w.node;
-    s_base[0] = tl ? atomicAdd(cursor, tl) : 0;
-    s_base[1] = tr ? atomicAdd(cursor + 1, tr) : 0;
+    if (d.ablate == 12) {  // timing-only: no cursor atomics
+      s_base[0] = 0; s_base[1] = 0;
+    } else {
+      s_base[0] = tl ? atomicAdd(cursor, tl) : 0;
+      s_base[1] = tr ? atomicAdd(cursor + 1, tr) : 0;
+    }
     if (d.dp) {  // global child counts: all-reduced before the next histogram pass
       if (tl) atomicAdd(d.child_cnt + 2 * w.node, tl);
       if (tr) atomicAdd(d.child_cnt + 2 * w.node + 1, tr);
@@ -879,7 +890,7 @@ __global__ __launch_bounds__(256) void k_partition(GbdtDev d, int parity, int64_
   for (int k = 0; k < kPartSteps; ++k) {
     const bool valid = (vbits >> k) & 1u, left = (lbits >> k) & 1u;
     const uint64_t lm = __ballot(valid && left), rm = __ballot(valid && !left);
-    if (valid) {
+    if (valid && d.ablate != 13) {
       if (left) nxt[nd.start + bl + mask_rank(lm)] = r[k];
       else nxt[rend - (br + mask_rank(rm))] = r[k];
     }
@@ -915,7 +926,14 @@ static int pow2_clamp(int64_t v, int lo, int hi) {
 static int chunk_hist(const GbdtDev& d, int level) {
   return level == 0 ? d.chunk : pow2_clamp((d.n / 2 + 1535) / 1536, 1024, 16384);
 }
-static int chunk_part(const GbdtDev& d) { return pow2_clamp((d.n + 1535) / 1536, 1024, 8192); }
+// Partition item size and block shape (see k_partition); COBALT_PART_CHUNK overrides the size.
+static bool part_wide(const GbdtDev& d) { return d.n < 4000000; }
+static int chunk_part(const GbdtDev& d) {
+  static const int env = getenv("COBALT_PART_CHUNK") ? atoi(getenv("COBALT_PART_CHUNK")) : 0;
+  const int cap = (part_wide(d) ? 16 : 4) * kPartSteps * kWave;
+  if (env > 0) return std::min(cap, std::max(1024, env / 1024 * 1024));
+  return 8192;
+}
 
 static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
   CK(hipMalloc(p, bytes < 16 ? 16 : bytes));
@@ -1080,7 +1098,10 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
         const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;
-        hipLaunchKernelGGL(k_partition, dim3(ubp), dim3(256), 0, stream, d, parity, zero_next, level, chp);
+        if (part_wide(d))
+          hipLaunchKernelGGL(k_partition<16>, dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next, level, chp);
+        else
+          hipLaunchKernelGGL(k_partition<4>, dim3(ubp), dim3(4 * kWave), 0, stream, d, parity, zero_next, level, chp);
       }
       CK_LAUNCH();
     }
