@@ -924,7 +924,12 @@ static int pow2_clamp(int64_t v, int lo, int hi) {
 // Work-item sizes: the root level uses the configured chunk (~768 items of 512 threads); deeper
 // levels histogram at most ~N/2 rows -> aim for ~1536 items; partition items cover all split rows.
 static int chunk_hist(const GbdtDev& d, int level) {
-  return level == 0 ? d.chunk : pow2_clamp((d.n / 2 + 1535) / 1536, 1024, 16384);
+  // COBALT_HIST_CHUNK0 / COBALT_HIST_CHUNK override the root / deeper item sizes (tuning experiments)
+  static const int env0 = getenv("COBALT_HIST_CHUNK0") ? atoi(getenv("COBALT_HIST_CHUNK0")) : 0;
+  static const int env1 = getenv("COBALT_HIST_CHUNK") ? atoi(getenv("COBALT_HIST_CHUNK")) : 0;
+  if (level == 0) return env0 > 0 ? std::min(16384, std::max(512, env0)) : d.chunk;
+  if (env1 > 0) return std::min(16384, std::max(512, env1));
+  return pow2_clamp((d.n / 2 + 383) / 384, 1024, 8192);
 }
 // Partition item size and block shape (see k_partition); COBALT_PART_CHUNK overrides the size.
 static bool part_wide(const GbdtDev& d) { return d.n < 4000000; }

@@ -38,7 +38,9 @@ class RFEResult:
 
 def rfe(X, y, params: gbdt.GBDTParams | dict, n_features_to_select: int = 20, step: int = 1,
         device=None, feature_names: list[str] | None = None, importance_type: str = "gain",
-        binned: gbdt.BinnedData | None = None) -> RFEResult:
+        binned: gbdt.BinnedData | None = None, step_score=None) -> RFEResult:
+    """``step_score(booster, support)`` (optional) is called for every fitted subset, from all
+    features down to the final one -- the hook RFECV scores the elimination path with."""
     if isinstance(params, dict):
         params = gbdt.GBDTParams.from_kwargs(**params)
     bd = binned if binned is not None else gbdt.bin_dataset(X, max_bin=params.max_bin,
@@ -52,6 +54,8 @@ def rfe(X, y, params: gbdt.GBDTParams | dict, n_features_to_select: int = 20, st
         feats = np.nonzero(support)[0]
         t0 = time.perf_counter()
         bst = gbdt.train_binned(bd, y, params, feature_mask=support, feature_names=feature_names)
+        if step_score is not None:
+            step_score(bst, support.copy())
         imp_full = bst.feature_importances(importance_type)
         imp = imp_full[feats]
         ranks = np.argsort(imp)
@@ -62,4 +66,6 @@ def rfe(X, y, params: gbdt.GBDTParams | dict, n_features_to_select: int = 20, st
         hist.append({"n_features": int(len(feats)), "dropped": drop.tolist(), "fit_s": time.perf_counter() - t0})
         log.debug("RFE: %d features, dropped %s", len(feats), drop.tolist())
     est = gbdt.train_binned(bd, y, params, feature_mask=support, feature_names=feature_names)
+    if step_score is not None:
+        step_score(est, support.copy())
     return RFEResult(support, ranking, int(support.sum()), est, hist)

@@ -93,3 +93,21 @@ def test_parse_multipart():
             b"Content-Type: text/csv\r\n\r\na,b\n1,2\n\r\n--XYZ--\r\n")
     parts = parse_multipart(body, "multipart/form-data; boundary=XYZ")
     assert parts["file"] == ("a.csv", b"a,b\n1,2\n")
+
+
+def test_tree_explainer_api(reference_booster):
+    from cobalt_smart_lender_ai_amd.explain import TreeExplainer, bar_plot, force_data, summary_plot
+
+    ex = TreeExplainer(reference_booster, device="cpu")
+    assert abs(ex.expected_value - (-0.0027751700)) < 1e-7
+    X = np.array([[UI_DEFAULT[f] for f in DEPLOYED_FEATURES]], dtype=np.float32).repeat(3, 0)
+    X[1, 0] = 20000.0
+    e = ex(X)
+    assert e.values.shape == (3, 20)
+    sv = dict(zip(DEPLOYED_FEATURES, e.values[0]))
+    assert abs(sv["last_fico_range_high"] - (-1.93206)) < 1e-4
+    fd = force_data(e, 0)
+    assert fd["contributions"][0]["feature"] == "last_fico_range_high"
+    assert abs(fd["output"] - (-2.2636339)) < 1e-5
+    bar_plot(e)
+    summary_plot(e)

@@ -165,3 +165,20 @@ def test_automation_sample_and_score(tmp_path, reference_booster):
     out = score_file(reference_booster, tmp_path / "in" / "test_sample.csv", tmp_path / "out" / "latest.csv",
                      device="cpu")
     assert out["prob_default"].between(0, 1).all() and len(out) == 10
+
+
+def test_rfecv_matches_sklearn():
+    from sklearn.feature_selection import RFECV
+    from sklearn.model_selection import StratifiedKFold
+
+    from cobalt_smart_lender_ai_amd.select.rfecv import rfecv
+
+    X, y = _toy(n=1500, f=9, seed=7)
+    params = dict(n_estimators=5, max_depth=3, learning_rate=0.3, random_state=1)
+    ours = rfecv(X, y, params, step=2, cv=3, min_features_to_select=3, device="cpu")
+    sk = RFECV(gbdt.GBDTClassifier(device="cpu", **params), step=2, cv=StratifiedKFold(3), scoring="roc_auc",
+               min_features_to_select=3).fit(X, y)
+    np.testing.assert_array_equal(ours.cv_results_["n_features"], sk.cv_results_["n_features"])
+    np.testing.assert_allclose(ours.cv_results_["mean_test_score"], sk.cv_results_["mean_test_score"], rtol=1e-12)
+    assert ours.n_features_ == sk.n_features_
+    np.testing.assert_array_equal(ours.support_, sk.support_)

@@ -126,3 +126,21 @@ def test_prep_ops_host_semantics():
     Z = torch.tensor([[1.0, 1.0, 2.0, 1.0], [np.nan, np.nan, 0.0, np.nan]], dtype=torch.float64)
     dup, _ = prep_ops.duplicated_numeric(Z)
     assert dup.tolist() == [False, True, False, True]
+
+
+def test_eda_helpers_match_pandas_scipy():
+    from scipy import stats
+
+    from cobalt_smart_lender_ai_amd.prep import eda
+
+    rng = np.random.default_rng(3)
+    df = pd.DataFrame({"a": rng.normal(100, 20, 500), "b": rng.random(500), "s": ["x"] * 500})
+    df.loc[rng.random(500) < 0.3, "b"] = np.nan
+    ours = eda.null_data_summary(df, threshold_percentage=0, device="cpu")
+    assert list(ours["Column"]) == ["b"] and ours["Percentage"].iloc[0] == pytest.approx(df["b"].isna().mean() * 100)
+    np.testing.assert_allclose(eda.zscore(df["a"], device="cpu"), stats.zscore(df["a"]), rtol=1e-10)
+    z = np.abs(stats.zscore(df["a"]))
+    assert eda.zscore_outlier_counts(df["a"], device="cpu") == {t: int((z > t).sum()) for t in (2.0, 2.25, 2.5, 2.75)}
+    d = eda.describe(df, device="cpu")
+    ref = df.describe()
+    np.testing.assert_allclose(d[["a", "b"]].to_numpy(), ref[["a", "b"]].to_numpy(), rtol=1e-9)
