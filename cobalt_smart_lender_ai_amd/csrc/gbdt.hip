@@ -124,7 +124,9 @@ struct GbdtDev {
   int64_t n;
   int64_t row_offset;
   int32_t F, stride, max_depth, max_nodes, chunk, feat_tile;
-  int64_t slot_elems;     // (F+1)*256*2
+  int64_t slot_elems;     // (ncells + 1) * 2: compact histogram slot (int64 g, h per cell + node total)
+  int32_t* hoff;          // [F+1] compact cell offset of feature f (cells = its nbins); hoff[F] = ncells
+  int32_t ncells;         // sum of nbins: real bins only, so low-cardinality features cost 2-3 cells
   double eta, lambda_, alpha, gamma, mcw, subsample, gscale, hscale, ginv, hinv;
   uint64_t seed;
 };
@@ -451,19 +453,32 @@ __global__ __launch_bounds__(512) void k_hist(GbdtDev d, int parity, int tree, i
   const uint32_t trash = (uint32_t)(ft * kMaxBins) + lane;
   if (d.stride == 32 && ft == d.F && ft <= 24) {
     // 32-byte records (bins | pad | (g,h)): one pair of 16-byte loads per row
+    // software pipeline: the row ids of iteration k+1 are loaded while iteration k's records are in
+    // flight, so each iteration waits on one memory round trip instead of two (ridx -> record)
+    int rn[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = w.begin + threadIdx.x + u * B;
+      rn[u] = i < w.end ? (identity ? i : rix[i]) : -1;
+    }
     for (int i0 = w.begin + threadIdx.x; i0 < w.end; i0 += U * B) {
       int r[U];
       uint4 a[U], b2[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * B;
-        r[u] = i < w.end ? (identity ? i : rix[i]) : -1;
-      }
+      for (int u = 0; u < U; ++u) r[u] = rn[u];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint4* rec = reinterpret_cast<const uint4*>(d.bins + (int64_t)(r[u] >= 0 ? r[u] : r[0]) * 32);
         a[u] = rec[0];
         b2[u] = rec[1];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + U * B + u * B;
+        rn[u] = i < w.end ? (identity ? i : rix[i]) : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
         if (r[u] < 0) { b2[u].z = 0u; b2[u].w = 0u; }
         tg += (int64_t)(int32_t)b2[u].w;
         th += (int64_t)b2[u].z;
@@ -536,11 +551,15 @@ __global__ __launch_bounds__(512) void k_hist(GbdtDev d, int parity, int tree, i
   __syncthreads();
   // Per-item partial histogram -> slab (plain coalesced stores; the packed u64 of the K copies can
   // be summed directly because the per-item sums obey the same < 2^31 / < 2^32 bounds).
-  uint64_t* slab = d.slab + (int64_t)item * d.F * kMaxBins + (int64_t)f0 * kMaxBins;
-  for (int e = threadIdx.x; e < ft * kMaxBins; e += blockDim.x) {
-    const int fl = e >> 8, b = e & 255;
+  // compact layout: only the nbins real cells of each feature travel (Sum nbins << F * 256)
+  const int c0 = d.hoff[f0], c1 = d.hoff[f0 + ft];
+  uint64_t* slab = d.slab + (int64_t)item * d.ncells;
+  for (int e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
+    int fl = 0;
+    while (fl + 1 < ft && d.hoff[f0 + fl + 1] <= e) ++fl;
+    const int b = e - d.hoff[f0 + fl];
     uint64_t v = 0;
-    if (((fbits >> fl) & 1ull) && b < d.nbins[f0 + fl]) {
+    if ((fbits >> fl) & 1ull) {
       const int sh = lay[fl].y;
       const uint64_t* cell = s_hist + fl * kMaxBins + (b << sh);
       for (int c = 0; c < (1 << sh); ++c) v += cell[c];
@@ -561,8 +580,8 @@ __global__ __launch_bounds__(512) void k_hist(GbdtDev d, int parity, int tree, i
   }
 }
 
-// Reduce the per-item slabs into the level's histogram slots: thread = one (feature, bin) cell
-// (cell == F*256 is the node-total cell), block.x = a run of kRedItems consecutive items; one int64
+// Reduce the per-item slabs into the level's histogram slots: thread = one compact (feature, bin)
+// cell (cell == ncells is the node-total cell), block.x = a run of kRedItems consecutive items; one int64
 // global atomic per non-zero cell per (run, slot) -- coalesced, 30-100x fewer than per-block flushes.
 constexpr int kRedItems = 16;
 
@@ -571,7 +590,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity) {
   const int i0 = blockIdx.x * kRedItems;
   if (i0 >= n_items) return;
   const int i1 = min(n_items, i0 + kRedItems);
-  const int ncell = d.F * kMaxBins;
+  const int ncell = d.ncells;
   const int cell = blockIdx.y * blockDim.x + threadIdx.x;
   if (cell > ncell) return;
   const bool tot = cell == ncell;
@@ -642,8 +661,8 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 
   if (threadIdx.x == 0) {
     if (level == 0) {
-      nodes[n].G = hb[(int64_t)d.F * kMaxBins * 2];
-      nodes[n].H = hb[(int64_t)d.F * kMaxBins * 2 + 1];
+      nodes[n].G = hb[(int64_t)d.ncells * 2];
+      nodes[n].H = hb[(int64_t)d.ncells * 2 + 1];
     }
     s_GH[0] = nodes[n].G;
     s_GH[1] = nodes[n].H;
@@ -672,17 +691,24 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       if (!fm[f]) continue;
       const int nb = d.nbins[f];
       int64_t g[4], h[4];
-      const int64_t base = ((int64_t)f * kMaxBins + lane * 4) * 2;
+      const int64_t base = ((int64_t)d.hoff[f] + lane * 4) * 2;  // compact cells: bins [0, nb)
       if (built) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { g[k] = hb[base + 2 * k]; h[k] = hb[base + 2 * k + 1]; }
+        for (int k = 0; k < 4; ++k) {
+          const bool in = lane * 4 + k < nb;
+          g[k] = in ? hb[base + 2 * k] : 0;
+          h[k] = in ? hb[base + 2 * k + 1] : 0;
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          g[k] = parent[base + 2 * k] - hb[base + 2 * k];
-          h[k] = parent[base + 2 * k + 1] - hb[base + 2 * k + 1];
-          hs[base + 2 * k] = g[k];
-          hs[base + 2 * k + 1] = h[k];
+          const bool in = lane * 4 + k < nb;
+          g[k] = in ? parent[base + 2 * k] - hb[base + 2 * k] : 0;
+          h[k] = in ? parent[base + 2 * k + 1] - hb[base + 2 * k + 1] : 0;
+          if (in) {
+            hs[base + 2 * k] = g[k];
+            hs[base + 2 * k + 1] = h[k];
+          }
         }
       }
       int64_t cg[4], ch[4];
@@ -1010,6 +1036,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.hoff, (F + 1) * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.tile_entries, ntiles * sizeof(int32_t)))) return rc;
   *out = c;
   return 0;
@@ -1047,6 +1074,11 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
     max_ent = std::max(max_ent, off);
   }
   CK(hipMemcpy(c->d.layout, lay.data(), F * sizeof(int2), hipMemcpyHostToDevice));
+  std::vector<int32_t> hoff(F + 1, 0);
+  for (int f = 0; f < F; ++f) hoff[f + 1] = hoff[f] + std::max(1, std::min(255, nb[f]));
+  CK(hipMemcpy(c->d.hoff, hoff.data(), (F + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->d.ncells = hoff[F];
+  c->d.slot_elems = (int64_t)(hoff[F] + 1) * 2;
   CK(hipMemcpy(c->d.tile_entries, ent.data(), ntiles * sizeof(int32_t), hipMemcpyHostToDevice));
   c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t);
   if (c->lds_hist > 64 * 1024) {
@@ -1091,7 +1123,7 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
       const int chh = chunk_hist(d, level);
       const int ub = ceil_div(d.n, chh) + (1 << level);
       hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(512), c->lds_hist, stream, d, parity, t, level, chh, cnt_src);
-      hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.F * kMaxBins + 1, 256)),
+      hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
                          dim3(256), 0, stream, d, parity);
       CK_LAUNCH();
       if (dp) {
