@@ -408,10 +408,12 @@ __device__ void publish_level(const GbdtDev& d, int level, const int32_t* cnt_sr
   }
 }
 
-__global__ __launch_bounds__(512) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk,
+constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
+
+__global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk,
                                               const int32_t* __restrict__ cnt_src) {
   extern __shared__ uint64_t s_hist[];
-  __shared__ int64_t s_tot[2][8];
+  __shared__ int64_t s_tot[2][kHistThreads / 64];
   __shared__ int s_plan[5];
   const int item = blockIdx.x;
   const int n_ent = level == 0 ? 1 : (1 << (level - 1));
@@ -1122,7 +1124,8 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
       const int slots = level == 0 ? 1 : (1 << (level - 1));
       const int chh = chunk_hist(d, level);
       const int ub = ceil_div(d.n, chh) + (1 << level);
-      hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(512), c->lds_hist, stream, d, parity, t, level, chh, cnt_src);
+      hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level, chh,
+                         cnt_src);
       hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
                          dim3(256), 0, stream, d, parity);
       CK_LAUNCH();
