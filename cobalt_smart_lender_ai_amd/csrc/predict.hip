@@ -94,6 +94,83 @@ COBALT_API int cobalt_predict(const float* X, int64_t n, int F, int64_t ldx, con
   return 0;
 }
 
+// Small/medium batches: the row-block kernel above gives each block ALL trees, so n / 256 blocks
+// would leave most CUs idle (a 1-row request streamed the whole 59k-node forest through one CU).
+// Here the grid is (row blocks x tree tiles); each block writes its rows' leaf values of its tile's
+// trees to leaves[t][row], and k_sum_leaves adds them per row in tree order starting from the base
+// margin -- the same fp32 sequence as k_predict, so results are bit-identical across the paths.
+__global__ __launch_bounds__(256) void k_predict_leaves(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
+                                                        const uint2* __restrict__ nodes,
+                                                        const int32_t* __restrict__ tree_ptr,
+                                                        const int32_t* __restrict__ tile_ptr,
+                                                        float* __restrict__ leaves) {
+  extern __shared__ unsigned char smem[];
+  uint2* s_nodes = reinterpret_cast<uint2*>(smem);
+  float* s_x = reinterpret_cast<float*>(smem + kTileNodes * sizeof(uint2));
+  const int xs = F | 1;
+  const int64_t row0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t row = row0 + threadIdx.x;
+  const int nrows = (int)min((int64_t)blockDim.x, n - row0);
+  const int tile = blockIdx.y;
+  const int t_begin = tile_ptr[tile], t_end = tile_ptr[tile + 1];
+  const int nbase = tree_ptr[t_begin];
+  const int nn = tree_ptr[t_end] - nbase;
+  for (int e = threadIdx.x; e < nrows * F; e += blockDim.x) {
+    const int r = e / F, f = e - r * F;
+    s_x[r * xs + f] = X[(row0 + r) * ldx + f];
+  }
+  for (int i = threadIdx.x; i < nn; i += blockDim.x) s_nodes[i] = nodes[nbase + i];
+  __syncthreads();
+  if (row >= n) return;
+  const float* x = s_x + threadIdx.x * xs;
+  for (int t = t_begin; t < t_end; ++t) {
+    const uint2* tn = s_nodes + (tree_ptr[t] - nbase);
+    uint2 nd = tn[0];
+    while ((nd.x & 0xFFFFu) != 0xFFFFu) {
+      const int f = (nd.x >> 16) & 0x7FFF;
+      const float v = x[f];
+      const bool left = (v != v) ? ((nd.x >> 31) != 0) : (v < __uint_as_float(nd.y));
+      nd = tn[(nd.x & 0xFFFFu) + (left ? 0u : 1u)];
+    }
+    leaves[(int64_t)t * n + row] = __uint_as_float(nd.y);
+  }
+}
+
+__global__ void k_sum_leaves(const float* __restrict__ leaves, int64_t n, int T, float base_margin,
+                             float* __restrict__ out_margin, float* __restrict__ out_prob) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n) return;
+  float acc = base_margin;
+  for (int t = 0; t < T; ++t) acc += leaves[(int64_t)t * n + row];
+  if (out_margin) out_margin[row] = acc;
+  if (out_prob) out_prob[row] = 1.0f / (1.0f + expf(-acc));
+}
+
+// Rows below which the tile-parallel path is used (fewer than ~2 row blocks per CU otherwise).
+COBALT_API int64_t cobalt_predict_small_rows() { return 131072; }
+
+COBALT_API int cobalt_predict_small(const float* X, int64_t n, int F, int64_t ldx, const void* nodes,
+                                    const int32_t* tree_ptr, const int32_t* tile_ptr, int n_tiles, int n_trees,
+                                    float base_margin, float* leaves, float* out_margin, float* out_prob,
+                                    hipStream_t stream) {
+  if (n <= 0) return 0;
+  const int block = 256;
+  const size_t lds = kTileNodes * sizeof(uint2) + (size_t)block * (F | 1) * sizeof(float);
+  if (lds > 160 * 1024) return -3;
+  static size_t attr_set = 64 * 1024;
+  if (lds > attr_set) {
+    CK(hipFuncSetAttribute((const void*)k_predict_leaves, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_set = lds;
+  }
+  hipLaunchKernelGGL(k_predict_leaves, dim3(ceil_div(n, block), n_tiles), dim3(block), lds, stream, X, n, F, ldx,
+                     static_cast<const uint2*>(nodes), tree_ptr, tile_ptr, leaves);
+  CK_LAUNCH();
+  hipLaunchKernelGGL(k_sum_leaves, dim3(ceil_div(n, 256)), dim3(256), 0, stream, leaves, n, n_trees, base_margin,
+                     out_margin, out_prob);
+  CK_LAUNCH();
+  return 0;
+}
+
 // ------------------------------------------------------------------------------------ TreeSHAP
 struct PathElem {
   float lo, hi;        // row follows the path on this feature iff lo <= x < hi (non-missing)

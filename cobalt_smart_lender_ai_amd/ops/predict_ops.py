@@ -25,6 +25,12 @@ _native.register("cobalt_treeshap", ctypes.c_int,
                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                   ctypes.c_void_p])
 _native.register("cobalt_treeshap_chunks", ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int])
+_native.register("cobalt_predict_small_rows", ctypes.c_int64, [])
+_native.register("cobalt_predict_small", ctypes.c_int,
+                 [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p])
+_SMALL_ROWS = 131072
 
 PATH_ELEM = np.dtype([("lo", "<f4"), ("hi", "<f4"), ("feat", "<i4"), ("nan_ok", "<i4"), ("zero", "<f8")])
 
@@ -181,16 +187,25 @@ def _as_f32(X, device: torch.device) -> torch.Tensor:
 
 def predict_gpu(b: Booster, X: torch.Tensor, n_trees: int | None = None, out_margin: torch.Tensor | None = None,
                 out_prob: torch.Tensor | None = None) -> None:
-    """Launch the predictor on the current stream (graph-capturable; no allocation, no sync)."""
+    """Launch the predictor on the current stream (graph-capturable: no host sync; small batches use a
+    scratch buffer from the caching allocator, which a graph capture takes from its private pool)."""
     gf = gpu_forest(b, X.device, n_trees)
     N, F = X.shape
     if F < b.num_feature:
         raise ValueError(f"X has {F} features, model needs {b.num_feature}")
-    rc = _native.lib().cobalt_predict(X.data_ptr(), N, F, X.stride(0), gf.nodes.data_ptr(), gf.tree_ptr.data_ptr(),
-                                      gf.tile_ptr.data_ptr(), gf.n_tiles, b.base_margin,
-                                      out_margin.data_ptr() if out_margin is not None else None,
-                                      out_prob.data_ptr() if out_prob is not None else None,
-                                      _native.stream_handle())
+    lib = _native.lib()
+    om = out_margin.data_ptr() if out_margin is not None else None
+    op = out_prob.data_ptr() if out_prob is not None else None
+    if N < _SMALL_ROWS and N * gf.n_trees <= (1 << 24):
+        # tile-parallel path (see csrc/predict.hip): grid = row blocks x tree tiles
+        leaves = torch.empty(N * gf.n_trees, dtype=torch.float32, device=X.device)
+        rc = lib.cobalt_predict_small(X.data_ptr(), N, F, X.stride(0), gf.nodes.data_ptr(), gf.tree_ptr.data_ptr(),
+                                      gf.tile_ptr.data_ptr(), gf.n_tiles, gf.n_trees, b.base_margin,
+                                      leaves.data_ptr(), om, op, _native.stream_handle())
+        _native.check(rc, "cobalt_predict_small")
+        return
+    rc = lib.cobalt_predict(X.data_ptr(), N, F, X.stride(0), gf.nodes.data_ptr(), gf.tree_ptr.data_ptr(),
+                            gf.tile_ptr.data_ptr(), gf.n_tiles, b.base_margin, om, op, _native.stream_handle())
     _native.check(rc, "cobalt_predict")
 
 

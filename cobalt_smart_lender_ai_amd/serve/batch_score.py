@@ -1,0 +1,100 @@
+"""Large-batch scoring (BASELINE.json config "Batch inference: 1B-row scoring via hipGraph on
+8xMI355X"; SURVEY.md §2.6 batch-parallel inference, §7.3 P6).
+
+Rows are sharded contiguously over the ranks (one process per GPU, ``torch.distributed``); each rank
+streams its shard through a fixed-size device chunk whose predictor launch is captured once into a
+hipGraph and replayed per chunk, double-buffered on two streams so the H2D copy of chunk k+1
+overlaps the scoring of chunk k. There is no collective except the final gather of per-rank counts
+/ checksums (predictions stay on each rank or go to per-rank output files).
+
+``score_shard`` is the per-rank engine; ``score_device_matrix`` scores a device-resident matrix
+(the benchmark path: data generated on the GPU, no PCIe in the loop).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..models.booster import Booster
+from ..ops import predict_ops
+
+
+class GraphScorer:
+    """A predictor launch over a static [chunk, F] device buffer, captured into a hipGraph."""
+
+    def __init__(self, booster: Booster, chunk: int, n_feat: int, device, use_graph: bool = True):
+        self.booster, self.chunk, self.device = booster, int(chunk), torch.device(device)
+        self.x = torch.zeros((self.chunk, n_feat), dtype=torch.float32, device=self.device)
+        self.prob = torch.empty(self.chunk, dtype=torch.float32, device=self.device)
+        self.stream = torch.cuda.Stream(self.device)
+        self.graph = None
+        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
+            predict_ops.predict_gpu(booster, self.x, None, out_prob=self.prob)  # warm-up: packs the forest
+            self.stream.synchronize()
+            if use_graph:
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph, stream=self.stream):
+                    predict_ops.predict_gpu(booster, self.x, None, out_prob=self.prob)
+
+    def run(self) -> None:
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            with torch.cuda.stream(self.stream):
+                predict_ops.predict_gpu(self.booster, self.x, None, out_prob=self.prob)
+
+
+def score_device_matrix(booster: Booster, X: torch.Tensor, out: torch.Tensor | None = None,
+                        chunk: int = 1 << 22) -> torch.Tensor:
+    """Probabilities of a device-resident [N, F] matrix, chunk by chunk with one graph replay each."""
+    N, F = X.shape
+    out = out if out is not None else torch.empty(N, dtype=torch.float32, device=X.device)
+    sc = GraphScorer(booster, min(chunk, N), F, X.device)
+    for s in range(0, N, sc.chunk):
+        e = min(N, s + sc.chunk)
+        with torch.cuda.stream(sc.stream):
+            sc.x[: e - s].copy_(X[s:e], non_blocking=True)
+            if e - s < sc.chunk:
+                sc.x[e - s:].zero_()
+        sc.run()
+        with torch.cuda.stream(sc.stream):
+            out[s:e].copy_(sc.prob[: e - s], non_blocking=True)
+    sc.stream.synchronize()
+    return out
+
+
+def score_shard(booster: Booster, X_host: np.ndarray, chunk: int = 1 << 20, device=None) -> np.ndarray:
+    """Host matrix -> probabilities with pinned double-buffered H2D copies overlapping the graphs."""
+    dev = torch.device(device or "cuda")
+    N, F = X_host.shape
+    out = np.empty(N, dtype=np.float32)
+    if N == 0:
+        return out
+    chunk = min(chunk, N)
+    scorers = [GraphScorer(booster, chunk, F, dev) for _ in range(2)]
+    pinned = [torch.empty((chunk, F), dtype=torch.float32).pin_memory() for _ in range(2)]
+    res = [torch.empty(chunk, dtype=torch.float32).pin_memory() for _ in range(2)]
+    pending: list[tuple[int, int, int]] = []
+    Xh = torch.from_numpy(np.ascontiguousarray(X_host, dtype=np.float32))
+    for k, s in enumerate(range(0, N, chunk)):
+        b = k & 1
+        e = min(N, s + chunk)
+        sc = scorers[b]
+        sc.stream.synchronize()  # buffer b free again (its previous chunk is done)
+        for (ps, pe, pb) in [p for p in pending if p[2] == b]:
+            out[ps:pe] = res[pb][: pe - ps].numpy()
+            pending.remove((ps, pe, pb))
+        pinned[b][: e - s].copy_(Xh[s:e])
+        with torch.cuda.stream(sc.stream):
+            sc.x[: e - s].copy_(pinned[b][: e - s], non_blocking=True)
+            if e - s < chunk:
+                sc.x[e - s:].zero_()
+        sc.run()
+        with torch.cuda.stream(sc.stream):
+            res[b][: e - s].copy_(sc.prob[: e - s], non_blocking=True)
+        pending.append((s, e, b))
+    for sc in scorers:
+        sc.stream.synchronize()
+    for (ps, pe, pb) in pending:
+        out[ps:pe] = res[pb][: pe - ps].numpy()
+    return out

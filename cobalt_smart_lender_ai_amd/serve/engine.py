@@ -5,7 +5,7 @@ The reference scores one HTTP request at a time with ``xgb_model.predict_proba``
 padded to a bucket size (1, 8, 64, 512, 4096) whose whole pipeline -- predictor kernel + TreeSHAP kernel
 (+ its fixed-order chunk reduction) -- was captured once into a hipGraph (``torch.cuda.CUDAGraph``
 over the library's own launches on the capture stream). Serving a batch is then: one H2D copy into
-the bucket's static input, one graph replay, one D2H copy. Larger batches are split into bucket
+the bucket's static input (from pinned staging), one graph replay, one D2H copy. Larger batches are split into bucket
 sized pieces. On a CPU-only host the engine runs the NumPy reference path instead.
 """
 from __future__ import annotations
@@ -27,6 +27,9 @@ class _Bucket:
     x: torch.Tensor          # [B, F] float32 (static graph input)
     prob: torch.Tensor       # [B] float32
     phi: torch.Tensor | None  # [B, F] float64
+    x_pin: torch.Tensor | None = None     # pinned host staging of x / prob / phi (async copies)
+    prob_pin: torch.Tensor | None = None
+    phi_pin: torch.Tensor | None = None
     graph_prob: torch.cuda.CUDAGraph | None = None
     graph_full: torch.cuda.CUDAGraph | None = None
 
@@ -66,7 +69,10 @@ class ScoringEngine:
         dev = self.device
         bk = _Bucket(size=size, x=torch.zeros((size, self.F), dtype=torch.float32, device=dev),
                      prob=torch.zeros(size, dtype=torch.float32, device=dev),
-                     phi=torch.zeros((size, self.F), dtype=torch.float64, device=dev))
+                     phi=torch.zeros((size, self.F), dtype=torch.float64, device=dev),
+                     x_pin=torch.zeros((size, self.F), dtype=torch.float32).pin_memory(),
+                     prob_pin=torch.zeros(size, dtype=torch.float32).pin_memory(),
+                     phi_pin=torch.zeros((size, self.F), dtype=torch.float64).pin_memory())
         if not self.use_graphs:
             return bk
         with torch.cuda.device(dev), torch.cuda.stream(self._stream):
@@ -106,18 +112,24 @@ class ScoringEngine:
                 bk = self._bucket_for(N - s)
                 e = min(N, s + bk.size)
                 n = e - s
-                bk.x[:n].copy_(torch.from_numpy(X[s:e]), non_blocking=False)
+                xp = bk.x_pin.numpy()
+                xp[:n] = X[s:e]
                 if n < bk.size:
-                    bk.x[n:].zero_()
+                    xp[n:] = 0.0
+                bk.x.copy_(bk.x_pin, non_blocking=True)
                 if self.use_graphs:
                     (bk.graph_full if with_shap else bk.graph_prob).replay()
                 elif with_shap:
                     self._run_full(bk)
                 else:
                     self._run_prob(bk)
-                probs[s:e] = bk.prob[:n].cpu().numpy()
+                bk.prob_pin[:n].copy_(bk.prob[:n], non_blocking=True)
                 if with_shap:
-                    phis[s:e] = bk.phi[:n].cpu().numpy()
+                    bk.phi_pin[:n].copy_(bk.phi[:n], non_blocking=True)
+                self._stream.synchronize()
+                probs[s:e] = bk.prob_pin.numpy()[:n]
+                if with_shap:
+                    phis[s:e] = bk.phi_pin.numpy()[:n]
                 s = e
             self._stream.synchronize()
         return probs, phis

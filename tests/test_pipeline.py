@@ -182,3 +182,20 @@ def test_rfecv_matches_sklearn():
     np.testing.assert_allclose(ours.cv_results_["mean_test_score"], sk.cv_results_["mean_test_score"], rtol=1e-12)
     assert ours.n_features_ == sk.n_features_
     np.testing.assert_array_equal(ours.support_, sk.support_)
+
+
+def test_raw_data_manifest_verify(tmp_path):
+    from cobalt_smart_lender_ai_amd.dataio import datasets
+    from cobalt_smart_lender_ai_amd.dataio.artifacts import LocalStore
+
+    blob = b"loan_amnt,term\n1000, 36 months\n"
+    f = datasets.RawFile("raw/sample.csv", __import__("hashlib").md5(blob).hexdigest(), len(blob), "dataset/1-raw/x")
+    assert datasets.verify(tmp_path, (f,)) == {"raw/sample.csv": "missing"}
+    (tmp_path / "raw").mkdir()
+    (tmp_path / "raw" / "sample.csv").write_bytes(blob)
+    assert datasets.verify(tmp_path, (f,)) == {"raw/sample.csv": "ok"}
+    st = LocalStore(tmp_path / "lake")
+    assert datasets.stage_into_store(st, tmp_path, (f,)) == ["dataset/1-raw/x"]
+    assert st.get_bytes("dataset/1-raw/x") == blob
+    (tmp_path / "raw" / "sample.csv").write_bytes(blob[:-1] + b"!")
+    assert datasets.verify(tmp_path, (f,)) == {"raw/sample.csv": "md5 mismatch"}
