@@ -98,3 +98,52 @@ def score_shard(booster: Booster, X_host: np.ndarray, chunk: int = 1 << 20, devi
     for (ps, pe, pb) in pending:
         out[ps:pe] = res[pb][: pe - ps].numpy()
     return out
+
+
+def main(argv=None) -> int:
+    """``python -m cobalt_smart_lender_ai_amd.serve.batch_score --rows-per-gpu N`` (torchrun for N GPUs):
+    scores synthetic LendingClub-shaped rows generated on each GPU with the given (or shipped) model
+    and prints one JSON line with the whole-job rows/s (max time over ranks)."""
+    import argparse
+    import json
+    import time
+    from pathlib import Path
+
+    from ..dataio import synth
+    from ..models.booster import load_pickle_bytes
+    from ..parallel import dist as pdist
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows-per-gpu", type=int, default=125_000_000)
+    ap.add_argument("--model", default=str(Path(__file__).resolve().parents[2] / "src/api/models/xgb_model_tree.pkl"))
+    ap.add_argument("--chunk", type=int, default=1 << 22)
+    ap.add_argument("--gen-chunk", type=int, default=25_000_000)
+    a = ap.parse_args(argv)
+    ctx = pdist.init_from_env()
+    dev = torch.device("cuda", ctx.local_rank)
+    torch.cuda.set_device(dev)
+    _, b = load_pickle_bytes(Path(a.model).read_bytes())
+    n = a.rows_per_gpu
+    X = torch.empty((n, b.num_feature), dtype=torch.float32, device=dev)
+    for s in range(0, n, a.gen_chunk):  # generate in pieces: bounded scratch memory
+        e = min(n, s + a.gen_chunk)
+        X[s:e] = synth.make_lendingclub(e - s, seed=1, row_offset=ctx.rank * n + s, device=dev)[0][:, : b.num_feature]
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    score_device_matrix(b, X[: min(n, a.chunk)], out[: min(n, a.chunk)], chunk=a.chunk)  # warm-up / graph
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    score_device_matrix(b, X, out, chunk=a.chunk)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    dt = ctx.allreduce_scalar(time.perf_counter() - t0, "max", dev)
+    mean_p = ctx.allreduce_scalar(float(out.double().sum()), "sum", dev) / (n * ctx.world)
+    if ctx.rank == 0:
+        print(json.dumps({"metric": "batch scoring rows/s", "value": n * ctx.world / dt, "n_gpus": ctx.world,
+                          "rows": n * ctx.world, "seconds": dt, "mean_prob": mean_p, "chunk": a.chunk}))
+    pdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
