@@ -71,13 +71,14 @@ def clean_data_flow(df: pd.DataFrame, preset: str = "script", device=None,
         out = out.assign(term=_parse_term(out["term"]))
     if "int_rate" in out.columns:
         out = out.assign(int_rate=_parse_percent(out["int_rate"]))
+    out = drop_columns_with_missing_values(out, null_threshold, dev)
     if preset == "notebook" and "mths_since_last_delinq" in out.columns:
+        # notebooks/01_data_cleaning.ipynb:9926-9934, after the >70% column drop (:9194)
         fill = out["mths_since_last_delinq"].isna()
         if "acc_now_delinq" in out.columns:
             fill &= out["acc_now_delinq"] == 0
         out = out.assign(mths_since_last_delinq=out["mths_since_last_delinq"].mask(fill, 999))
         out = out.loc[out["mths_since_last_delinq"].notna()]
-    out = drop_columns_with_missing_values(out, null_threshold, dev)
     unnecessary = SCRIPT_UNNECESSARY if preset == "script" else NOTEBOOK_UNNECESSARY
     out = out.drop(columns=[c for c in unnecessary if c in out.columns])
     fills = {c: 0 for c in ZERO_FILL if c in out.columns}

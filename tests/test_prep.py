@@ -144,3 +144,26 @@ def test_eda_helpers_match_pandas_scipy():
     d = eda.describe(df, device="cpu")
     ref = df.describe()
     np.testing.assert_allclose(d[["a", "b"]].to_numpy(), ref[["a", "b"]].to_numpy(), rtol=1e-9)
+
+
+def test_notebook_preset_matches_pandas_oracle():
+    raw = make_raw_lendingclub(4000, seed=9)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        ours = clean.clean_data_flow(raw, preset="notebook", device="cpu")
+        d = raw.drop(columns=["Unnamed: 0.1", "Unnamed: 0"], errors="ignore")
+        d["hardship_status"] = d["hardship_status"].fillna("No Hardship")
+        d["term"] = d["term"].str.replace(" months", "").astype(int)
+        d["int_rate"] = d["int_rate"].str.replace("%", "").astype(float) / 100
+        pct = d.isnull().sum() / len(d) * 100
+        d = d.drop(columns=pct[pct > 70].index.tolist())
+        if "mths_since_last_delinq" in d.columns:
+            m = d["mths_since_last_delinq"].isna() & (d["acc_now_delinq"] == 0)
+            d.loc[m, "mths_since_last_delinq"] = 999
+            d = d.dropna(subset=["mths_since_last_delinq"])
+        d = d.drop(columns=[c for c in clean.NOTEBOOK_UNNECESSARY if c in d.columns])
+        for c in ["inq_last_12m", "open_acc_6m", "chargeoff_within_12_mths"]:
+            if c in d.columns:
+                d[c] = d[c].fillna(0)
+        d = d.drop_duplicates()
+    pd.testing.assert_frame_equal(ours.reset_index(drop=True), d.reset_index(drop=True), check_dtype=False)
