@@ -647,170 +647,183 @@ __device__ __forceinline__ double calc_weight(double g, double h, double lambda_
   return -t / (h + lambda_);
 }
 
+// Latency structure: one round of scalar loads for the node (and its parent's build flag / the root
+// total), then every wave issues ALL loads of its <= 2 features (histogram bins, parent bins for the
+// subtraction, masks, bin counts, cut values) before computing, so a level costs ~2 dependent memory
+// round trips; the winning candidate carries its cut value (no load after the reduction).
+struct EvalFeat {
+  int f, nb;
+  bool on;
+  int64_t g[4], h[4];
+  float cut[4], cutm1;  // cut of bins lane*4+k, and of bin lane*4-1 (missing-left splits at b-1)
+};
+
 __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree) {
   const int pos = blockIdx.x;
   const int n = (1 << level) - 1 + pos;
   Node* nodes = d.nodes;
-  if (nodes[n].status != kActive) return;
-  __shared__ Cand s_best[16];
-  __shared__ int64_t s_GH[2];
-
   const int pair = level == 0 ? 0 : (pos >> 1);
   const int64_t SE = d.slot_elems;
   const int64_t* hb = d.hist_b[parity] + pair * SE;
   int64_t* hs = d.hist_s[parity] + pair * SE;
+  // round trip 1 (uniform scalar loads)
+  const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
-
-  if (threadIdx.x == 0) {
-    if (level == 0) {
-      nodes[n].G = hb[(int64_t)d.ncells * 2];
-      nodes[n].H = hb[(int64_t)d.ncells * 2 + 1];
-    }
-    s_GH[0] = nodes[n].G;
-    s_GH[1] = nodes[n].H;
+  int64_t G = nodes[n].G, H = nodes[n].H;
+  int pbuild = 1;
+  if (level > 0) pbuild = nodes[(1 << (level - 1)) - 1 + (pos >> 1)].build;
+  if (level == 0) {
+    G = hb[(int64_t)d.ncells * 2];
+    H = hb[(int64_t)d.ncells * 2 + 1];
   }
-  __syncthreads();
-  const int64_t G = s_GH[0], H = s_GH[1];
+  if (status != kActive) return;
+  __shared__ Cand s_best[16];
+  __shared__ float s_cut[16];
   const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
-
-  if (level < d.max_depth) {
-    const int64_t* parent = nullptr;
-    if (!built) {
-      const int ppos = pos >> 1;
-      const int q = (1 << (level - 1)) - 1 + ppos;
-      const int ppair = level == 1 ? 0 : (ppos >> 1);
-      parent = (nodes[q].build ? d.hist_b[parity ^ 1] : d.hist_s[parity ^ 1]) + ppair * SE;
+  const int64_t* parent = nullptr;
+  if (!built) {
+    const int ppos = pos >> 1;
+    const int ppair = level == 1 ? 0 : (ppos >> 1);
+    parent = (pbuild ? d.hist_b[parity ^ 1] : d.hist_s[parity ^ 1]) + ppair * SE;
+  }
+  const double parent_gain = calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw);
+  Cand best;
+  best.gain = -INFINITY;
+  best.key = 0x7fffffff;
+  best.gl = 0;
+  best.hl = 0;
+  float best_cut = -FLT_MAX;
+  const int lane = lane_id();
+  const int nw = (int)(blockDim.x / kWave);
+  const uint8_t* fm = d.fmask + (int64_t)tree * d.F;
+  for (int fbase = wave_id(); fbase < d.F; fbase += 2 * nw) {  // one pass for F <= 32
+  // round trip 2: everything the wave's features need
+  EvalFeat ef[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    EvalFeat& e = ef[s];
+    e.f = fbase + s * nw;
+    e.on = e.f < d.F && fm[e.f] != 0;
+    e.nb = e.f < d.F ? d.nbins[e.f] : 0;
+    const int64_t base = e.f < d.F ? ((int64_t)d.hoff[e.f] + lane * 4) * 2 : 0;  // compact cells
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool in = e.on && lane * 4 + k < e.nb;
+      const int64_t bg = in ? hb[base + 2 * k] : 0, bh = in ? hb[base + 2 * k + 1] : 0;
+      const int64_t pg = (in && !built) ? parent[base + 2 * k] : 0;
+      const int64_t ph = (in && !built) ? parent[base + 2 * k + 1] : 0;
+      e.g[k] = built ? bg : pg - bg;
+      e.h[k] = built ? bh : ph - bh;
+      e.cut[k] = in ? d.cuts[e.f * kMaxBins + lane * 4 + k] : 0.0f;
     }
-    const double parent_gain = calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw);
-    Cand best;
-    best.gain = -INFINITY;
-    best.key = 0x7fffffff;
-    best.gl = 0;
-    best.hl = 0;
-    const int lane = lane_id();
-    const uint8_t* fm = d.fmask + (int64_t)tree * d.F;
-    for (int f = wave_id(); f < d.F; f += (int)(blockDim.x / kWave)) {
-      if (!fm[f]) continue;
-      const int nb = d.nbins[f];
-      int64_t g[4], h[4];
-      const int64_t base = ((int64_t)d.hoff[f] + lane * 4) * 2;  // compact cells: bins [0, nb)
-      if (built) {
+    e.cutm1 = (e.on && lane > 0 && lane * 4 - 1 < e.nb) ? d.cuts[e.f * kMaxBins + lane * 4 - 1] : -FLT_MAX;
+  }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool in = lane * 4 + k < nb;
-          g[k] = in ? hb[base + 2 * k] : 0;
-          h[k] = in ? hb[base + 2 * k + 1] : 0;
+  for (int s = 0; s < 2; ++s) {
+    const EvalFeat& e = ef[s];
+    if (!e.on) continue;
+    const int f = e.f, nb = e.nb;
+    if (!built) {  // materialise the sibling histogram for the next level
+      const int64_t base = ((int64_t)d.hoff[f] + lane * 4) * 2;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (lane * 4 + k < nb) {
+          hs[base + 2 * k] = e.g[k];
+          hs[base + 2 * k + 1] = e.h[k];
         }
-      } else {
+    }
+    int64_t cg[4], ch[4];
+    cg[0] = e.g[0]; ch[0] = e.h[0];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool in = lane * 4 + k < nb;
-          g[k] = in ? parent[base + 2 * k] - hb[base + 2 * k] : 0;
-          h[k] = in ? parent[base + 2 * k + 1] - hb[base + 2 * k + 1] : 0;
-          if (in) {
-            hs[base + 2 * k] = g[k];
-            hs[base + 2 * k + 1] = h[k];
-          }
+    for (int k = 1; k < 4; ++k) { cg[k] = cg[k - 1] + e.g[k]; ch[k] = ch[k - 1] + e.h[k]; }
+    const int64_t ig = wave_incl_scan(cg[3]), ih = wave_incl_scan(ch[3]);
+    const int64_t eg = ig - cg[3], eh = ih - ch[3];
+    const int64_t sg = __shfl(ig, kWave - 1, kWave), sh = __shfl(ih, kWave - 1, kWave);
+    const int64_t mg = G - sg, mh = H - sh;  // missing-value statistics
+    const bool has_missing = (mg != 0) || (mh != 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = lane * 4 + k;
+      if (b >= nb) continue;
+      // direction 0: missing -> right, left = bins <= b
+      {
+        const int64_t GL = eg + cg[k], HL = eh + ch[k];
+        const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
+        const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
+        if (hl >= d.mcw && hr >= d.mcw) {
+          Cand c;
+          c.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+          c.key = f * 1024 + b;
+          c.gl = GL;
+          c.hl = HL;
+          if (cand_better(c, best)) { best = c; best_cut = e.cut[k]; }
         }
       }
-      int64_t cg[4], ch[4];
-      cg[0] = g[0]; ch[0] = h[0];
-#pragma unroll
-      for (int k = 1; k < 4; ++k) { cg[k] = cg[k - 1] + g[k]; ch[k] = ch[k - 1] + h[k]; }
-      const int64_t ig = wave_incl_scan(cg[3]), ih = wave_incl_scan(ch[3]);
-      const int64_t eg = ig - cg[3], eh = ih - ch[3];
-      const int64_t sg = __shfl(ig, kWave - 1, kWave), sh = __shfl(ih, kWave - 1, kWave);
-      const int64_t mg = G - sg, mh = H - sh;  // missing-value statistics
-      const bool has_missing = (mg != 0) || (mh != 0);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int b = lane * 4 + k;
-        if (b >= nb) continue;
-        // direction 0: missing -> right, left = bins <= b
-        {
-          const int64_t GL = eg + cg[k], HL = eh + ch[k];
-          const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
-          const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
-          if (hl >= d.mcw && hr >= d.mcw) {
-            Cand c;
-            c.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
-            c.key = f * 1024 + b;
-            c.gl = GL;
-            c.hl = HL;
-            if (cand_better(c, best)) best = c;
-          }
-        }
-        // direction 1: missing -> left, left = bins <= b-1 (+ missing)
-        if (has_missing && b <= nb - 1) {
-          const int64_t GL = eg + cg[k] - g[k] + mg, HL = eh + ch[k] - h[k] + mh;
-          const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
-          const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
-          if (hl >= d.mcw && hr >= d.mcw) {
-            Cand c;
-            c.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
-            c.key = f * 1024 + 512 + (nb - 1 - b);
-            c.gl = GL;
-            c.hl = HL;
-            if (cand_better(c, best)) best = c;
-          }
+      // direction 1: missing -> left, left = bins <= b-1 (+ missing)
+      if (has_missing && b <= nb - 1) {
+        const int64_t GL = eg + cg[k] - e.g[k] + mg, HL = eh + ch[k] - e.h[k] + mh;
+        const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
+        const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
+        if (hl >= d.mcw && hr >= d.mcw) {
+          Cand c;
+          c.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+          c.key = f * 1024 + 512 + (nb - 1 - b);
+          c.gl = GL;
+          c.hl = HL;
+          if (cand_better(c, best)) { best = c; best_cut = b == 0 ? -FLT_MAX : (k == 0 ? e.cutm1 : e.cut[k - 1]); }
         }
       }
     }
+  }
+  }
 #pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      Cand other = cand_shfl_xor(best, o);
-      if (cand_better(other, best)) best = other;
-    }
-    if (lane == 0) s_best[wave_id()] = best;
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    for (int k = 1; k < (int)(blockDim.x / kWave); ++k)
-      if (cand_better(s_best[k], best)) best = s_best[k];
-    const float loss = (float)best.gain;
-    const bool ok = best.key != 0x7fffffff && loss > 1e-6f && loss >= (float)d.gamma;
-    const double wgt = calc_weight(Gd, Hd, d.lambda_, d.alpha, d.mcw);
-    Node& nd = nodes[n];
-    nd.sum_hess = (float)Hd;
-    nd.base_weight = (float)(wgt * d.eta);
-    if (ok) {
-      const int f = best.key >> 10;
-      const int r = best.key & 1023;
-      const int nb = d.nbins[f];
-      int j, dl;
-      if (r < 512) { j = r; dl = 0; } else { j = (nb - 1 - (r - 512)) - 1; dl = 1; }
-      nd.status = kSplit;
-      nd.feat = f;
-      nd.bin = j;
-      nd.default_left = dl;
-      nd.split_cond = j >= 0 ? d.cuts[f * kMaxBins + j] : -FLT_MAX;
-      nd.loss_chg = loss;
-      Node& L = nodes[2 * n + 1];
-      Node& R = nodes[2 * n + 2];
-      L.status = kActive; L.G = best.gl; L.H = best.hl;
-      R.status = kActive; R.G = G - best.gl; R.H = H - best.hl;
-      if (level + 1 == d.max_depth) {  // children are at max depth: finalise them as leaves here
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    Cand other = cand_shfl_xor(best, o);
+    const float ocut = __shfl_xor(best_cut, o, kWave);
+    if (cand_better(other, best)) { best = other; best_cut = ocut; }
+  }
+  if (lane == 0) { s_best[wave_id()] = best; s_cut[wave_id()] = best_cut; }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int k = 1; k < nw; ++k)
+    if (cand_better(s_best[k], best)) { best = s_best[k]; best_cut = s_cut[k]; }
+  const float loss = (float)best.gain;
+  const bool ok = best.key != 0x7fffffff && loss > 1e-6f && loss >= (float)d.gamma;
+  const double wgt = calc_weight(Gd, Hd, d.lambda_, d.alpha, d.mcw);
+  Node& nd = nodes[n];
+  if (level == 0) { nd.G = G; nd.H = H; }
+  nd.sum_hess = (float)Hd;
+  nd.base_weight = (float)(wgt * d.eta);
+  if (ok) {
+    const int f = best.key >> 10;
+    const int r = best.key & 1023;
+    const int nb = d.nbins[f];
+    int j, dl;
+    if (r < 512) { j = r; dl = 0; } else { j = (nb - 1 - (r - 512)) - 1; dl = 1; }
+    nd.status = kSplit;
+    nd.feat = f;
+    nd.bin = j;
+    nd.default_left = dl;
+    nd.split_cond = j >= 0 ? best_cut : -FLT_MAX;
+    nd.loss_chg = loss;
+    Node& L = nodes[2 * n + 1];
+    Node& R = nodes[2 * n + 2];
+    L.status = kActive; L.G = best.gl; L.H = best.hl;
+    R.status = kActive; R.G = G - best.gl; R.H = H - best.hl;
+    if (level + 1 == d.max_depth) {  // children are at max depth: finalise them as leaves here
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          Node& ch = c == 0 ? L : R;
-          const double cg = (double)ch.G * d.ginv, chh = (double)ch.H * d.hinv;
-          const double cw = calc_weight(cg, chh, d.lambda_, d.alpha, d.mcw);
-          ch.sum_hess = (float)chh;
-          ch.base_weight = (float)(cw * d.eta);
-          ch.status = kLeaf;
-          ch.leaf_value = (float)(cw * d.eta);
-          ch.split_cond = ch.leaf_value;
-        }
+      for (int c = 0; c < 2; ++c) {
+        Node& ch = c == 0 ? L : R;
+        const double cg = (double)ch.G * d.ginv, chh = (double)ch.H * d.hinv;
+        const double cw = calc_weight(cg, chh, d.lambda_, d.alpha, d.mcw);
+        ch.sum_hess = (float)chh;
+        ch.base_weight = (float)(cw * d.eta);
+        ch.status = kLeaf;
+        ch.leaf_value = (float)(cw * d.eta);
+        ch.split_cond = ch.leaf_value;
       }
-    } else {
-      nd.status = kLeaf;
-      nd.leaf_value = (float)(wgt * d.eta);
-      nd.split_cond = nd.leaf_value;
     }
-  } else if (threadIdx.x == 0) {
-    const double wgt = calc_weight(Gd, Hd, d.lambda_, d.alpha, d.mcw);
-    Node& nd = nodes[n];
-    nd.sum_hess = (float)Hd;
-    nd.base_weight = (float)(wgt * d.eta);
+  } else {
     nd.status = kLeaf;
     nd.leaf_value = (float)(wgt * d.eta);
     nd.split_cond = nd.leaf_value;
