@@ -322,10 +322,6 @@ __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Level planning: child row ranges from partition cursors, choose which child to build,
-// emit histogram work items. One block; work items are emitted by all threads in parallel.
-// ------------------------------------------------------------------------------------------
-// Exclusive scan of v[0..n) (n <= 1024) in LDS by a 256-thread block; returns the total.
 // Self-planning work lists. A pass over the rows of several nodes is cut into items of at most
 // `chunk` rows; item i of the pass belongs to the entry (node) e with off[e] <= i < off[e+1], where
 // off is the exclusive scan of ceil(rows(e) / chunk). Every block of the pass computes this plan for
@@ -408,12 +404,191 @@ __device__ void publish_level(const GbdtDev& d, int level, const int32_t* cnt_sr
   }
 }
 
+// LDS histogram helpers shared by k_hist and k_grad_hist (32-byte record fast path).
+struct HistLanes {
+  uint64_t fbits;                 // colsample mask of the tile's features
+  uint32_t sh0, sh1, sh2, sh3;    // 3-bit copy shifts per feature, 8 features per word (SGPRs)
+  uint32_t trash;                 // per-lane trash cell (missing values, disabled features)
+  uint32_t lane;
+};
+
+__device__ __forceinline__ HistLanes hist_lanes(const GbdtDev& d, int tree, int f0, int ft) {
+  HistLanes hl;
+  const int2* __restrict__ lay = d.layout + f0;
+  const uint8_t* fm = d.fmask + (int64_t)tree * d.F + f0;
+  hl.fbits = 0;
+  for (int k = 0; k < ft; ++k) hl.fbits |= (uint64_t)(fm[k] != 0) << k;
+  hl.sh0 = hl.sh1 = hl.sh2 = hl.sh3 = 0;
+  for (int fl = 0; fl < ft; ++fl) {
+    const uint32_t v = (uint32_t)(lay[fl].y & 7) << (3 * (fl & 7));
+    switch (fl >> 3) { case 0: hl.sh0 |= v; break; case 1: hl.sh1 |= v; break; case 2: hl.sh2 |= v; break; default: hl.sh3 |= v; }
+  }
+  hl.lane = lane_id();
+  hl.trash = (uint32_t)(ft * kMaxBins) + hl.lane;
+  return hl;
+}
+
+// Add one 32-byte record (bins in a.xyzw / b.xy, packed (g, h) in b.wz) to the LDS histogram.
+__device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes& hl, int ft, const uint4& a,
+                                               const uint4& b) {
+  const uint64_t gp = ((uint64_t)b.w << 32) | b.z;
+#pragma unroll
+  for (int fl = 0; fl < 24; ++fl) {
+    if (fl < ft) {
+      const bool fen = (hl.fbits >> fl) & 1ull;
+      const uint32_t shw = fl < 8 ? hl.sh0 : (fl < 16 ? hl.sh1 : hl.sh2);
+      const uint32_t sh = (shw >> (3 * (fl & 7))) & 7u;
+      const uint32_t cbase = (uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << sh) - 1u));
+      const int q = fl >> 2;
+      const uint32_t word = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : b.y;
+      const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
+      const uint32_t cell = (bb != kMissingBin && fen) ? cbase + (bb << sh) : hl.trash;
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp);
+    }
+  }
+}
+
+// Per-item partial histogram -> compact slab (+ the item's (G, H) totals when tot_block).
+__device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistLanes& hl, int item, int f0, int ft,
+                           int64_t tg, int64_t th, bool tot_block, int64_t (*s_tot)[16]) {
+  const int2* __restrict__ lay = d.layout + f0;
+  const int c0 = d.hoff[f0], c1 = d.hoff[f0 + ft];
+  uint64_t* slab = d.slab + (int64_t)item * d.ncells;
+  for (int e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
+    int fl = 0;
+    while (fl + 1 < ft && d.hoff[f0 + fl + 1] <= e) ++fl;
+    const int b = e - d.hoff[f0 + fl];
+    uint64_t v = 0;
+    if ((hl.fbits >> fl) & 1ull) {
+      const int sh = lay[fl].y;
+      const uint64_t* cell = s_hist + fl * kMaxBins + (b << sh);
+      for (int c = 0; c < (1 << sh); ++c) v += cell[c];
+    }
+    slab[e] = v;
+  }
+  if (tot_block) {
+    tg = wave_sum(tg);
+    th = wave_sum(th);
+    if (hl.lane == 0) { s_tot[0][wave_id()] = tg; s_tot[1][wave_id()] = th; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t G = 0, H = 0;
+      for (int k = 0; k < (int)(blockDim.x / kWave); ++k) { G += s_tot[0][k]; H += s_tot[1][k]; }
+      d.slab_tot[2 * item] = G;
+      d.slab_tot[2 * item + 1] = H;
+    }
+  }
+}
+
+// Gradients fused with the ROOT histogram (32-byte records, one feature tile): the gradient pass
+// already streams every record, so the level-0 LDS histogram is accumulated from the registers
+// holding the freshly quantised (g, h) and the bins -- the separate root histogram pass (a full
+// 32 B/row re-read) disappears. Block b = root work item b: rows [b*chunk, (b+1)*chunk).
+// Also: previous-tree margin update + archive and node-table init, as k_grad.
+__global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
+  extern __shared__ uint64_t s_dyn[];
+  __shared__ int64_t s_tot[2][16];
+  const int entries = d.tile_entries[0] + kWave;
+  uint64_t* s_hist = s_dyn;
+  uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries);
+  float* s_leaf = reinterpret_cast<float*>(s_meta + d.max_nodes);
+  {  // zero the root histogram slot (k_hist_reduce accumulates into it)
+    int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
+         e += (int64_t)gridDim.x * blockDim.x)
+      zp[e] = make_int4(0, 0, 0, 0);
+  }
+  if (apply_tree >= 0) {
+    stage_tree(d, d.prev_nodes, s_meta, s_leaf);
+    const int4* src = reinterpret_cast<const int4*>(d.prev_nodes);
+    int4* dst = reinterpret_cast<int4*>(d.trees + (int64_t)apply_tree * d.max_nodes);
+    const int nv = d.max_nodes * (int)(sizeof(Node) / sizeof(int4));
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nv; e += gridDim.x * blockDim.x) dst[e] = src[e];
+  }
+  if (blockIdx.x == 0) {
+    init_tree_block(d);
+    if (threadIdx.x == 0) d.counters[0] = gridDim.x;
+  }
+  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
+  __syncthreads();
+  const int item = blockIdx.x;
+  const int64_t begin = (int64_t)item * chunk, end = min(d.n, begin + chunk);
+  if (threadIdx.x == 0) {
+    WorkItem w;
+    w.node = 0; w.slot = 0; w.begin = (int32_t)begin; w.end = (int32_t)end;
+    d.items_h[item] = w;
+  }
+  const int ft = d.F;
+  const HistLanes hl = hist_lanes(d, tree, 0, ft);
+  const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
+  int64_t tg = 0, th = 0;
+  constexpr int U = 2;
+  const int B = blockDim.x;
+  for (int64_t i0 = begin + threadIdx.x; i0 < end; i0 += U * B) {
+    uint4 ra[U], rb[U];
+    float mf[U], yl[U], wt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * B;
+      const int64_t ii = i < end ? i : begin;
+      const uint4* rec = reinterpret_cast<const uint4*>(d.bins + ii * 32);
+      ra[u] = rec[0];
+      rb[u] = rec[1];
+      mf[u] = d.margin[ii];
+      yl[u] = d.label[ii];
+      wt[u] = d.weight[ii];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * B;
+      if (i >= end) continue;
+      if (apply_tree >= 0) {  // walk the previous tree with the record held in registers
+        int nidx = 0;
+        uint32_t m = s_meta[0];
+        while (m & (1u << 25)) {
+          const int f = m & 0xFFFF, q = f >> 2;
+          const uint32_t word = q == 0 ? ra[u].x : q == 1 ? ra[u].y : q == 2 ? ra[u].z : q == 3 ? ra[u].w
+                              : q == 4 ? rb[u].x : rb[u].y;
+          const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
+          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          nidx = 2 * nidx + (left ? 1 : 2);
+          m = s_meta[nidx];
+        }
+        mf[u] += s_leaf[nidx];
+        d.margin[i] = mf[u];
+      }
+      const double mm = (double)mf[u];
+      const double p = 1.0 / (1.0 + exp(-mm));
+      const double y = (double)yl[u];
+      const double w = (double)wt[u];
+      double g = (p - y) * w;
+      double h = fmax(p * (1.0 - p), 1e-16) * w;
+      if (d.subsample < 1.0) {
+        const uint64_t hsh = splitmix64(tree_key ^ (uint64_t)(d.row_offset + i));
+        if (!(uniform01(hsh) < d.subsample)) { g = 0.0; h = 0.0; }
+      }
+      int64_t gq = (int64_t)rint(g * d.gscale);
+      int64_t hq = (int64_t)rint(h * d.hscale);
+      gq = gq > 65536 ? 65536 : (gq < -65536 ? -65536 : gq);
+      hq = hq > 65536 ? 65536 : (hq < 0 ? 0 : hq);
+      rb[u].z = (uint32_t)hq;
+      rb[u].w = (uint32_t)(int32_t)gq;
+      reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
+      tg += gq;
+      th += hq;
+      hist_add_rec32(s_hist, hl, ft, ra[u], rb[u]);
+    }
+  }
+  __syncthreads();
+  hist_flush(d, s_hist, hl, item, 0, ft, tg, th, true, s_tot);
+}
+
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 
 __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk,
                                               const int32_t* __restrict__ cnt_src) {
   extern __shared__ uint64_t s_hist[];
-  __shared__ int64_t s_tot[2][kHistThreads / 64];
+  __shared__ int64_t s_tot[2][16];
   __shared__ int s_plan[5];
   const int item = blockIdx.x;
   const int n_ent = level == 0 ? 1 : (1 << (level - 1));
@@ -430,11 +605,10 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   const int f0 = blockIdx.y * d.feat_tile;
   if (f0 >= d.F) return;
   const int ft = min(d.feat_tile, d.F - f0);
-  const int2* __restrict__ lay = d.layout + f0;
   const int entries = d.tile_entries[blockIdx.y] + kWave;  // + per-lane trash cells
-  const uint8_t* fm = d.fmask + (int64_t)tree * d.F + f0;
-  uint64_t fbits = 0;
-  for (int k = 0; k < ft; ++k) fbits |= (uint64_t)(fm[k] != 0) << k;
+  const HistLanes hl = hist_lanes(d, tree, f0, ft);
+  const uint64_t fbits = hl.fbits;
+  const uint32_t sh0 = hl.sh0, sh1 = hl.sh1, sh2 = hl.sh2, sh3 = hl.sh3;
 
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   __syncthreads();
@@ -445,14 +619,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
   constexpr int U = 4;  // rows in flight per thread
-  // per-feature copy shift (3 bits) for each 8-feature chunk, kept in scalar registers: reading
-  // them from LDS or scalar memory inside the loop would force lgkmcnt waits on in-flight ds_add
-  uint32_t sh0 = 0, sh1 = 0, sh2 = 0, sh3 = 0;
-  for (int fl = 0; fl < ft; ++fl) {
-    const uint32_t v = (uint32_t)(lay[fl].y & 7) << (3 * (fl & 7));
-    switch (fl >> 3) { case 0: sh0 |= v; break; case 1: sh1 |= v; break; case 2: sh2 |= v; break; default: sh3 |= v; }
-  }
-  const uint32_t trash = (uint32_t)(ft * kMaxBins) + lane;
+  const uint32_t trash = hl.trash;
   if (d.stride == 32 && ft == d.F && ft <= 24) {
     // 32-byte records (bins | pad | (g,h)): one pair of 16-byte loads per row
     // software pipeline: the row ids of iteration k+1 are loaded while iteration k's records are in
@@ -486,24 +653,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
         th += (int64_t)b2[u].z;
       }
 #pragma unroll
-      for (int fl = 0; fl < 24; ++fl) {
-        if (fl < ft) {
-          const bool fen = (fbits >> fl) & 1ull;  // colsample: disabled features add into trash
-          const uint32_t shw = fl < 8 ? sh0 : (fl < 16 ? sh1 : sh2);
-          const uint32_t sh = (shw >> (3 * (fl & 7))) & 7u;
-          const uint32_t cbase = (uint32_t)(fl * kMaxBins) + (lane & ((1u << sh) - 1u));
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int q = fl >> 2;
-            const uint32_t word = q == 0 ? a[u].x : q == 1 ? a[u].y : q == 2 ? a[u].z : q == 3 ? a[u].w
-                                : q == 4 ? b2[u].x : b2[u].y;
-            const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
-            const uint32_t cell = (bb != kMissingBin && fen) ? cbase + (bb << sh) : trash;
-            const uint64_t gp = ((uint64_t)b2[u].w << 32) | b2[u].z;
-            atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp);
-          }
-        }
-      }
+      for (int u = 0; u < U; ++u) hist_add_rec32(s_hist, hl, ft, a[u], b2[u]);
     }
   } else {
   const int nchunks = (ft + 7) >> 3;
@@ -553,33 +703,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   __syncthreads();
   // Per-item partial histogram -> slab (plain coalesced stores; the packed u64 of the K copies can
   // be summed directly because the per-item sums obey the same < 2^31 / < 2^32 bounds).
-  // compact layout: only the nbins real cells of each feature travel (Sum nbins << F * 256)
-  const int c0 = d.hoff[f0], c1 = d.hoff[f0 + ft];
-  uint64_t* slab = d.slab + (int64_t)item * d.ncells;
-  for (int e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
-    int fl = 0;
-    while (fl + 1 < ft && d.hoff[f0 + fl + 1] <= e) ++fl;
-    const int b = e - d.hoff[f0 + fl];
-    uint64_t v = 0;
-    if ((fbits >> fl) & 1ull) {
-      const int sh = lay[fl].y;
-      const uint64_t* cell = s_hist + fl * kMaxBins + (b << sh);
-      for (int c = 0; c < (1 << sh); ++c) v += cell[c];
-    }
-    slab[e] = v;
-  }
-  if (blockIdx.y == 0) {
-    tg = wave_sum(tg);
-    th = wave_sum(th);
-    if (lane == 0) { s_tot[0][wave_id()] = tg; s_tot[1][wave_id()] = th; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int64_t G = 0, H = 0;
-      for (int k = 0; k < (int)(blockDim.x / kWave); ++k) { G += s_tot[0][k]; H += s_tot[1][k]; }
-      d.slab_tot[2 * item] = G;
-      d.slab_tot[2 * item + 1] = H;
-    }
-  }
+  hist_flush(d, s_hist, hl, item, f0, ft, tg, th, blockIdx.y == 0, s_tot);
 }
 
 // Reduce the per-item slabs into the level's histogram slots: thread = one compact (feature, bin)
@@ -1099,6 +1223,10 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   if (c->lds_hist > 64 * 1024) {
     CK(hipFuncSetAttribute((const void*)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
+  const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
+  if (grad_hist_lds > 64 * 1024) {
+    CK(hipFuncSetAttribute((const void*)k_grad_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
+  }
   return 0;
 }
 
@@ -1114,6 +1242,11 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
   // any native communicator turns on the data-parallel protocol (a 1-rank one exercises it on 1 GPU)
   const bool dp = c->cfg.comm != nullptr;
   d.dp = dp ? 1 : 0;
+  // gradients + root histogram in one pass (32-byte records, one feature tile)
+  const bool fuse_root = d.stride == 32 && d.F <= 24 && ftiles == 1 && d.ablate == 0 &&
+                         getenv("COBALT_NO_FUSED_ROOT") == nullptr;
+  // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items)
+  const int root_chunk = std::min(chunk_hist(d, 0), 8192);
   // Per tree: grad (+ node-table init, + archive/apply of the previous tree), then per level
   // hist (self-planned) -> reduce -> [RCCL histogram all-reduce] -> eval -> partition (self-planned)
   // [-> RCCL child-count all-reduce]; the last split level's children are finalised by eval.
@@ -1122,7 +1255,11 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
     d.nodes = d.nodes_buf[t & 1];
     d.prev_nodes = d.nodes_buf[(t + 1) & 1];
     const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
-    hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
+    if (fuse_root)
+      hipLaunchKernelGGL(k_grad_hist, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
+                         d, t, apply, root_chunk);
+    else
+      hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
     if (apply >= 0) c->applied = t;
     CK_LAUNCH();
     for (int level = 0; level < D; ++level) {
@@ -1135,10 +1272,11 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
         if (rc) return rc;
       }
       const int slots = level == 0 ? 1 : (1 << (level - 1));
-      const int chh = chunk_hist(d, level);
+      const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
       const int ub = ceil_div(d.n, chh) + (1 << level);
-      hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level, chh,
-                         cnt_src);
+      if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
+        hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level, chh,
+                           cnt_src);
       hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
                          dim3(256), 0, stream, d, parity);
       CK_LAUNCH();
