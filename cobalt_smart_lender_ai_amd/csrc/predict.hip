@@ -180,27 +180,28 @@ struct PathElem {
 };
 static_assert(sizeof(PathElem) == 24, "PathElem");
 
-// One block = (path chunk, row). Each thread walks its paths in a fixed order and accumulates into a
-// private LDS column s_part[f][tid]; a fixed-shape tree reduction then sums the columns. The result
-// of every block goes to its own slab slot (or straight to phi when there is one chunk), and
-// k_shap_reduce sums the chunk slots in ascending order -- no floating-point atomics. The chunk size
-// depends only on the forest and F (never on the batch size), so a row's SHAP values are
-// bit-identical run to run and whether it is scored alone or inside a bulk batch.
-// P = path register capacity (max unique features on a path + 1): 8 covers depth <= 7 trees without
-// paying for the predicated iterations of a 16/32-slot path.
+// Canonical summation order (shared by both SHAP kernels, so a row's values do not depend on the
+// batch size or on which kernel ran): paths are cut into fixed chunks of kShapChunk; within a chunk
+// contributions are added in path order; k_shap_reduce adds the chunk sums in chunk order. No
+// floating-point atomics anywhere.
+constexpr int kShapChunk = 256;
+constexpr int kShapMaxF = 80;  // path-parallel kernel: [kShapChunk][F] doubles of LDS
+
+// Path-parallel kernel (small batches): block = (chunk, row), one path per thread; each thread
+// writes its path's contributions to its LDS row, then thread f sums column f in path order.
 template <int P>
-__global__ __launch_bounds__(256) void k_treeshap(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
-                                                  const PathElem* __restrict__ elems,
-                                                  const int32_t* __restrict__ path_ptr,
-                                                  const double* __restrict__ path_val, int n_paths, int chunk,
-                                                  int nchunks, double* __restrict__ out) {
-  extern __shared__ double s_part[];  // [F][blockDim.x]
-  const int B = blockDim.x, tid = threadIdx.x;
+__global__ __launch_bounds__(kShapChunk) void k_treeshap(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
+                                                        const PathElem* __restrict__ elems,
+                                                        const int32_t* __restrict__ path_ptr,
+                                                        const double* __restrict__ path_val, int n_paths, int nchunks,
+                                                        double* __restrict__ out) {
+  extern __shared__ double s_c[];  // [kShapChunk][F]
+  const int tid = threadIdx.x;
   const int64_t row = blockIdx.y;
-  for (int f = 0; f < F; ++f) s_part[f * B + tid] = 0.0;
-  const int p_end = min(n_paths, (int)(blockIdx.x + 1) * chunk);
+  for (int f = 0; f < F; ++f) s_c[tid * F + f] = 0.0;
+  const int p = blockIdx.x * kShapChunk + tid;
   const float* x = X + row * ldx;
-  for (int p = blockIdx.x * chunk + tid; p < p_end; p += B) {
+  if (p < n_paths) {
     const int e0 = path_ptr[p], k = path_ptr[p + 1] - e0;  // k unique features (bias excluded)
     double z[P], o[P], w[P];
     int feat[P];
@@ -249,19 +250,130 @@ __global__ __launch_bounds__(256) void k_treeshap(const float* __restrict__ X, i
           }
         }
         total *= (double)(k + 1);
-        s_part[feat[i] * B + tid] += total * (one - zero) * leaf;
+        s_c[tid * F + feat[i]] = total * (one - zero) * leaf;
       }
     }
   }
   __syncthreads();
-  for (int stride = B >> 1; stride >= 1; stride >>= 1) {
-    for (int idx = tid; idx < F * stride; idx += B) {
-      const int f = idx / stride, j = idx - f * stride;
-      s_part[f * B + j] += s_part[f * B + j + stride];
-    }
-    __syncthreads();
+  const int np = min(kShapChunk, n_paths - (int)blockIdx.x * kShapChunk);
+  for (int f = tid; f < F; f += blockDim.x) {
+    double acc = 0.0;
+    for (int q = 0; q < np; ++q) acc += s_c[q * F + f];
+    out[(row * nchunks + blockIdx.x) * F + f] = acc;
   }
-  for (int f = tid; f < F; f += B) out[(row * nchunks + blockIdx.x) * F + f] = s_part[f * B];
+}
+
+// ---------------------------------------------------------------- TreeSHAP with pattern tables
+// Fast TreeSHAP "v2" (Yang 2021): the EXTEND/UNWOUND result of a path depends on the row only
+// through which of the path's k elements the row satisfies (a k-bit pattern), so all 2^k outcomes
+// are tabulated once per model (k_shap_table: the same fp64 arithmetic as k_treeshap, pattern bits
+// in place of the row's one-fractions). Scoring a (row, path) is then k interval tests plus k
+// table reads. Values and accumulation order equal k_treeshap's, so results are bit-identical.
+template <int P>
+__global__ void k_shap_table(const PathElem* __restrict__ elems, const int32_t* __restrict__ path_ptr,
+                             const double* __restrict__ path_val, int n_paths, const int64_t* __restrict__ tab_ptr,
+                             double* __restrict__ table) {
+  const int p = blockIdx.x;
+  if (p >= n_paths) return;
+  const int e0 = path_ptr[p], k = path_ptr[p + 1] - e0;
+  const double leaf = path_val[p];
+  for (int pat = threadIdx.x; pat < (1 << k); pat += blockDim.x) {
+    double z[P], o[P], w[P];
+    z[0] = 1.0; o[0] = 1.0; w[0] = 1.0;
+#pragma unroll
+    for (int i = 1; i < P; ++i) { z[i] = 0.0; o[i] = 0.0; w[i] = 0.0; }
+#pragma unroll
+    for (int l = 1; l < P; ++l) {
+      if (l <= k) {
+        const PathElem e = elems[e0 + l - 1];
+        const double one = ((pat >> (l - 1)) & 1) ? 1.0 : 0.0;
+        z[l] = e.zero; o[l] = one;
+        w[l] = 0.0;
+#pragma unroll
+        for (int j = P - 2; j >= 0; --j) {
+          if (j <= l - 1) {
+            w[j + 1] += one * w[j] * (double)(j + 1) / (double)(l + 1);
+            w[j] = e.zero * w[j] * (double)(l - j) / (double)(l + 1);
+          }
+        }
+      }
+    }
+    double* out = table + tab_ptr[p] + (int64_t)pat * k;
+#pragma unroll
+    for (int i = 1; i < P; ++i) {
+      if (i <= k) {
+        const double one = o[i], zero = z[i];
+        double total = 0.0;
+        if (one != 0.0) {
+          double next = w[k];
+#pragma unroll
+          for (int j = P - 2; j >= 0; --j) {
+            if (j <= k - 1) {
+              const double tmp = next / ((double)(j + 1) * one);
+              total += tmp;
+              next = w[j] - tmp * zero * (double)(k - j);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = P - 2; j >= 0; --j) {
+            if (j <= k - 1) total += w[j] / (zero * (double)(k - j));
+          }
+        }
+        total *= (double)(k + 1);
+        out[i - 1] = total * (one - zero) * leaf;
+      }
+    }
+  }
+}
+
+// Row-parallel kernel (batches): block = (256 rows, chunk); the chunk's path elements live in LDS
+// and are read as broadcasts, every thread walks the chunk's paths in order for ITS row: k interval
+// tests -> pattern -> k table values added to its private LDS column.
+constexpr int kShapRowsF = 48;  // row-parallel kernel: [F][256] doubles of per-row accumulators
+
+__global__ __launch_bounds__(256) void k_treeshap_rows(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
+                                                       const PathElem* __restrict__ elems,
+                                                       const int32_t* __restrict__ path_ptr, int n_paths,
+                                                       const int64_t* __restrict__ tab_ptr,
+                                                       const double* __restrict__ table, int max_len, int nchunks,
+                                                       double* __restrict__ out) {
+  extern __shared__ double s_dyn[];
+  const int B = blockDim.x, tid = threadIdx.x;
+  double* s_phi = s_dyn;                                              // [F][B]
+  float* s_x = reinterpret_cast<float*>(s_phi + (size_t)F * B);        // [B][F|1]
+  const int xs = F | 1;
+  PathElem* s_el = reinterpret_cast<PathElem*>(s_x + (size_t)B * xs + ((B * xs) & 1));  // chunk elements
+  const int c = blockIdx.y;
+  const int p0 = c * kShapChunk, p1 = min(n_paths, p0 + kShapChunk);
+  const int ebase = path_ptr[p0], eend = path_ptr[p1];
+  for (int i = tid; i < eend - ebase; i += B) s_el[i] = elems[ebase + i];
+  const int64_t row0 = (int64_t)blockIdx.x * B;
+  const int nrows = (int)min((int64_t)B, n - row0);
+  for (int e = tid; e < nrows * F; e += B) {
+    const int r = e / F, f = e - r * F;
+    s_x[r * xs + f] = X[(row0 + r) * ldx + f];
+  }
+  for (int f = 0; f < F; ++f) s_phi[f * B + tid] = 0.0;
+  __syncthreads();
+  if (tid < nrows) {
+    const float* x = s_x + tid * xs;
+    for (int p = p0; p < p1; ++p) {
+      const int e0 = path_ptr[p] - ebase, k = path_ptr[p + 1] - path_ptr[p];
+      int pat = 0;
+      for (int l = 0; l < k; ++l) {
+        const PathElem e = s_el[e0 + l];
+        const float v = x[e.feat];
+        const bool one = (v != v) ? (e.nan_ok != 0) : (v >= e.lo && v < e.hi);
+        pat |= (int)one << l;
+      }
+      const double* t = table + tab_ptr[p] + (int64_t)pat * k;
+      for (int l = 0; l < k; ++l) s_phi[s_el[e0 + l].feat * B + tid] += t[l];
+    }
+    const int64_t row = row0 + tid;
+    for (int f = 0; f < F; ++f) out[(row * nchunks + c) * F + f] = s_phi[f * B + tid];
+  }
+  (void)max_len;
 }
 
 __global__ void k_shap_reduce(const double* __restrict__ slab, int64_t n, int F, int nchunks,
@@ -276,22 +388,57 @@ __global__ void k_shap_reduce(const double* __restrict__ slab, int64_t n, int F,
   phi[i] = acc;
 }
 
-constexpr int kShapPathsPerThread = 2;
-
-static int shap_block(int F) {
-  // LDS column store: F * block * 8 bytes must fit the 160 KB of a CU
-  int b = 256;
-  while (b > 64 && (int64_t)F * b * 8 > 160 * 1024) b >>= 1;
-  return ((int64_t)F * b * 8 > 160 * 1024) ? 0 : b;
+// Number of path chunks (and so slab slots per row): fixed by the forest, never by the batch.
+COBALT_API int cobalt_treeshap_chunks(int64_t n, int F, int n_paths) {
+  (void)n;
+  (void)F;
+  return n_paths <= 0 ? 1 : (int)ceil_div((int64_t)n_paths, (int64_t)kShapChunk);
 }
 
-// Number of path chunks (and so slab slots per row) the launch for n rows uses; the caller sizes
-// the workspace as n * chunks * F doubles when chunks > 1.
-COBALT_API int cobalt_treeshap_chunks(int64_t n, int F, int n_paths) {
-  const int B = shap_block(F);
-  if (B == 0 || n <= 0 || n_paths <= 0) return 1;
-  (void)n;
-  return (int)ceil_div((int64_t)n_paths, (int64_t)B * kShapPathsPerThread);
+static int shap_reduce_launch(const double* work, int64_t n, int F, int nchunks, double* phi, hipStream_t stream) {
+  const int64_t tot = n * F;
+  hipLaunchKernelGGL(k_shap_reduce, dim3((unsigned)ceil_div(tot, (int64_t)256)), dim3(256), 0, stream, work, n, F,
+                     nchunks, phi);
+  CK_LAUNCH();
+  return 0;
+}
+
+// Table size (doubles) for paths with unique-feature counts given by path_ptr diffs; -1 if some
+// path is longer than kMaxTabK (the direct kernel is used then).
+constexpr int kMaxTabK = 10;
+
+COBALT_API int cobalt_shap_table_build(const void* elems, const int32_t* path_ptr, const double* path_val, int n_paths,
+                                       int max_len, const int64_t* tab_ptr, double* table, hipStream_t stream) {
+  if (n_paths <= 0) return 0;
+  if (max_len > kMaxTabK) return -3;
+  const PathElem* pe = static_cast<const PathElem*>(elems);
+  if (max_len + 1 <= 8)
+    hipLaunchKernelGGL(k_shap_table<8>, dim3(n_paths), dim3(128), 0, stream, pe, path_ptr, path_val, n_paths, tab_ptr,
+                       table);
+  else
+    hipLaunchKernelGGL(k_shap_table<kMaxPath>, dim3(n_paths), dim3(256), 0, stream, pe, path_ptr, path_val, n_paths,
+                       tab_ptr, table);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_treeshap_tab(const float* X, int64_t n, int F, int64_t ldx, const void* elems,
+                                   const int32_t* path_ptr, int n_paths, int max_len, const int64_t* tab_ptr,
+                                   const double* table, double* phi, double* work, int nchunks, hipStream_t stream) {
+  if (n <= 0 || n_paths <= 0) return 0;
+  if (F > kShapRowsF || max_len > kMaxTabK) return -5;
+  if (nchunks != cobalt_treeshap_chunks(n, F, n_paths)) return -8;
+  if (nchunks > 1 && work == nullptr) return -7;
+  const int B = 256;
+  const size_t lds = (size_t)F * B * sizeof(double) + (size_t)B * (F | 1) * sizeof(float) + 8 +
+                     (size_t)kShapChunk * max_len * sizeof(PathElem);
+  if (lds > 160 * 1024) return -3;
+  if (lds > 64 * 1024) CK(hipFuncSetAttribute((const void*)k_treeshap_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_treeshap_rows, dim3((unsigned)ceil_div(n, (int64_t)B), (unsigned)nchunks), dim3(B), lds, stream,
+                     X, n, F, ldx, static_cast<const PathElem*>(elems), path_ptr, n_paths, tab_ptr, table, max_len,
+                     nchunks, nchunks > 1 ? work : phi);
+  CK_LAUNCH();
+  return nchunks > 1 ? shap_reduce_launch(work, n, F, nchunks, phi, stream) : 0;
 }
 
 COBALT_API int cobalt_treeshap(const float* X, int64_t n, int F, int64_t ldx, const void* elems, const int32_t* path_ptr,
@@ -300,31 +447,22 @@ COBALT_API int cobalt_treeshap(const float* X, int64_t n, int F, int64_t ldx, co
   if (n <= 0 || n_paths <= 0) return 0;
   if (max_len + 1 > kMaxPath) return -3;
   if (n > 65535) return -4;  // grid.y limit; the caller batches rows
-  const int B = shap_block(F);
-  if (B == 0) return -5;
-  if (nchunks < 1) return -6;
-  if (nchunks > 1 && work == nullptr) return -7;
+  if (F > kShapMaxF) return -5;
   if (nchunks != cobalt_treeshap_chunks(n, F, n_paths)) return -8;
-  const int chunk = B * kShapPathsPerThread;
-  const size_t lds = (size_t)F * B * sizeof(double);
+  if (nchunks > 1 && work == nullptr) return -7;
+  const size_t lds = (size_t)F * kShapChunk * sizeof(double);
   dim3 grid((unsigned)nchunks, (unsigned)n);
   const PathElem* pe = static_cast<const PathElem*>(elems);
   double* dst = nchunks > 1 ? work : phi;
   if (max_len + 1 <= 8) {
     if (lds > 64 * 1024) CK(hipFuncSetAttribute((const void*)k_treeshap<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_treeshap<8>, grid, dim3(B), lds, stream, X, n, F, ldx, pe, path_ptr, path_val, n_paths, chunk,
-                       nchunks, dst);
+    hipLaunchKernelGGL(k_treeshap<8>, grid, dim3(kShapChunk), lds, stream, X, n, F, ldx, pe, path_ptr, path_val,
+                       n_paths, nchunks, dst);
   } else {
     if (lds > 64 * 1024) CK(hipFuncSetAttribute((const void*)k_treeshap<kMaxPath>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_treeshap<kMaxPath>, grid, dim3(B), lds, stream, X, n, F, ldx, pe, path_ptr, path_val, n_paths,
-                       chunk, nchunks, dst);
+    hipLaunchKernelGGL(k_treeshap<kMaxPath>, grid, dim3(kShapChunk), lds, stream, X, n, F, ldx, pe, path_ptr, path_val,
+                       n_paths, nchunks, dst);
   }
   CK_LAUNCH();
-  if (nchunks > 1) {
-    const int64_t tot = n * F;
-    hipLaunchKernelGGL(k_shap_reduce, dim3((unsigned)ceil_div(tot, (int64_t)256)), dim3(256), 0, stream, work, n, F,
-                       nchunks, phi);
-    CK_LAUNCH();
-  }
-  return 0;
+  return nchunks > 1 ? shap_reduce_launch(work, n, F, nchunks, phi, stream) : 0;
 }

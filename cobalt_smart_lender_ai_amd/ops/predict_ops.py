@@ -31,6 +31,17 @@ _native.register("cobalt_predict_small", ctypes.c_int,
                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_void_p])
 _SMALL_ROWS = 131072
+_native.register("cobalt_shap_table_build", ctypes.c_int,
+                 [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p])
+_native.register("cobalt_treeshap_tab", ctypes.c_int,
+                 [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_int, ctypes.c_void_p])
+SHAP_ROWS_MIN = 256  # batches from this size use the row-parallel table kernel
+SHAP_ROWS_MAX_F = 48
+SHAP_TABLE_MAX_K = 10             # longest path (unique features) that gets a pattern table
+SHAP_TABLE_MAX_BYTES = 2 << 30    # per-model table budget on the device
 
 PATH_ELEM = np.dtype([("lo", "<f4"), ("hi", "<f4"), ("feat", "<i4"), ("nan_ok", "<i4"), ("zero", "<f8")])
 
@@ -144,6 +155,8 @@ class _GpuForest:
     path_val: torch.Tensor | None = None
     n_paths: int = 0
     max_len: int = 0
+    tab_ptr: torch.Tensor | None = None   # Fast-TreeSHAP pattern tables (None: direct kernel)
+    table: torch.Tensor | None = None
 
 
 def gpu_forest(b: Booster, device: torch.device, n_trees: int | None = None, with_shap: bool = False) -> _GpuForest:
@@ -164,6 +177,17 @@ def gpu_forest(b: Booster, device: torch.device, n_trees: int | None = None, wit
         gf.path_val = torch.from_numpy(pv).to(device)
         gf.n_paths = len(pv)
         gf.max_len = ml
+        k = np.diff(pp).astype(np.int64)
+        sizes = (np.left_shift(1, k) * k) if len(k) else np.zeros(0, np.int64)
+        if len(k) and ml <= SHAP_TABLE_MAX_K and int(sizes.sum()) * 8 <= SHAP_TABLE_MAX_BYTES:
+            tp = np.zeros(len(k) + 1, dtype=np.int64)
+            np.cumsum(sizes, out=tp[1:])
+            gf.tab_ptr = torch.from_numpy(tp).to(device)
+            gf.table = torch.empty(int(tp[-1]), dtype=torch.float64, device=device)
+            rc = _native.lib().cobalt_shap_table_build(gf.elems.data_ptr(), gf.path_ptr.data_ptr(),
+                                                       gf.path_val.data_ptr(), gf.n_paths, ml, gf.tab_ptr.data_ptr(),
+                                                       gf.table.data_ptr(), _native.stream_handle())
+            _native.check(rc, "cobalt_shap_table_build")
     return gf
 
 
@@ -209,6 +233,9 @@ def predict_gpu(b: Booster, X: torch.Tensor, n_trees: int | None = None, out_mar
     _native.check(rc, "cobalt_predict")
 
 
+_FORCE_DIRECT_SHAP = False  # tests compare the row-parallel table kernel against the direct kernel
+
+
 def treeshap_gpu(b: Booster, X: torch.Tensor, phi: torch.Tensor) -> None:
     """Write TreeSHAP values into ``phi`` [N, F] float64 on the current stream (deterministic: no
     floating-point atomics; partial sums are combined in a fixed order)."""
@@ -219,10 +246,17 @@ def treeshap_gpu(b: Booster, X: torch.Tensor, phi: torch.Tensor) -> None:
         e = min(N, s + 65535)
         nch = int(lib.cobalt_treeshap_chunks(e - s, F, gf.n_paths))
         work = torch.empty((e - s) * nch * F, dtype=torch.float64, device=X.device) if nch > 1 else None
-        rc = lib.cobalt_treeshap(X[s:e].data_ptr(), e - s, F, X.stride(0), gf.elems.data_ptr(), gf.path_ptr.data_ptr(),
-                                 gf.path_val.data_ptr(), gf.n_paths, gf.max_len, phi[s:e].data_ptr(),
-                                 work.data_ptr() if work is not None else None, nch, _native.stream_handle())
-        _native.check(rc, "cobalt_treeshap")
+        wp = work.data_ptr() if work is not None else None
+        if gf.table is not None and not _FORCE_DIRECT_SHAP and e - s >= SHAP_ROWS_MIN and F <= SHAP_ROWS_MAX_F:
+            rc = lib.cobalt_treeshap_tab(X[s:e].data_ptr(), e - s, F, X.stride(0), gf.elems.data_ptr(),
+                                         gf.path_ptr.data_ptr(), gf.n_paths, gf.max_len, gf.tab_ptr.data_ptr(),
+                                         gf.table.data_ptr(), phi[s:e].data_ptr(), wp, nch, _native.stream_handle())
+            _native.check(rc, "cobalt_treeshap_tab")
+        else:
+            rc = lib.cobalt_treeshap(X[s:e].data_ptr(), e - s, F, X.stride(0), gf.elems.data_ptr(),
+                                     gf.path_ptr.data_ptr(), gf.path_val.data_ptr(), gf.n_paths, gf.max_len,
+                                     phi[s:e].data_ptr(), wp, nch, _native.stream_handle())
+            _native.check(rc, "cobalt_treeshap")
 
 
 def predict_margin(b: Booster, X, device=None, n_trees: int | None = None):

@@ -85,3 +85,22 @@ def test_shap_is_batch_size_invariant(engines, reference_booster):
     for i in (0, 17, 4999):
         np.testing.assert_array_equal(g.score(X[i:i + 1])[1][0], full[i])
         np.testing.assert_array_equal(e.score(X[i:i + 3])[1][0], full[i])
+
+
+def test_shap_pattern_tables_equal_direct_kernel(reference_booster):
+    """Fast-TreeSHAP pattern tables give bit-identical values to the direct EXTEND/UNWIND kernel."""
+    from cobalt_smart_lender_ai_amd.ops import predict_ops
+
+    gf = predict_ops.gpu_forest(reference_booster, torch.device("cuda", 0), None, with_shap=True)
+    assert gf.table is not None
+    X = torch.as_tensor(_rows(3000, reference_booster.num_feature, seed=33), device="cuda")
+    a = torch.zeros((3000, reference_booster.num_feature), dtype=torch.float64, device="cuda")
+    b = torch.zeros_like(a)
+    predict_ops.treeshap_gpu(reference_booster, X, a)
+    predict_ops._FORCE_DIRECT_SHAP = True
+    try:
+        predict_ops.treeshap_gpu(reference_booster, X, b)
+    finally:
+        predict_ops._FORCE_DIRECT_SHAP = False
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
