@@ -91,6 +91,9 @@ def compute_cuts(sample: torch.Tensor, max_bin: int = 256) -> tuple[torch.Tensor
         nb = torch.where(exact, nb, nbq)
     # sentinel in the last used slot
     cuts.scatter_(1, (nb - 1).clamp(min=0)[:, None], FLT_MAX)
+    # -0.0 and +0.0 sort as equal, so which one a cut inherits depends on the sort implementation
+    # (CPU vs rocPRIM); canonicalise so model files are byte-identical across devices.
+    cuts = cuts + 0.0
     return cuts, nb.to(torch.int32)
 
 

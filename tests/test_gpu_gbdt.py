@@ -153,3 +153,25 @@ def test_gpu_data_parallel_protocol_with_one_rank_rccl():
     dp = gbdt.train(X, y, params, device="cuda", dist=ctx)
     assert dp.save_raw("ubj") == ref.save_raw("ubj")
     lib.cobalt_comm_destroy(h, 0)
+
+
+def _wide(n, F, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    X[:, ::3] = np.round(X[:, ::3] * 2)            # low-cardinality columns (lane replication)
+    X[:, 1::7] = (X[:, 1::7] > 0).astype(np.float32)  # binary columns
+    X[rng.random((n, F)) < 0.05] = np.nan
+    z = X[:, 0] - np.nan_to_num(X[:, F // 2]) + 0.5 * np.nan_to_num(X[:, F - 1])
+    y = (rng.random(n) < 1 / (1 + np.exp(-np.nan_to_num(z)))).astype(np.float32)
+    return X, y
+
+
+@pytest.mark.parametrize("F", [7, 37, 106])
+def test_gpu_trees_identical_to_host_oracle_other_widths(F):
+    """Generic record layouts and multi-tile histograms (F=106 is the RFE stage's width)."""
+    X, y = _wide(20_000, F, seed=F)
+    p = gbdt.GBDTParams(n_estimators=4, max_depth=6, learning_rate=0.3, gamma=0.5, colsample_bytree=0.8,
+                        subsample=0.9, random_state=3)
+    bg = gbdt.train(X, y, p, device="cuda")
+    bc = gbdt.train(X, y, p, device="cpu")
+    assert bg.save_raw("ubj") == bc.save_raw("ubj")
