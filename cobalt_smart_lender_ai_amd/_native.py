@@ -55,6 +55,10 @@ _SIGS: dict[str, tuple] = {
     "cobalt_comm_destroy": (c_int, [c_void_p, c_int]),
     "cobalt_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
     "cobalt_comm_allgather": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    # loopcomm.hip
+    "cobalt_comm_loop_group": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
+    "cobalt_comm_loop_rank": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),
+    "cobalt_comm_loop_group_free": (c_int, [c_void_p]),
 }
 
 

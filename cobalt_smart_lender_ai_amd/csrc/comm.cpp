@@ -11,6 +11,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include "comm.h"
+
 #define COBALT_API extern "C" __attribute__((visibility("default")))
 
 namespace {
@@ -59,6 +61,11 @@ int dtype_code(int code) {
 
 COBALT_API const char* cobalt_comm_last_error() { return g_err; }
 
+void comm_set_error(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
+
+static inline void* nccl_of(void* h) { return static_cast<CobaltComm*>(h)->nccl; }
+static inline bool is_loop(void* h) { return static_cast<CobaltComm*>(h)->kind == 1; }
+
 COBALT_API int cobalt_comm_load(const char* path) {
   if (g_api.lib) return 0;
   g_api.lib = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
@@ -93,18 +100,26 @@ COBALT_API int cobalt_comm_init(const void* id128, int nranks, int rank, void** 
   Comm c = nullptr;
   Result r = g_api.comm_init_rank(&c, nranks, id, rank);
   if (r) { snprintf(g_err, sizeof(g_err), "ncclCommInitRank: %s", g_api.error_string(r)); return r; }
-  *out = c;
+  *out = new CobaltComm{0, c, nullptr, rank, nranks};
   return 0;
 }
 
 COBALT_API int cobalt_comm_destroy(void* comm, int abort) {
-  if (!g_api.lib || !comm) return 0;
-  Result r = abort ? g_api.comm_abort(static_cast<Comm>(comm)) : g_api.comm_destroy(static_cast<Comm>(comm));
+  if (!comm) return 0;
+  CobaltComm* h = static_cast<CobaltComm*>(comm);
+  Result r = 0;
+  if (h->kind == 1) {
+    loop_release(h);
+  } else if (g_api.lib) {
+    r = abort ? g_api.comm_abort(static_cast<Comm>(h->nccl)) : g_api.comm_destroy(static_cast<Comm>(h->nccl));
+  }
+  delete h;
   return r;
 }
 
 COBALT_API int cobalt_comm_allreduce_sum_i64(void* comm, int64_t* buf, int64_t count, hipStream_t stream) {
-  Result r = g_api.all_reduce(buf, buf, (size_t)count, kInt64, kSum, static_cast<Comm>(comm), stream);
+  if (is_loop(comm)) return loop_allreduce(static_cast<CobaltComm*>(comm), buf, count, 0, kSum, stream);
+  Result r = g_api.all_reduce(buf, buf, (size_t)count, kInt64, kSum, static_cast<Comm>(nccl_of(comm)), stream);
   if (r) snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", g_api.error_string(r));
   return r;
 }
@@ -113,7 +128,8 @@ COBALT_API int cobalt_comm_allreduce_sum_i64(void* comm, int64_t* buf, int64_t c
 COBALT_API int cobalt_comm_allreduce(void* comm, void* buf, int64_t count, int dtype, int op, hipStream_t stream) {
   const int dt = dtype_code(dtype);
   if (dt < 0 || (op != kSum && op != kMax && op != kMin)) return -3;
-  Result r = g_api.all_reduce(buf, buf, (size_t)count, dt, op, static_cast<Comm>(comm), stream);
+  if (is_loop(comm)) return loop_allreduce(static_cast<CobaltComm*>(comm), buf, count, dtype, op, stream);
+  Result r = g_api.all_reduce(buf, buf, (size_t)count, dt, op, static_cast<Comm>(nccl_of(comm)), stream);
   if (r) snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", g_api.error_string(r));
   return r;
 }
@@ -122,7 +138,8 @@ COBALT_API int cobalt_comm_allgather(void* comm, const void* send, void* recv, i
                                      hipStream_t stream) {
   const int dt = dtype_code(dtype);
   if (dt < 0) return -3;
-  Result r = g_api.all_gather(send, recv, (size_t)count, dt, static_cast<Comm>(comm), stream);
+  if (is_loop(comm)) return loop_allgather(static_cast<CobaltComm*>(comm), send, recv, count, dtype, stream);
+  Result r = g_api.all_gather(send, recv, (size_t)count, dt, static_cast<Comm>(nccl_of(comm)), stream);
   if (r) snprintf(g_err, sizeof(g_err), "ncclAllGather: %s", g_api.error_string(r));
   return r;
 }
