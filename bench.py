@@ -12,7 +12,7 @@ its own shard by global row index. Scaling mode "weak" (default) gives every ran
 (N GPUs train one model on N x 10M rows: per-GPU work fixed, sized for 288 GB HBM -- the
 data-parallel deployment shape); "strong" keeps 10M global rows and shards them over the ranks.
 Strong scaling of a 300-tree x 7-level boosting run is bounded by its 2,100 sequential level steps
-(each needs two collectives under DP), see docs/PERF.md for both curves.
+(each needs one histogram all-reduce under DP), see docs/PERF.md for both curves.
 
 Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
 Rank 0 prints one JSON line.

@@ -116,11 +116,11 @@ struct GbdtDev {
   int32_t* cursors;       // [max_nodes][2]
   int2* layout;           // [F] histogram LDS layout: x = cell offset within tile, y = log2(copies)
   int32_t* tile_entries;  // [n_tiles] LDS cells per feature tile
-  int32_t* child_cnt;     // [2*max_nodes] all-reduced copy of the partition cursors (DP only)
+  int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush
-  int32_t dp;             // data parallel: partition also accumulates child_cnt for the all-reduce
+  int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
   int64_t n;
   int64_t row_offset;
   int32_t F, stride, max_depth, max_nodes, chunk, feat_tile;
@@ -197,8 +197,6 @@ __device__ void init_tree_block(const GbdtDev& d) {
     d.nodes[i] = nd;
     d.cursors[2 * i] = 0;
     d.cursors[2 * i + 1] = 0;
-    d.child_cnt[2 * i] = 0;
-    d.child_cnt[2 * i + 1] = 0;
   }
 }
 
@@ -362,22 +360,25 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
   return PlanOut{s_out[0], s_out[1], s_out[2], s_out[3], s_out[4]};
 }
 
-// Histogram pass of `level`: entries are the node pairs; the built child of a split parent is the
-// one with fewer GLOBAL rows (cnt_src: partition cursors, or their all-reduced copy under DP); the
-// sibling comes by exact subtraction.
-__device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, const int32_t* cnt_src, int p) {
+// Histogram pass of `level`: entries are the node pairs; the child histogrammed from rows is the one
+// with fewer LOCAL rows (the partition cursors), the sibling comes by exact subtraction. Under DP each
+// rank picks by its own counts and k_dp_local turns the result into the pair's local LEFT histogram
+// before the all-reduce, so no collective is needed to agree on the choice.
+__device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, int p) {
   if (level == 0) return PlanEntry{0, 0, 0, (int)d.n};
   const int q = (1 << (level - 1)) - 1 + p;
   const Node& par = d.nodes[q];
   if (par.status != kSplit) return PlanEntry{-1, p, 0, 0};
   const int lc = d.cursors[2 * q];
-  const bool left_small = cnt_src[2 * q] <= cnt_src[2 * q + 1];
+  const bool left_small = lc <= d.cursors[2 * q + 1];
   return left_small ? PlanEntry{2 * q + 1, p, par.start, lc} : PlanEntry{2 * q + 2, p, par.start + lc, par.count - lc};
 }
 
 // Block (0, 0) of the histogram pass publishes the level's node ranges / build flags for the
 // evaluation and partition kernels, resets the level's partition counters and the item count.
-__device__ void publish_level(const GbdtDev& d, int level, const int32_t* cnt_src, int total) {
+// `build` is the child whose GLOBAL histogram sits in hist_b after the reduce (+ all-reduce): the
+// locally smaller one on one GPU, always the left one under DP.
+__device__ void publish_level(const GbdtDev& d, int level, int total) {
   if (threadIdx.x == 0) d.counters[0] = total;
   if (level == 0) return;
   const int npairs = 1 << (level - 1);
@@ -387,7 +388,7 @@ __device__ void publish_level(const GbdtDev& d, int level, const int32_t* cnt_sr
     if (par.status != kSplit) continue;
     const int L = 2 * q + 1, R = 2 * q + 2;
     const int lc = d.cursors[2 * q];
-    const bool left_small = cnt_src[2 * q] <= cnt_src[2 * q + 1];
+    const bool left_small = d.dp || lc <= d.cursors[2 * q + 1];
     d.nodes[L].start = par.start;
     d.nodes[L].count = lc;
     d.nodes[R].start = par.start + lc;
@@ -399,8 +400,6 @@ __device__ void publish_level(const GbdtDev& d, int level, const int32_t* cnt_sr
   for (int i = threadIdx.x; i < nlev; i += blockDim.x) {
     d.cursors[2 * (first + i)] = 0;
     d.cursors[2 * (first + i) + 1] = 0;
-    d.child_cnt[2 * (first + i)] = 0;
-    d.child_cnt[2 * (first + i) + 1] = 0;
   }
 }
 
@@ -585,16 +584,15 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
 
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 
-__global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk,
-                                              const int32_t* __restrict__ cnt_src) {
+__global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk) {
   extern __shared__ uint64_t s_hist[];
   __shared__ int64_t s_tot[2][16];
   __shared__ int s_plan[5];
   const int item = blockIdx.x;
   const int n_ent = level == 0 ? 1 : (1 << (level - 1));
-  const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, cnt_src, p); },
+  const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
                                 s_plan);
-  if (item == 0 && blockIdx.y == 0) publish_level(d, level, cnt_src, pl.total);
+  if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total);
   if (pl.node < 0) return;
   WorkItem w;
   w.node = pl.node;
@@ -763,6 +761,42 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity) {
     atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)sg);
     atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)sh);
   }
+}
+
+// Data parallel, between the reduce and the all-reduce: hist_b holds, per pair, the histogram of
+// the child this rank built from rows (its locally smaller one). With the rank's local parent
+// histogram (kept from the previous level) the local sibling is an exact subtraction, so every rank
+// can send its LOCAL LEFT child whatever it built; the all-reduced slot is then the global left
+// child on every rank, and both children's local histograms are kept for the next level. This
+// replaces an all-reduce of the children's row counts per level (one collective, and one
+// cross-rank synchronisation, fewer per level). Grid: (pair, 256-cell block); level 0 keeps the root.
+__global__ __launch_bounds__(256) void k_dp_local(GbdtDev d, int level, int parity) {
+  const int p = blockIdx.x;
+  const int64_t e = ((int64_t)blockIdx.y * blockDim.x + threadIdx.x) * 2;  // (g, h) of one cell
+  if (e >= d.slot_elems) return;
+  const int64_t SE = d.slot_elems;
+  int64_t* hb = d.hist_b[parity] + p * SE + e;
+  if (level == 0) {
+    int64_t* loc = d.hist_loc[0] + e;
+    loc[0] = hb[0];
+    loc[1] = hb[1];
+    return;
+  }
+  const int q = (1 << (level - 1)) - 1 + p;  // the parent (level - 1, position p)
+  if (d.nodes[q].status != kSplit) return;
+  const bool left_built = d.cursors[2 * q] <= d.cursors[2 * q + 1];
+  const int64_t* par = d.hist_loc[parity ^ 1] + p * SE + e;
+  const int64_t bg = hb[0], bh = hb[1];
+  const int64_t sg = par[0] - bg, sh = par[1] - bh;
+  int64_t* lo = d.hist_loc[parity] + (int64_t)(2 * p) * SE + e;  // left child (position 2p)
+  int64_t* ro = lo + SE;                                          // right child (position 2p + 1)
+  const int64_t lg = left_built ? bg : sg, lh = left_built ? bh : sh;
+  lo[0] = lg;
+  lo[1] = lh;
+  ro[0] = left_built ? sg : bg;
+  ro[1] = left_built ? sh : bh;
+  hb[0] = lg;
+  hb[1] = lh;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1074,10 +1108,6 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
       s_base[0] = tl ? atomicAdd(cursor, tl) : 0;
       s_base[1] = tr ? atomicAdd(cursor + 1, tr) : 0;
     }
-    if (d.dp) {  // global child counts: all-reduced before the next histogram pass
-      if (tl) atomicAdd(d.child_cnt + 2 * w.node, tl);
-      if (tr) atomicAdd(d.child_cnt + 2 * w.node + 1, tr);
-    }
   }
   __syncthreads();
   int bl = s_base[0], br = s_base[1];
@@ -1202,7 +1232,10 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.items_h, c->items_cap * sizeof(WorkItem)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.counters, 16 * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&d.child_cnt, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
+  if (cfg->comm) {  // local histograms of every node of a level (positions 0 .. 2^(max_depth-1))
+    for (int k = 0; k < 2; ++k)
+      if ((rc = dev_alloc(c, (void**)&d.hist_loc[k], 2 * hist_bytes))) return rc;
+  }
   if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
@@ -1296,23 +1329,18 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
     CK_LAUNCH();
     for (int level = 0; level < D; ++level) {
       const int parity = level & 1;
-      const int32_t* cnt_src = dp ? d.child_cnt : d.cursors;
-      if (level > 0 && dp) {
-        // global child row counts decide which child is histogrammed (identically on every rank)
-        const int pfirst = (1 << (level - 1)) - 1, np = 1 << (level - 1);
-        int rc = cobalt_comm_allreduce(c->cfg.comm, d.child_cnt + 2 * pfirst, 2 * np, 2 /*int32*/, 0 /*sum*/, stream);
-        if (rc) return rc;
-      }
       const int slots = level == 0 ? 1 : (1 << (level - 1));
       const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
       const int ub = ceil_div(d.n, chh) + (1 << level);
       if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-        hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level, chh,
-                           cnt_src);
+        hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level, chh);
       hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
                          dim3(256), 0, stream, d, parity);
       CK_LAUNCH();
       if (dp) {
+        hipLaunchKernelGGL(k_dp_local, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d, level,
+                           parity);
+        CK_LAUNCH();
         int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
         if (rc) return rc;
       }

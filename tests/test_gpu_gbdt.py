@@ -132,8 +132,7 @@ def test_gpu_checkpoint_resume_bit_identical(tmp_path, monkeypatch):
 
 
 def test_gpu_data_parallel_protocol_with_one_rank_rccl():
-    """The DP code path (RCCL child-count + histogram all-reduces, child_cnt accumulation) on a
-    1-rank RCCL communicator must give exactly the single-GPU trees."""
+    """The DP code path (local-left histograms, RCCL histogram all-reduce) on a 1-rank RCCL communicator must give exactly the single-GPU trees."""
     import ctypes
 
     from cobalt_smart_lender_ai_amd import _native
