@@ -47,12 +47,15 @@ _SIGS: dict[str, tuple] = {
     "cobalt_gbdt_destroy": (c_int, [c_void_p]),
     "cobalt_bin_matrix": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int,
                                   c_void_p, c_void_p]),
+    "cobalt_bin_matrix_ld": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int,
+                                     c_void_p, c_int64, c_void_p]),
     # comm.cpp
     "cobalt_comm_load": (c_int, [c_char_p]),
     "cobalt_comm_last_error": (c_char_p, []),
     "cobalt_comm_unique_id": (c_int, [c_void_p]),
     "cobalt_comm_init": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_void_p)]),
     "cobalt_comm_destroy": (c_int, [c_void_p, c_int]),
+    "cobalt_comm_async_error": (c_int, [c_void_p]),
     "cobalt_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
     "cobalt_comm_allgather": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     # loopcomm.hip

@@ -34,6 +34,7 @@ struct Api {
   Result (*all_gather)(const void*, void*, size_t, int, Comm, hipStream_t) = nullptr;
   Result (*broadcast)(const void*, void*, size_t, int, int, Comm, hipStream_t) = nullptr;
   const char* (*error_string)(Result) = nullptr;
+  Result (*async_error)(Comm, Result*) = nullptr;  // optional (ncclCommGetAsyncError)
 };
 
 Api g_api;
@@ -81,6 +82,7 @@ COBALT_API int cobalt_comm_load(const char* path) {
     snprintf(g_err, sizeof(g_err), "missing RCCL symbol in %s", path);
     return -2;
   }
+  sym(g_api.async_error, "ncclCommGetAsyncError");
   return 0;
 }
 
@@ -115,6 +117,20 @@ COBALT_API int cobalt_comm_destroy(void* comm, int abort) {
   }
   delete h;
   return r;
+}
+
+// Asynchronous communicator error (a peer died, a network/transport failure): 0 = healthy. Polled by
+// the host-side collective watchdog (parallel/dist.py) while it waits on the trainer's stream.
+COBALT_API int cobalt_comm_async_error(void* comm) {
+  if (!comm || is_loop(comm) || !g_api.async_error) return 0;
+  Result st = 0;
+  Result r = g_api.async_error(static_cast<Comm>(nccl_of(comm)), &st);
+  if (r) return r;
+  if (st && st != 7 /* ncclInProgress */) {
+    snprintf(g_err, sizeof(g_err), "RCCL async error: %s", g_api.error_string(st));
+    return st;
+  }
+  return 0;
 }
 
 COBALT_API int cobalt_comm_allreduce_sum_i64(void* comm, int64_t* buf, int64_t count, hipStream_t stream) {

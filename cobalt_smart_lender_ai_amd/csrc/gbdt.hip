@@ -139,7 +139,7 @@ template <bool CUTS_IN_LDS>
 __global__ __launch_bounds__(256) void k_bin(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
                                              const float* __restrict__ cuts, const int32_t* __restrict__ nbins,
                                              uint8_t* __restrict__ bins, int stride,
-                                             uint8_t* __restrict__ binsT) {
+                                             uint8_t* __restrict__ binsT, int64_t ldt) {
   extern __shared__ float s_cuts[];
   if (CUTS_IN_LDS) {
     for (int i = threadIdx.x; i < F * kMaxBins; i += blockDim.x) s_cuts[i] = cuts[i];
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_bin(const float* __restrict__ X, int64_
           }
           b = lo >= nb ? (uint32_t)(nb - 1) : (uint32_t)lo;
         }
-        binsT[(int64_t)f * n + row] = (uint8_t)b;
+        binsT[(int64_t)f * ldt + row] = (uint8_t)b;
       }
       word |= b << (8 * (f & 3));
       if ((f & 3) == 3) {
@@ -1403,17 +1403,27 @@ COBALT_API int cobalt_gbdt_destroy(void* h) {
   return 0;
 }
 
-COBALT_API int cobalt_bin_matrix(const float* X, int64_t n, int F, int64_t ldx, const float* cuts,
-                                 const int32_t* nbins, uint8_t* bins, int stride, uint8_t* binsT,
-                                 hipStream_t stream) {
-  if (stride % 4 != 0 || stride < F) return -3;
+// Quantise n rows into row records (pitch `stride`) and feature-major bins with row pitch `ldt`
+// (ldt = n for a whole matrix; the full row count when a streamed chunk is binned in place).
+COBALT_API int cobalt_bin_matrix_ld(const float* X, int64_t n, int F, int64_t ldx, const float* cuts,
+                                    const int32_t* nbins, uint8_t* bins, int stride, uint8_t* binsT, int64_t ldt,
+                                    hipStream_t stream) {
+  if (stride % 4 != 0 || stride < F || ldt < n) return -3;
   const int grid = std::max(1, std::min(ceil_div(n, 256), 256 * 8));
   const size_t lds = (size_t)F * kMaxBins * sizeof(float);
   if (lds <= 64 * 1024) {
-    hipLaunchKernelGGL(k_bin<true>, dim3(grid), dim3(256), lds, stream, X, n, F, ldx, cuts, nbins, bins, stride, binsT);
+    hipLaunchKernelGGL(k_bin<true>, dim3(grid), dim3(256), lds, stream, X, n, F, ldx, cuts, nbins, bins, stride, binsT,
+                       ldt);
   } else {
-    hipLaunchKernelGGL(k_bin<false>, dim3(grid), dim3(256), 0, stream, X, n, F, ldx, cuts, nbins, bins, stride, binsT);
+    hipLaunchKernelGGL(k_bin<false>, dim3(grid), dim3(256), 0, stream, X, n, F, ldx, cuts, nbins, bins, stride, binsT,
+                       ldt);
   }
   CK_LAUNCH();
   return 0;
+}
+
+COBALT_API int cobalt_bin_matrix(const float* X, int64_t n, int F, int64_t ldx, const float* cuts,
+                                 const int32_t* nbins, uint8_t* bins, int stride, uint8_t* binsT,
+                                 hipStream_t stream) {
+  return cobalt_bin_matrix_ld(X, n, F, ldx, cuts, nbins, bins, stride, binsT, n, stream);
 }

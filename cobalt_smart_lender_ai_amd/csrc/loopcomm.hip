@@ -30,7 +30,8 @@ struct LoopGroup {
   std::vector<void*> tmp;
   std::vector<size_t> tmp_bytes;
 
-  // false on timeout (a rank died before the collective): the group is then unusable
+  // false when the group is broken: a rank left (its handle was destroyed, e.g. it failed) or the
+  // meeting timed out -- every waiter then fails fast instead of hanging
   bool barrier() {
     std::unique_lock<std::mutex> lk(mu);
     if (broken) return false;
@@ -41,13 +42,13 @@ struct LoopGroup {
       cv.notify_all();
       return true;
     }
-    if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return gen != g || broken; }) || broken) {
-      broken = true;
-      cv.notify_all();
-      return false;
-    }
-    return true;
+    cv.wait_for(lk, std::chrono::seconds(timeout_s), [&] { return gen != g || broken; });
+    if (gen != g) return true;  // completed (a rank may have left right after it)
+    broken = true;
+    cv.notify_all();
+    return false;
   }
+  int timeout_s = 300;
 };
 
 namespace {
@@ -156,6 +157,8 @@ COBALT_API int cobalt_comm_loop_group_free(void* group) {
 void loop_release(CobaltComm* c) {
   std::lock_guard<std::mutex> lk(c->group->mu);
   --c->group->refs;
+  c->group->broken = true;  // a departed rank can never join another collective
+  c->group->cv.notify_all();
 }
 
 int loop_allreduce(CobaltComm* c, void* buf, int64_t count, int dtype, int op, hipStream_t stream) {

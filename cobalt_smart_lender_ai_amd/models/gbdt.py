@@ -16,6 +16,7 @@ histogram trees (K14-K20). See ``csrc/gbdt.hip`` for the device design.
 """
 from __future__ import annotations
 
+import ctypes
 import json
 import logging
 import math
@@ -347,6 +348,8 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
             for s0 in range(T0, T, seg):
                 s1 = min(T, s0 + seg)
                 tr.grow(s0, s1 - s0)
+                if world > 1:  # fail fast (abort the communicator) if a peer rank dies mid-segment
+                    _watch_segment(dist, dev, s0, s1)
                 tp = rep.mark("grow", tp, dev)
                 seg_nodes = tr.fetch(s0, s1 - s0)
                 tp = rep.mark("fetch", tp, dev)
@@ -385,6 +388,19 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         report.extra["cuts"] = bd.cuts
         report.extra["nbins"] = bd.nbins
     return bst
+
+
+def _watch_segment(dist, dev, s0: int, s1: int) -> None:
+    from .. import _native
+    from ..parallel import dist as pdist
+
+    ev = torch.cuda.Event()
+    ev.record()
+    comm = dist.native_comm
+    lib = _native.lib()
+    pdist.wait_with_watchdog(ev.query, timeout_s=pdist.collective_timeout_s(),
+                             comm_error=(lambda: lib.cobalt_comm_async_error(ctypes.c_void_p(comm))) if comm else None,
+                             abort=lambda: pdist.abort_native_comm(dist), what=f"trees {s0}..{s1 - 1}")
 
 
 class InjectedFault(RuntimeError):

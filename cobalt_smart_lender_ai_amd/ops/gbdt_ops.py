@@ -84,6 +84,24 @@ def bin_matrix(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> tupl
     return bins, binsT
 
 
+def bin_matrix_into(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor, records: torch.Tensor,
+                    binsT: torch.Tensor, row0: int) -> None:
+    """Quantise the chunk ``X`` [n, F] (CUDA) in place into rows ``row0 .. row0+n`` of preallocated
+    ``records`` [N, stride] and ``binsT`` [F, N] (streamed ingestion: no per-chunk copies)."""
+    X = X.contiguous()
+    n, F = X.shape
+    N, st = records.shape
+    if binsT.shape != (F, N) or row0 < 0 or row0 + n > N or st != row_stride(F):
+        raise ValueError("chunk does not fit the preallocated binned matrix")
+    if not (records.is_contiguous() and binsT.is_contiguous()):
+        raise ValueError("records/binsT must be contiguous")
+    rc = _native.lib().cobalt_bin_matrix_ld(X.data_ptr(), n, F, F, cuts.contiguous().data_ptr(),
+                                            nbins.to(torch.int32).contiguous().data_ptr(),
+                                            records.data_ptr() + row0 * st, st, binsT.data_ptr() + row0, N,
+                                            _native.stream_handle())
+    _native.check(rc, "cobalt_bin_matrix_ld")
+
+
 class GpuGbdtTrainer:
     def __init__(self, *, n_rows: int, n_feat: int, max_depth: int, max_trees: int, eta: float,
                  reg_lambda: float, reg_alpha: float, gamma: float, min_child_weight: float, subsample: float,

@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import datetime
 import os
+import time
 from dataclasses import dataclass, field
 
 import torch
@@ -148,6 +149,48 @@ def create_native_comm(ctx: DistContext) -> int:
     if rc != 0:
         raise RuntimeError(f"ncclCommInitRank failed: {lib.cobalt_comm_last_error().decode()}")
     return int(handle.value)
+
+
+class CollectiveTimeout(RuntimeError):
+    """A data-parallel step did not finish in time (a peer rank died or hung); the communicator has
+    been aborted so this rank's GPU work is released and the process can exit cleanly."""
+
+
+def collective_timeout_s() -> float:
+    """Watchdog deadline for one enqueued training segment (``COBALT_COLLECTIVE_TIMEOUT_S``)."""
+    return float(os.environ.get("COBALT_COLLECTIVE_TIMEOUT_S", "1800"))
+
+
+def wait_with_watchdog(done: "callable", *, timeout_s: float, comm_error: "callable | None" = None,
+                       abort: "callable | None" = None, poll_s: float = 2e-4, what: str = "collective") -> None:
+    """Poll ``done()`` (e.g. a HIP event query after an enqueued segment of trees) until it is true.
+
+    Fails fast instead of hanging forever when a peer is gone: if ``comm_error()``
+    reports an asynchronous communicator error, or ``timeout_s`` passes, ``abort()`` is called (it
+    aborts the RCCL communicator, which releases the collectives this rank's stream is blocked
+    in) and :class:`CollectiveTimeout` is raised. The poll interval is capped at ``poll_s`` so the
+    watchdog adds at most that much latency to a healthy step."""
+    t0 = time.monotonic()
+    sleep = 1e-5
+    while not done():
+        err = comm_error() if comm_error is not None else 0
+        late = time.monotonic() - t0 > timeout_s
+        if err or late:
+            if abort is not None:
+                abort()
+            reason = f"communicator error {err}" if err else f"no progress for {timeout_s:.0f} s"
+            raise CollectiveTimeout(f"{what}: {reason}; communicator aborted")
+        time.sleep(sleep)
+        sleep = min(sleep * 2, poll_s)
+
+
+def abort_native_comm(ctx: DistContext) -> None:
+    """Abort (not destroy) the native communicator: unblocks kernels waiting on dead peers."""
+    if ctx.native_comm:
+        from .. import _native
+
+        _native.lib().cobalt_comm_destroy(ctypes.c_void_p(ctx.native_comm), 1)
+        ctx.native_comm = None
 
 
 def get_context() -> DistContext:

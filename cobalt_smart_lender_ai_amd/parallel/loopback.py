@@ -110,10 +110,9 @@ def run_ranks(world: int, fn: Callable[[LoopbackContext], Any], device: str | to
         t.join()
     torch.cuda.synchronize(dev)
     lib.cobalt_comm_loop_group_free(grp)
-    for e in errors:
-        if e is not None and not isinstance(e, threading.BrokenBarrierError):
-            raise e
-    for e in errors:
-        if e is not None:
-            raise e
+    failed = [e for e in errors if e is not None]
+    if failed:  # the root cause first (peers fail with barrier / communicator errors after it)
+        first = next((e for e in failed if not isinstance(e, threading.BrokenBarrierError)), failed[0])
+        first.rank_errors = errors
+        raise first
     return results

@@ -146,3 +146,18 @@ def test_continue_training_from_model_equals_longer_fit():
     clf = gbdt.GBDTClassifier(device="cpu", **{**p8, "n_estimators": 3})
     clf.fit(X, y, xgb_model=first)
     assert clf.get_booster().save_raw("ubj") == full.save_raw("ubj")
+
+
+def test_collective_watchdog_aborts_and_raises():
+    from cobalt_smart_lender_ai_amd.parallel import dist as pdist
+
+    aborted = []
+    with pytest.raises(pdist.CollectiveTimeout, match="no progress"):
+        pdist.wait_with_watchdog(lambda: False, timeout_s=0.05, abort=lambda: aborted.append(1))
+    assert aborted == [1]
+    aborted.clear()
+    with pytest.raises(pdist.CollectiveTimeout, match="communicator error 5"):
+        pdist.wait_with_watchdog(lambda: False, timeout_s=60, comm_error=lambda: 5, abort=lambda: aborted.append(1))
+    assert aborted == [1]
+    calls = iter([False, False, True])
+    pdist.wait_with_watchdog(lambda: next(calls), timeout_s=1, comm_error=lambda: 0)

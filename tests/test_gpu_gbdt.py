@@ -197,3 +197,38 @@ def test_gpu_data_parallel_multi_rank_loopback(world):
 
     outs = loopback.run_ranks(world, rank_fit)
     assert all(o == ref for o in outs)
+
+
+def test_gpu_data_parallel_rank_failure_fails_fast_and_resumes(tmp_path, monkeypatch):
+    """A rank dies mid-fit (fault injection): its peer fails fast instead of hanging in the next
+    collective, and a restarted 2-rank job resumes from the checkpoint to the uninterrupted model."""
+    import time
+
+    from cobalt_smart_lender_ai_amd.parallel import loopback
+    from cobalt_smart_lender_ai_amd.parallel.dist import shard_range
+
+    n = 200_000
+    X, y = _data(n, seed=17)
+    params = dict(n_estimators=8, max_depth=6, learning_rate=0.2, subsample=0.8, random_state=9)
+    ref = gbdt.train(X, y, params, device="cuda").save_raw("ubj")
+    ck = str(tmp_path / "dp_ck.ubj")
+
+    def rank_fit(ctx):
+        s, e = shard_range(n, ctx.rank, ctx.world)
+        b = gbdt.train(X[s:e], y[s:e], params, device="cuda", dist=ctx, n_rows_global=n, row_offset=s,
+                       checkpoint_path=ck, checkpoint_every=2)
+        return b.save_raw("ubj")
+
+    monkeypatch.setenv("COBALT_FAULT_AFTER_TREES", "4")
+    monkeypatch.setenv("COBALT_FAULT_RANK", "1")
+    t0 = time.monotonic()
+    with pytest.raises(Exception) as ei:
+        loopback.run_ranks(2, rank_fit)
+    assert time.monotonic() - t0 < 120
+    errs = ei.value.rank_errors
+    assert isinstance(errs[1], gbdt.InjectedFault)
+    assert errs[0] is not None  # the surviving rank failed fast (communicator error), did not hang
+    monkeypatch.delenv("COBALT_FAULT_AFTER_TREES")
+    monkeypatch.delenv("COBALT_FAULT_RANK")
+    outs = loopback.run_ranks(2, rank_fit)
+    assert all(o == ref for o in outs)
