@@ -378,8 +378,10 @@ __device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, int
 // evaluation and partition kernels, resets the level's partition counters and the item count.
 // `build` is the child whose GLOBAL histogram sits in hist_b after the reduce (+ all-reduce): the
 // locally smaller one on one GPU, always the left one under DP.
-__device__ void publish_level(const GbdtDev& d, int level, int total) {
-  if (threadIdx.x == 0) d.counters[0] = total;
+// With keep_build (fused partition path) the build flags chosen by k_eval stay, and total < 0 leaves
+// the item count alone (it was written by the fused pass itself).
+__device__ void publish_level(const GbdtDev& d, int level, int total, bool keep_build = false) {
+  if (total >= 0 && threadIdx.x == 0) d.counters[0] = total;
   if (level == 0) return;
   const int npairs = 1 << (level - 1);
   for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
@@ -393,8 +395,10 @@ __device__ void publish_level(const GbdtDev& d, int level, int total) {
     d.nodes[L].count = lc;
     d.nodes[R].start = par.start + lc;
     d.nodes[R].count = par.count - lc;
-    d.nodes[L].build = left_small ? 1 : 0;
-    d.nodes[R].build = left_small ? 0 : 1;
+    if (!keep_build) {
+      d.nodes[L].build = left_small ? 1 : 0;
+      d.nodes[R].build = left_small ? 0 : 1;
+    }
   }
   const int first = (1 << level) - 1, nlev = 1 << level;
   for (int i = threadIdx.x; i < nlev; i += blockDim.x) {
@@ -709,7 +713,9 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
 // global atomic per non-zero cell per (run, slot) -- coalesced, 30-100x fewer than per-block flushes.
 constexpr int kRedItems = 16;
 
-__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity) {
+__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int publish) {
+  // fused partition path: block (0, 0) publishes the level's node ranges from the finished claims
+  if (publish > 0 && blockIdx.x == 0 && blockIdx.y == 0) publish_level(d, publish, -1, true);
   const int n_items = d.counters[0];
   const int i0 = blockIdx.x * kRedItems;
   if (i0 >= n_items) return;
@@ -1000,6 +1006,12 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     Node& R = nodes[2 * n + 2];
     L.status = kActive; L.G = best.gl; L.H = best.hl;
     R.status = kActive; R.G = G - best.gl; R.H = H - best.hl;
+    // Child histogrammed from rows by the fused partition pass (k_part_hist): the one with the
+    // smaller GLOBAL hessian (known here, before the partition; identical on every rank, and the
+    // host oracle's choice). The unfused path overrides this with row counts in publish_level.
+    const int lb = best.hl <= H - best.hl ? 1 : 0;
+    L.build = lb;
+    R.build = 1 - lb;
     if (level + 1 == d.max_depth) {  // children are at max depth: finalise them as leaves here
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -1101,12 +1113,13 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   if (threadIdx.x == 0) {
     int tl = 0, tr = 0;
     for (int k = 0; k < kPartWaves; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
-    int32_t* cursor = d.cursors + 2 * w.node;
     if (d.ablate == 12) {  // timing-only: no cursor atomics
       s_base[0] = 0; s_base[1] = 0;
-    } else {
-      s_base[0] = tl ? atomicAdd(cursor, tl) : 0;
-      s_base[1] = tr ? atomicAdd(cursor + 1, tr) : 0;
+    } else {  // both cursors in one 64-bit claim (left = low word, right = high word)
+      const unsigned long long c = atomicAdd(reinterpret_cast<unsigned long long*>(d.cursors + 2 * w.node),
+                                             ((unsigned long long)(uint32_t)tr << 32) | (uint32_t)tl);
+      s_base[0] = (int32_t)(uint32_t)c;
+      s_base[1] = (int32_t)(c >> 32);
     }
   }
   __syncthreads();
@@ -1124,6 +1137,142 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
     bl += __popcll(lm);
     br += __popcll(rm);
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused row partition of level L + histogram of level L + 1 (32-byte records, one feature tile).
+// The pass that routes the rows of level L's split nodes to their children also builds, from the
+// same rows, the histogram of the child k_eval chose to build (smaller global hessian), so that
+// child's rows are never re-read through ridx by a separate histogram launch, and the record
+// gathers are issued while the block's cursor claim is in flight. Both cursors of a node are
+// claimed with ONE 64-bit atomic: same-address device atomics serialise at the memory side
+// (~88 per us per word), which bounded the shallow levels, where every item claims on one node.
+// Work item = <= kPW * kPS * 64 rows of one parent node; its partial histogram goes to the item's
+// slab row with slot = the parent's position in level L (= the child pair's slot in level L + 1).
+// ------------------------------------------------------------------------------------------
+constexpr int kPartHistWaves = 8, kPartHistSteps = 16;
+constexpr int kPartHistRows = kPartHistWaves * kPartHistSteps * kWave;  // 8192 rows per work item
+
+template <int kPW, int kPS>
+__global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, int64_t zero_next, int level,
+                                                        int chunk, int tree) {
+  extern __shared__ uint64_t s_hist[];
+  __shared__ int32_t s_cnt[2][kPW];
+  __shared__ int32_t s_base[2];
+  __shared__ int s_plan[5];
+  __shared__ int64_t s_tot[2][16];
+  static_assert(kPS <= 32 && kPS % 4 == 0, "step bit masks are 32-bit; hist pipeline of 4 steps");
+  {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
+    int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
+    const int64_t nz = zero_next / 2;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
+      zp[e] = make_int4(0, 0, 0, 0);
+  }
+  const int item = blockIdx.x;
+  const int first = (1 << level) - 1;
+  const PlanOut pl = block_plan(1 << level, chunk, item, [&](int e) {
+    const Node& n = d.nodes[first + e];
+    return (n.status == kSplit && n.count > 0) ? PlanEntry{first + e, 0, n.start, n.count} : PlanEntry{-1, 0, 0, 0};
+  }, s_plan);
+  if (item == 0 && threadIdx.x == 0) d.counters[0] = pl.total;  // work items of the next level's reduce
+  if (pl.node < 0) return;
+  const int q = pl.node;
+  const Node nd = d.nodes[q];
+  const bool build_left = d.nodes[2 * q + 1].build != 0;
+  if (threadIdx.x == 0) {
+    WorkItem w;
+    w.node = build_left ? 2 * q + 1 : 2 * q + 2;
+    w.slot = q - first;
+    w.begin = pl.begin;
+    w.end = pl.end;
+    d.items_h[item] = w;
+  }
+  const int F = d.F;
+  const int entries = d.tile_entries[0] + kWave;  // + per-lane trash cells
+  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
+  const HistLanes hl = hist_lanes(d, tree, 0, F);
+
+  // pass 1: row ids + split-feature bins -> directions and per-wave counts (rows stay in registers)
+  const bool identity = parity == 0 && q == 0;
+  const int32_t* cur = d.ridx[parity];
+  int32_t* nxt = d.ridx[parity ^ 1];
+  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.n;
+  const int j = nd.bin;
+  const bool dl = nd.default_left != 0;
+  const int wv = wave_id(), lane = lane_id();
+  const int len = pl.end - pl.begin;
+  const int per = ((len + kPW - 1) / kPW + kWave - 1) / kWave * kWave;
+  const int wb = min(pl.end, pl.begin + wv * per), we = min(pl.end, wb + per);
+  int r[kPS];
+  uint32_t lbits = 0, vbits = 0;
+  int nl = 0, nr = 0;
+#pragma unroll
+  for (int k = 0; k < kPS; ++k) {
+    const int i = wb + k * kWave + lane;
+    r[k] = i < we ? (identity ? i : cur[i]) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < kPS; ++k) {
+    const bool valid = r[k] >= 0;
+    const bool left = valid && goes_left(col, r[k], j, dl);
+    lbits |= (uint32_t)left << k;
+    vbits |= (uint32_t)valid << k;
+    const uint64_t lm = __ballot(left), vm = __ballot(valid);
+    nl += __popcll(lm);
+    nr += __popcll(vm) - __popcll(lm);
+  }
+  if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nr; }
+  __syncthreads();  // (also orders the LDS histogram zeroing before the atomics below)
+  unsigned long long claim = 0;
+  if (threadIdx.x == 0) {
+    int tl = 0, tr = 0;
+    for (int k = 0; k < kPW; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
+    claim = atomicAdd(reinterpret_cast<unsigned long long*>(d.cursors + 2 * q),
+                      ((unsigned long long)(uint32_t)tr << 32) | (uint32_t)tl);
+  }
+  // pass 2 (while the claim is in flight): histogram of the build side from the records.
+  // Loads are unconditional (non-build lanes read row 0, a broadcast) so the compiler keeps all
+  // four rows of a step group in flight; only the LDS atomics are predicated.
+  const uint32_t want = build_left ? lbits : (vbits & ~lbits);
+  int64_t tg = 0, th = 0;
+  constexpr int U = 4;
+#pragma unroll
+  for (int k0 = 0; k0 < kPS; k0 += U) {
+    uint4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rk = ((want >> (k0 + u)) & 1u) ? r[k0 + u] : 0;
+      const uint4* rec = reinterpret_cast<const uint4*>(d.bins + (int64_t)rk * 32);
+      a[u] = rec[0];
+      b[u] = rec[1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if ((want >> (k0 + u)) & 1u) {
+        tg += (int64_t)(int32_t)b[u].w;
+        th += (int64_t)b[u].z;
+        hist_add_rec32(s_hist, hl, F, a[u], b[u]);
+      }
+    }
+  }
+  if (threadIdx.x == 0) { s_base[0] = (int32_t)(uint32_t)claim; s_base[1] = (int32_t)(claim >> 32); }
+  __syncthreads();  // claim published; every histogram atomic of the block has completed
+  // pass 3: scatter (left ascending from the node start, right descending from its end)
+  int bl = s_base[0], br = s_base[1];
+  for (int k = 0; k < wv; ++k) { bl += s_cnt[0][k]; br += s_cnt[1][k]; }
+  const int rend = nd.start + nd.count - 1;
+#pragma unroll
+  for (int k = 0; k < kPS; ++k) {
+    const bool valid = (vbits >> k) & 1u, left = (lbits >> k) & 1u;
+    const uint64_t lm = __ballot(valid && left), rm = __ballot(valid && !left);
+    if (valid) {
+      if (left) nxt[nd.start + bl + mask_rank(lm)] = r[k];
+      else nxt[rend - (br + mask_rank(rm))] = r[k];
+    }
+    bl += __popcll(lm);
+    br += __popcll(rm);
+  }
+  hist_flush(d, s_hist, hl, item, 0, F, tg, th, true, s_tot);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1287,6 +1436,8 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t);
   if (c->lds_hist > 64 * 1024) {
     CK(hipFuncSetAttribute((const void*)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
+    CK(hipFuncSetAttribute((const void*)k_part_hist<kPartHistWaves, kPartHistSteps>,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
   const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
   if (grad_hist_lds > 64 * 1024) {
@@ -1310,11 +1461,19 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const bool fuse_root = d.stride == 32 && d.F <= 24 && ftiles == 1 && d.ablate == 0 &&
                          getenv("COBALT_NO_FUSED_ROOT") == nullptr;
-  // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items)
-  const int root_chunk = std::min(chunk_hist(d, 0), 8192);
-  // Per tree: grad (+ node-table init, + archive/apply of the previous tree), then per level
-  // hist (self-planned) -> reduce -> [RCCL histogram all-reduce] -> eval -> partition (self-planned)
-  // [-> RCCL child-count all-reduce]; the last split level's children are finalised by eval.
+  // partition fused with the next level's histogram (same record-layout conditions); opt-in while it
+  // measures slower than the separate passes (COBALT_FUSED_PART=1)
+  const bool env_fuse_part = getenv("COBALT_FUSED_PART") != nullptr && atoi(getenv("COBALT_FUSED_PART")) != 0;
+  const bool fuse_part = fuse_root && env_fuse_part;
+  // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
+  // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
+  static const int env_root = getenv("COBALT_ROOT_CHUNK") ? atoi(getenv("COBALT_ROOT_CHUNK")) : 0;
+  const int root_chunk = env_root > 0 ? std::min(16384, std::max(1024, env_root / 64 * 64))
+                                      : std::min(chunk_hist(d, 0), 8192);
+  // Per tree: grad (+ root histogram, node-table init, archive/apply of the previous tree), then per
+  // level: [fused: partition of the previous level + this level's histogram | unfused: hist] ->
+  // reduce -> [RCCL histogram all-reduce] -> eval [-> unfused: partition]; the last split level's
+  // children are finalised by eval.
   for (int t = t0; t < t0 + n_trees; ++t) {
     if (t >= c->cfg.max_trees) return -10;
     d.nodes = d.nodes_buf[t & 1];
@@ -1330,22 +1489,35 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
     for (int level = 0; level < D; ++level) {
       const int parity = level & 1;
       const int slots = level == 0 ? 1 : (1 << (level - 1));
-      const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
-      const int ub = ceil_div(d.n, chh) + (1 << level);
-      if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-        hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level, chh);
+      int ub;  // upper bound on the level's histogram work items
+      if (fuse_part && level > 0) {  // partition of level - 1 and this level's histogram in one pass
+        const int pl = level - 1;
+        ub = ceil_div(d.n, kPartHistRows) + (1 << pl);
+        hipLaunchKernelGGL((k_part_hist<kPartHistWaves, kPartHistSteps>), dim3(ub), dim3(kPartHistWaves * kWave),
+                           c->lds_hist, stream, d, pl & 1, (int64_t)(1 << pl) * d.slot_elems, pl, kPartHistRows, t);
+      } else {
+        const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
+        ub = ceil_div(d.n, chh) + (1 << level);
+        if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
+          hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level,
+                             chh);
+      }
       hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
-                         dim3(256), 0, stream, d, parity);
+                         dim3(256), 0, stream, d, parity, fuse_part ? level : 0);
       CK_LAUNCH();
       if (dp) {
-        hipLaunchKernelGGL(k_dp_local, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d, level,
-                           parity);
-        CK_LAUNCH();
+        // unfused: ranks built their locally smaller child -> turn it into the local LEFT child;
+        // fused: every rank built the globally chosen child, all-reduced as is
+        if (!fuse_part) {
+          hipLaunchKernelGGL(k_dp_local, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d,
+                             level, parity);
+          CK_LAUNCH();
+        }
         int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
         if (rc) return rc;
       }
       hipLaunchKernelGGL(k_eval, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t);
-      if (level + 1 < D) {  // the last split level's children are leaves: no row lists needed
+      if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
         const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;

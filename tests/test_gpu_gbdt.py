@@ -232,3 +232,28 @@ def test_gpu_data_parallel_rank_failure_fails_fast_and_resumes(tmp_path, monkeyp
     monkeypatch.delenv("COBALT_FAULT_RANK")
     outs = loopback.run_ranks(2, rank_fit)
     assert all(o == ref for o in outs)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_gpu_fused_partition_histogram_pass(world, monkeypatch):
+    """The fused partition + next-level histogram pass (COBALT_FUSED_PART=1, k_part_hist) grows the
+    same trees as the host oracle, alone and under the multi-rank protocol (loopback group)."""
+    from cobalt_smart_lender_ai_amd.parallel import loopback
+    from cobalt_smart_lender_ai_amd.parallel.dist import shard_range
+
+    n = 200_000
+    X, y = _data(n, seed=21)
+    params = dict(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9, colsample_bytree=0.8,
+                  random_state=5, scale_pos_weight=6.0)
+    ref = gbdt.train(X, y, params, device="cpu").save_raw("ubj")
+    monkeypatch.setenv("COBALT_FUSED_PART", "1")
+    if world == 1:
+        assert gbdt.train(X, y, params, device="cuda").save_raw("ubj") == ref
+        return
+
+    def rank_fit(ctx):
+        s, e = shard_range(n, ctx.rank, ctx.world)
+        return gbdt.train(X[s:e], y[s:e], params, device="cuda", dist=ctx, n_rows_global=n,
+                          row_offset=s).save_raw("ubj")
+
+    assert all(o == ref for o in loopback.run_ranks(world, rank_fit))
