@@ -121,6 +121,7 @@ struct GbdtDev {
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
+  int32_t by_hess;        // timing experiment (COBALT_BUILD_BY_HESS): unfused path builds k_eval's hessian choice
   int64_t n;
   int64_t row_offset;
   int32_t F, stride, max_depth, max_nodes, chunk, feat_tile;
@@ -370,7 +371,7 @@ __device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, int
   const Node& par = d.nodes[q];
   if (par.status != kSplit) return PlanEntry{-1, p, 0, 0};
   const int lc = d.cursors[2 * q];
-  const bool left_small = lc <= d.cursors[2 * q + 1];
+  const bool left_small = d.by_hess ? d.nodes[2 * q + 1].build != 0 : lc <= d.cursors[2 * q + 1];
   return left_small ? PlanEntry{2 * q + 1, p, par.start, lc} : PlanEntry{2 * q + 2, p, par.start + lc, par.count - lc};
 }
 
@@ -488,6 +489,7 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // holding the freshly quantised (g, h) and the bins -- the separate root histogram pass (a full
 // 32 B/row re-read) disappears. Block b = root work item b: rows [b*chunk, (b+1)*chunk).
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
+template <int U>
 __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
   extern __shared__ uint64_t s_dyn[];
   __shared__ int64_t s_tot[2][16];
@@ -525,7 +527,6 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   const HistLanes hl = hist_lanes(d, tree, 0, ft);
   const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
   int64_t tg = 0, th = 0;
-  constexpr int U = 2;
   const int B = blockDim.x;
   for (int64_t i0 = begin + threadIdx.x; i0 < end; i0 += U * B) {
     uint4 ra[U], rb[U];
@@ -596,7 +597,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   const int n_ent = level == 0 ? 1 : (1 << (level - 1));
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
                                 s_plan);
-  if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total);
+  if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total, d.by_hess != 0);
   if (pl.node < 0) return;
   WorkItem w;
   w.node = pl.node;
@@ -1364,6 +1365,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.hinv = 1.0 / cfg->hscale;
   d.seed = cfg->seed;
   d.ablate = getenv("COBALT_HIST_ABLATE") ? atoi(getenv("COBALT_HIST_ABLATE")) : 0;
+  d.by_hess = (getenv("COBALT_BUILD_BY_HESS") && !cfg->comm) ? 1 : 0;
   c->lds_hist = (size_t)cfg->feat_tile * kMaxBins * sizeof(uint64_t);
   int rc = 0;
   const size_t hist_bytes = (size_t)c->pairs_max * d.slot_elems * sizeof(int64_t);
@@ -1441,7 +1443,8 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   }
   const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
   if (grad_hist_lds > 64 * 1024) {
-    CK(hipFuncSetAttribute((const void*)k_grad_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
+    CK(hipFuncSetAttribute((const void*)k_grad_hist<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
+    CK(hipFuncSetAttribute((const void*)k_grad_hist<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
   }
   return 0;
 }
@@ -1461,6 +1464,8 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const bool fuse_root = d.stride == 32 && d.F <= 24 && ftiles == 1 && d.ablate == 0 &&
                          getenv("COBALT_NO_FUSED_ROOT") == nullptr;
+  // rows in flight per thread in the gradient + root histogram pass (COBALT_GRAD_U=4: +1%, within noise)
+  static const int grad_u = getenv("COBALT_GRAD_U") ? atoi(getenv("COBALT_GRAD_U")) : 2;
   // partition fused with the next level's histogram (same record-layout conditions); opt-in while it
   // measures slower than the separate passes (COBALT_FUSED_PART=1)
   const bool env_fuse_part = getenv("COBALT_FUSED_PART") != nullptr && atoi(getenv("COBALT_FUSED_PART")) != 0;
@@ -1479,8 +1484,11 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
     d.nodes = d.nodes_buf[t & 1];
     d.prev_nodes = d.nodes_buf[(t + 1) & 1];
     const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
-    if (fuse_root)
-      hipLaunchKernelGGL(k_grad_hist, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
+    if (fuse_root && grad_u == 4)
+      hipLaunchKernelGGL(k_grad_hist<4>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
+                         d, t, apply, root_chunk);
+    else if (fuse_root)
+      hipLaunchKernelGGL(k_grad_hist<2>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
                          d, t, apply, root_chunk);
     else
       hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
