@@ -9,6 +9,7 @@ Commands mirror the reference's scripts:
   train     tree model training (model_tree_train_test.py)
   train-nn  NN challenger (notebook 04 cells 31-44)
   serve     FastAPI scoring service (cobalt_fast_api.py, uvicorn)
+  dictionary  descriptions of columns from the LendingClub data dictionary workbook (LCDataDictionary.xlsx)
 
 The artifact store is ``--store`` or ``$COBALT_ARTIFACT_URI`` (a local directory or ``s3://bucket``).
 """
@@ -90,6 +91,16 @@ def cmd_serve(args) -> int:
     return 0
 
 
+def cmd_dictionary(args) -> int:
+    from .dataio import dictionary, synth
+
+    dd = dictionary.load_data_dictionary(args.xlsx)
+    cols = args.columns or synth.FEATURES
+    for c, desc in dictionary.describe_columns(cols, dd).items():
+        print(f"{c}\t{desc}")
+    return 0
+
+
 def main(argv: list[str] | None = None) -> int:
     logging.basicConfig(level=logging.INFO, format="[%(levelname)s] %(message)s")
     p = argparse.ArgumentParser(prog="cobalt_smart_lender_ai_amd")
@@ -123,6 +134,10 @@ def main(argv: list[str] | None = None) -> int:
     s.add_argument("--host", default="0.0.0.0")
     s.add_argument("--port", type=int, default=8000)
     s.set_defaults(fn=cmd_serve)
+    s = sub.add_parser("dictionary", help="column descriptions (default: the 20 deployed model features)")
+    s.add_argument("--xlsx", required=True, help="path to LCDataDictionary.xlsx")
+    s.add_argument("columns", nargs="*")
+    s.set_defaults(fn=cmd_dictionary)
     args = p.parse_args(argv)
     return args.fn(args)
 

@@ -19,6 +19,7 @@ reads the checkpoint with the static, non-executing pickle decoder and takes the
 """
 from __future__ import annotations
 
+import asyncio
 import io
 import os
 import re
@@ -157,7 +158,10 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
             if list(df.columns) != feats:
                 raise ValueError(f"feature_names mismatch: expected {feats}, got {list(df.columns)}")
             X = df.to_numpy(dtype=np.float32, na_value=np.nan)
-            df["prob_default"] = state["engine"].predict_proba(X)
+            # scored on a worker thread: the reference runs this blocking call on the event loop
+            # (SURVEY App. B.8), which stalls every concurrent /predict request behind a bulk file
+            loop = asyncio.get_running_loop()
+            df["prob_default"] = await loop.run_in_executor(None, state["engine"].predict_proba, X)
             df_clean = df.replace([np.inf, -np.inf], np.nan).astype(object).where(
                 df.replace([np.inf, -np.inf], np.nan).notna(), "null")
             return {"predictions": df_clean.to_dict(orient="records")}
