@@ -123,6 +123,7 @@ struct GbdtDev {
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
   int32_t by_hess;        // timing experiment (COBALT_BUILD_BY_HESS): unfused path builds k_eval's hessian choice
   int64_t n;
+  int64_t ldt;            // row pitch of binsT (= the rows the context was created for; n <= ldt)
   int64_t row_offset;
   int32_t F, stride, max_depth, max_nodes, chunk, feat_tile;
   int64_t slot_elems;     // (ncells + 1) * 2: compact histogram slot (int64 g, h per cell + node total)
@@ -319,6 +320,148 @@ __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
        i += (int64_t)gridDim.x * blockDim.x)
     d.margin[i] += tree_leaf(d, i, s_meta, s_leaf);
 }
+
+// Start of a tree grown from precomputed gradients (external-memory path): node-table reset and the
+// root histogram slot zeroed (k_hist_reduce accumulates into it; k_grad does this on the normal path).
+__global__ __launch_bounds__(256) void k_tree_begin(GbdtDev d) {
+  int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
+       e += (int64_t)gridDim.x * blockDim.x)
+    zp[e] = make_int4(0, 0, 0, 0);
+  if (blockIdx.x == 0) init_tree_block(d);
+}
+
+// ------------------------------------------------------------------------------------------
+// External-memory training (BASELINE.json config "100M-row out-of-core GBDT with
+// host-DRAM spill"). The quantised row records live in host memory as pages; per tree every page
+// streams through k_ooc_page, which
+//   * applies the previous tree to the rows' margins (margins / labels / weights stay on the device),
+//   * computes binary:logistic g, h (fp64, as k_grad) and ghat = sqrt(g^2 + h^2),
+//   * keeps a minimal-variance sample (MVS -- the sampler of XGBoost's gradient_based external
+//     memory mode): row i with probability p_i = min(1, ghat_i / mu), its pair reweighted by 1/p_i
+//     (unbiased histograms; |g/p|, h/p <= mu, so the fixed-point scales hold when mu <= w_max),
+//   * compacts kept rows into the trainer's row records + feature-major bins (one wave-aggregated
+//     claim per wave; the order is irrelevant because every histogram sum is an exact integer),
+//   * counts ghat in kOocBins log-spaced bins (binary exponent x 16 mantissa steps, exact integer
+//     counts -> the host derives the next mu deterministically, models/external.py).
+// The in-core trainer then grows the tree on the sample (cobalt_gbdt_grow_sampled).
+// ------------------------------------------------------------------------------------------
+constexpr int kOocBins = 2048;
+
+__device__ __forceinline__ int ooc_bin(double v) {
+  if (!(v > 0.0)) return 0;
+  int e;
+  const double f = frexp(v, &e);  // v = f * 2^e, f in [0.5, 1)
+  const int b = (e + 64) * 16 + (int)floor((f - 0.5) * 32.0);
+  return b < 1 ? 1 : (b >= kOocBins ? kOocBins - 1 : b);
+}
+
+__global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ page, int64_t n, int64_t r0, int F,
+                                                  const Node* __restrict__ prev, int max_nodes,
+                                                  float* __restrict__ margin, const float* __restrict__ label,
+                                                  const float* __restrict__ weight, uint64_t key, int64_t row_offset,
+                                                  double mu, double gscale, double hscale, uint8_t* __restrict__ srec,
+                                                  uint8_t* __restrict__ sbinsT, int64_t cap,
+                                                  unsigned long long* __restrict__ counter,
+                                                  unsigned int* __restrict__ hist) {
+  __shared__ uint32_t s_meta[2047];
+  __shared__ float s_leaf[2047];
+  __shared__ unsigned int s_h[kOocBins];
+  for (int i = threadIdx.x; i < kOocBins; i += blockDim.x) s_h[i] = 0u;
+  if (prev != nullptr)
+    for (int i = threadIdx.x; i < max_nodes; i += blockDim.x) {
+      const Node nd = prev[i];
+      s_meta[i] = (uint32_t)(nd.feat & 0xFFFF) | ((uint32_t)(nd.bin & 0xFF) << 16) |
+                  ((uint32_t)(nd.default_left & 1) << 24) | ((nd.status == kSplit ? 1u : 0u) << 25);
+      s_leaf[i] = nd.leaf_value;
+    }
+  __syncthreads();
+  const int lane = lane_id();
+  // wave-uniform loop (ballots below): every lane of a wave iterates the same bases
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    const bool in = i < n;
+    bool keep = false;
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = make_uint4(0, 0, 0, 0);
+    if (in) {
+      const uint4* rec = reinterpret_cast<const uint4*>(page + i * 32);
+      ra = rec[0];
+      rb = rec[1];
+      float mf = margin[r0 + i];
+      if (prev != nullptr) {
+        int nx = 0;
+        uint32_t m = s_meta[0];
+        while (m & (1u << 25)) {
+          const int f = m & 0xFFFF, q = f >> 2;
+          const uint32_t word = q == 0 ? ra.x : q == 1 ? ra.y : q == 2 ? ra.z : q == 3 ? ra.w : q == 4 ? rb.x : rb.y;
+          const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
+          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          nx = 2 * nx + (left ? 1 : 2);
+          m = s_meta[nx];
+        }
+        mf += s_leaf[nx];
+        margin[r0 + i] = mf;
+      }
+      const double p = 1.0 / (1.0 + exp(-(double)mf));
+      const double y = (double)label[r0 + i], w = (double)weight[r0 + i];
+      const double g = (p - y) * w;
+      const double h = fmax(p * (1.0 - p), 1e-16) * w;
+      const double gh = sqrt(g * g + h * h);
+      atomicAdd(&s_h[ooc_bin(gh)], 1u);
+      if (mu > 0.0) {
+        const double pk = gh >= mu ? 1.0 : gh / mu;
+        keep = uniform01(splitmix64(key ^ (uint64_t)(row_offset + r0 + i))) < pk;
+        if (keep) {
+          int64_t gq = (int64_t)rint(g / pk * gscale), hq = (int64_t)rint(h / pk * hscale);
+          gq = gq > 65536 ? 65536 : (gq < -65536 ? -65536 : gq);
+          hq = hq > 65536 ? 65536 : (hq < 0 ? 0 : hq);
+          rb.z = (uint32_t)hq;
+          rb.w = (uint32_t)(int32_t)gq;
+        }
+      }
+    }
+    const uint64_t km = __ballot(keep);
+    if (km) {
+      const int leader = __ffsll((unsigned long long)km) - 1;
+      unsigned long long b0 = 0;
+      if (lane == leader) b0 = atomicAdd(counter, (unsigned long long)__popcll(km));
+      b0 = __shfl(b0, leader, kWave);
+      if (keep) {
+        const int64_t slot = (int64_t)b0 + mask_rank(km);
+        if (slot < cap) {
+          uint4* dst = reinterpret_cast<uint4*>(srec + slot * 32);
+          dst[0] = ra;
+          dst[1] = rb;
+          for (int f = 0; f < F; ++f) {
+            const int q = f >> 2;
+            const uint32_t word = q == 0 ? ra.x : q == 1 ? ra.y : q == 2 ? ra.z : q == 3 ? ra.w : q == 4 ? rb.x : rb.y;
+            sbinsT[(int64_t)f * cap + slot] = (uint8_t)((word >> (8 * (f & 3))) & 0xffu);
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kOocBins; i += blockDim.x)
+    if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
+COBALT_API int cobalt_ooc_page(const uint8_t* page, int64_t n, int64_t r0, int F, const void* prev, int max_nodes,
+                               float* margin, const float* label, const float* weight, uint64_t key,
+                               int64_t row_offset, double mu, double gscale, double hscale, uint8_t* srec,
+                               uint8_t* sbinsT, int64_t cap, unsigned long long* counter, unsigned int* hist,
+                               hipStream_t stream) {
+  if (F < 1 || F > 24 || max_nodes > 2047 || n < 0) return -3;  // 32-byte records only
+  if (n == 0) return 0;
+  const int grid = std::max(1, std::min(ceil_div(n, 256), 256 * 8));
+  hipLaunchKernelGGL(k_ooc_page, dim3(grid), dim3(256), 0, stream, page, n, r0, F, static_cast<const Node*>(prev),
+                     max_nodes, margin, label, weight, key, row_offset, mu, gscale, hscale, srec, sbinsT, cap, counter,
+                     hist);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_ooc_bins() { return kOocBins; }
 
 // ------------------------------------------------------------------------------------------
 // Self-planning work lists. A pass over the rows of several nodes is cut into items of at most
@@ -1083,7 +1226,7 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   const bool identity = parity == 0 && w.node == 0;
   const int32_t* cur = d.ridx[parity];
   int32_t* nxt = d.ridx[parity ^ 1];
-  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.n;
+  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.ldt;
   const int j = nd.bin;
   const bool dl = nd.default_left != 0;
   const int wv = wave_id(), lane = lane_id();
@@ -1197,7 +1340,7 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
   const bool identity = parity == 0 && q == 0;
   const int32_t* cur = d.ridx[parity];
   int32_t* nxt = d.ridx[parity ^ 1];
-  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.n;
+  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.ldt;
   const int j = nd.bin;
   const bool dl = nd.default_left != 0;
   const int wv = wave_id(), lane = lane_id();
@@ -1344,6 +1487,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   }
   GbdtDev& d = c->d;
   d.n = N;
+  d.ldt = N;
   d.row_offset = cfg->row_offset;
   d.F = F;
   d.stride = cfg->row_stride;
@@ -1450,8 +1594,10 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
 }
 
 // Enqueue `n_trees` boosting rounds starting at tree index `t0`. No host synchronisation.
-COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream) {
-  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+// `sampled`: the row records already hold the (reweighted) gradient pairs of this tree's rows --
+// the external-memory path, where k_ooc_page wrote a fresh sample -- so the tree starts with a
+// node-table reset + a plain root histogram instead of the gradient pass, and no margins are kept.
+static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool sampled) {
   GbdtDev& d = c->d;
   const int D = d.max_depth;
   const int grad_grid = std::min(ceil_div(d.n, 256), 256 * 16);
@@ -1462,7 +1608,7 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
   const bool dp = c->cfg.comm != nullptr;
   d.dp = dp ? 1 : 0;
   // gradients + root histogram in one pass (32-byte records, one feature tile)
-  const bool fuse_root = d.stride == 32 && d.F <= 24 && ftiles == 1 && d.ablate == 0 &&
+  const bool fuse_root = !sampled && d.stride == 32 && d.F <= 24 && ftiles == 1 && d.ablate == 0 &&
                          getenv("COBALT_NO_FUSED_ROOT") == nullptr;
   // rows in flight per thread in the gradient + root histogram pass (COBALT_GRAD_U=4: +1%, within noise)
   static const int grad_u = getenv("COBALT_GRAD_U") ? atoi(getenv("COBALT_GRAD_U")) : 2;
@@ -1484,7 +1630,10 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
     d.nodes = d.nodes_buf[t & 1];
     d.prev_nodes = d.nodes_buf[(t + 1) & 1];
     const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
-    if (fuse_root && grad_u == 4)
+    if (sampled)
+      hipLaunchKernelGGL(k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
+                         stream, d);
+    else if (fuse_root && grad_u == 4)
       hipLaunchKernelGGL(k_grad_hist<4>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
                          d, t, apply, root_chunk);
     else if (fuse_root)
@@ -1492,7 +1641,7 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
                          d, t, apply, root_chunk);
     else
       hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
-    if (apply >= 0) c->applied = t;
+    if (apply >= 0 && !sampled) c->applied = t;
     CK_LAUNCH();
     for (int level = 0; level < D; ++level) {
       const int parity = level & 1;
@@ -1537,6 +1686,7 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
       CK_LAUNCH();
     }
     c->grown = t + 1;
+    if (sampled) c->applied = t + 1;  // no training margins on a per-tree sample
   }
   // archive the last tree of this call (later trees are archived by the next tree's k_grad)
   if (c->grown > t0) {
@@ -1551,6 +1701,30 @@ COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream
     c->applied = c->grown;
   }
   return 0;
+}
+
+COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream) {
+  return grow_impl(static_cast<GbdtCtx*>(h), t0, n_trees, stream, false);
+}
+
+// External memory: grow tree t from the sample the last k_ooc_page passes wrote into the trainer's
+// row records / feature-major bins (n_rows set by cobalt_gbdt_set_rows).
+COBALT_API int cobalt_gbdt_grow_sampled(void* h, int t, hipStream_t stream) {
+  return grow_impl(static_cast<GbdtCtx*>(h), t, 1, stream, true);
+}
+
+// Rows of the current sample (<= the capacity the context was created with).
+COBALT_API int cobalt_gbdt_set_rows(void* h, int64_t n) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  if (n < 0 || n > c->cfg.n_rows) return -13;
+  c->d.n = n;
+  return 0;
+}
+
+// Device pointer to the heap-ordered node records of tree t (read by k_ooc_page to apply it).
+COBALT_API void* cobalt_gbdt_tree_ptr(void* h, int t) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  return c->d.trees + (size_t)t * c->max_nodes;
 }
 
 // Copy node records of trees [t0, t0+n) to host memory (blocking on `stream`).

@@ -85,10 +85,10 @@ class _PinnedUploader:
         return out
 
 
-def bin_stream(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256, sketch_rows: int = 1 << 18,
-               device=None, dist=None, row_offset: int = 0,
-               n_rows_global: int | None = None) -> tuple[BinnedData, torch.Tensor]:
-    """Quantise a chunk stream; returns the binned matrix and the labels (on ``device``)."""
+def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256, sketch_rows: int = 1 << 18,
+                device=None, dist=None, row_offset: int = 0, n_rows_global: int | None = None):
+    """Quantile cuts of a chunk stream from the rows whose GLOBAL index is a multiple of the sketch
+    stride (the in-core sample). Returns ``(cuts, nbins, n_rows, n_rows_global, n_features)``."""
     dev = _resolve_device(device, None)
     world = dist.world if dist is not None else 1
     if n_rows is None:
@@ -96,7 +96,6 @@ def bin_stream(source: ChunkSource, *, n_rows: int | None = None, max_bin: int =
     N = int(n_rows)
     n_glob = n_rows_global if n_rows_global is not None else (
         int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
-    ts = time.perf_counter()
     stride = sketch.sample_stride(n_glob, sketch_rows)
     F = None
     parts, seen = [], 0
@@ -114,6 +113,18 @@ def bin_stream(source: ChunkSource, *, n_rows: int | None = None, max_bin: int =
     cuts, nbins = sketch.compute_cuts(samp, max_bin)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+    return cuts, nbins, N, n_glob, F
+
+
+def bin_stream(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256, sketch_rows: int = 1 << 18,
+               device=None, dist=None, row_offset: int = 0,
+               n_rows_global: int | None = None) -> tuple[BinnedData, torch.Tensor]:
+    """Quantise a chunk stream; returns the binned matrix and the labels (on ``device``)."""
+    dev = _resolve_device(device, None)
+    ts = time.perf_counter()
+    cuts, nbins, N, n_glob, F = stream_cuts(source, n_rows=n_rows, max_bin=max_bin, sketch_rows=sketch_rows,
+                                            device=dev, dist=dist, row_offset=row_offset,
+                                            n_rows_global=n_rows_global)
     t_sketch = time.perf_counter() - ts
     tb = time.perf_counter()
     bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)

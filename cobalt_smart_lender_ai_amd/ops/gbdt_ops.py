@@ -157,6 +157,18 @@ class GpuGbdtTrainer:
             raise RuntimeError(f"cobalt_gbdt_grow failed ({rc}): {self.lib.cobalt_comm_last_error().decode()}")
         _native.check(rc, "cobalt_gbdt_grow")
 
+    # -------------------------------------------------------------- external-memory (sampled) mode
+    def set_rows(self, n: int) -> None:
+        """Rows of the current sample written into the bound records (<= the created capacity)."""
+        _native.check(self.lib.cobalt_gbdt_set_rows(self.h, int(n)), "cobalt_gbdt_set_rows")
+
+    def grow_sampled(self, t: int) -> None:
+        """Grow tree ``t`` from the precomputed (reweighted) gradient pairs in the bound records."""
+        _native.check(self.lib.cobalt_gbdt_grow_sampled(self.h, t, _native.stream_handle()), "cobalt_gbdt_grow_sampled")
+
+    def tree_ptr(self, t: int) -> int:
+        return int(self.lib.cobalt_gbdt_tree_ptr(self.h, t))
+
     def fetch(self, t0: int, n: int) -> np.ndarray:
         out = np.zeros((n, self.max_nodes), dtype=NODE_DTYPE)
         rc = self.lib.cobalt_gbdt_fetch_trees(self.h, t0, n, out.ctypes.data, _native.stream_handle())
