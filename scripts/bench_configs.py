@@ -26,7 +26,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 
-def plumbing_10k(rows: int = 10_000) -> dict:
+def plumbing_10k(rows: int = 10_000, trees: int = 300) -> dict:
     import numpy as np
     from sklearn.linear_model import LogisticRegression
     from sklearn.preprocessing import StandardScaler
@@ -59,7 +59,7 @@ def plumbing_10k(rows: int = 10_000) -> dict:
     auc_lr = roc_auc(y[te], lr.predict_proba(sc.transform(Xf[te]))[:, 1])
     spw = float((y[tr] == 0).sum() / max((y[tr] == 1).sum(), 1))
     t0 = time.perf_counter()
-    b = gbdt.train(X[tr], y[tr], dict(n_estimators=300, max_depth=7, learning_rate=0.05, gamma=5.0,
+    b = gbdt.train(X[tr], y[tr], dict(n_estimators=trees, max_depth=7, learning_rate=0.05, gamma=5.0,
                                       scale_pos_weight=spw), device="cpu")
     t_gb = time.perf_counter() - t0
     auc_gb = roc_auc(y[te], b.predict_proba(X[te], device="cpu"))

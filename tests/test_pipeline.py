@@ -199,3 +199,18 @@ def test_raw_data_manifest_verify(tmp_path):
     assert st.get_bytes("dataset/1-raw/x") == blob
     (tmp_path / "raw" / "sample.csv").write_bytes(blob[:-1] + b"!")
     assert datasets.verify(tmp_path, (f,)) == {"raw/sample.csv": "md5 mismatch"}
+
+
+def test_baseline_plumbing_config_runs_end_to_end():
+    """BASELINE.json config 1 (10k-row sample, sklearn LogisticRegression on CPU): raw rows through the
+    reference cleaning + feature engineering into a working classifier (scripts/bench_configs.py)."""
+    import importlib.util
+    from pathlib import Path
+
+    spec = importlib.util.spec_from_file_location("bench_configs",
+                                                  Path(__file__).resolve().parents[1] / "scripts/bench_configs.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    r = mod.plumbing_10k(rows=4_000, trees=20)
+    assert r["rows_after_prep"] > 3_500 and r["features"] > 40
+    assert r["logreg_auc"] > 0.85 and r["gbdt_cpu_auc"] > 0.85
