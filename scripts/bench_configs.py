@@ -12,6 +12,10 @@
   ooc-100m       "100M-row out-of-core GBDT with host-DRAM spill"             (scripts/bench_external.py)
   score-1b       "Batch inference: 1B-row scoring via hipGraph on 8xMI355X" -- one 125M-row shard per
                  GPU (serve/batch_score.py; ranks are independent, so 8 GPUs = 8 x the shard rate)
+  cpu-hist-gbdt-10m  CPU reference point for the headline metric (scikit-learn's OpenMP histogram
+                 GBDT on the same 10M rows; the reference publishes no throughput)
+  pipeline-100k  the reference's training job (RFE 106 -> 20 + 20 x 3-fold search + refit) end to end
+                 on a 100k-row synthetic sample (scripts/bench_pipeline.py)
 """
 from __future__ import annotations
 
@@ -70,6 +74,36 @@ def plumbing_10k(rows: int = 10_000, trees: int = 300) -> dict:
             "data": "synthetic raw LendingClub-shaped rows (dataio/synth_raw.py), reference-date 2025-07-04"}
 
 
+def cpu_hist_gbdt(rows: int = 10_000_000) -> dict:
+    """CPU reference point for the headline metric: scikit-learn's HistGradientBoostingClassifier
+    (OpenMP C++ histogram GBDT, the closest installed stand-in for the reference's XGBoost CPU
+    `hist` fit; xgboost itself is not installed) on the same synthetic 10M x 20 rows and the deployed
+    hyper-parameters (300 trees, depth 7, eta 0.05, lambda 1, 255 bins, class weight = spw)."""
+    import os
+
+    from sklearn.ensemble import HistGradientBoostingClassifier
+
+    from cobalt_smart_lender_ai_amd.dataio import synth
+    from cobalt_smart_lender_ai_amd.metrics.auc import roc_auc
+
+    X, y = synth.make_lendingclub(rows, seed=0)
+    Xte, yte = synth.make_lendingclub(1_000_000, seed=0, row_offset=rows)
+    X, y, Xte, yte = X.numpy(), y.numpy(), Xte.numpy(), yte.numpy()
+    spw = float((y == 0).sum() / (y == 1).sum())
+    clf = HistGradientBoostingClassifier(max_iter=300, max_depth=7, learning_rate=0.05, l2_regularization=1.0,
+                                         max_bins=255, min_samples_leaf=1, max_leaf_nodes=None,
+                                         early_stopping=False, class_weight={0: 1.0, 1: spw}, random_state=78,
+                                         verbose=1)
+    t0 = time.perf_counter()
+    clf.fit(X, y)
+    dt = time.perf_counter() - t0
+    auc = roc_auc(yte, clf.predict_proba(Xte)[:, 1])
+    return {"config": "cpu-hist-gbdt-10m", "metric": "rows/sec GBDT train, CPU reference point",
+            "value": round(rows / dt, 1), "unit": "rows/s", "fit_s": round(dt, 3), "auc": round(float(auc), 5),
+            "engine": "sklearn HistGradientBoostingClassifier", "threads": os.environ.get("OMP_NUM_THREADS"),
+            "cpus_visible": os.cpu_count(), "rows": rows}
+
+
 def _json_line(out: str) -> dict:
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
     if not lines:
@@ -86,6 +120,8 @@ def _run(cmd: list[str], timeout: int) -> dict:
 
 CONFIGS = {
     "plumbing-10k": lambda: plumbing_10k(),
+    "cpu-hist-gbdt-10m": lambda: cpu_hist_gbdt(),
+    "pipeline-100k": lambda: {"config": "pipeline-100k", **_run(["scripts/bench_pipeline.py"], 1100)},
     "gbdt-1m": lambda: {"config": "gbdt-1m", **_run(["bench.py", "--rows", "1000000", "--steps", "3"], 600)},
     "gbdt-10m": lambda: {"config": "gbdt-10m", **_run(["bench.py", "--steps", "3"], 600)},
     "ooc-100m": lambda: {"config": "ooc-100m",
