@@ -144,6 +144,10 @@ class GpuGbdtTrainer:
             if not t.is_cuda or not t.is_contiguous():
                 raise ValueError("trainer inputs must be contiguous CUDA tensors")
         self._keep = ts
+        # cobalt_gbdt_set_data reads the bin counts with a blocking hipMemcpy, which is not ordered
+        # after work on a non-default stream (e.g. the int32 conversion of ``nbins`` on a search
+        # worker's stream): finish the caller's stream first
+        torch.cuda.current_stream(bins.device).synchronize()
         rc = self.lib.cobalt_gbdt_set_data(self.h, *[t.data_ptr() for t in ts])
         _native.check(rc, "cobalt_gbdt_set_data")
 

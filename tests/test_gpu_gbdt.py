@@ -257,3 +257,19 @@ def test_gpu_fused_partition_histogram_pass(world, monkeypatch):
                           row_offset=s).save_raw("ubj")
 
     assert all(o == ref for o in loopback.run_ranks(world, rank_fit))
+
+
+def test_concurrent_search_fits_equal_sequential():
+    """randomized_search's (fold, candidate) fits on 4 HIP streams score exactly like one stream."""
+    from cobalt_smart_lender_ai_amd.select import search
+    from cobalt_smart_lender_ai_amd.select.split import stratified_kfold_indices
+
+    X, y = _data(20_000, seed=23)
+    X, y = X.numpy(), y.numpy()
+    cands = search.sample_candidates({"max_depth": [3, 5], "learning_rate": [0.1, 0.3], "subsample": [0.8, 1.0]},
+                                     6, 22)
+    folds = stratified_kfold_indices(y, 3)
+    base = dict(n_estimators=20, scale_pos_weight=3.0, random_state=78)
+    one = search._fold_scores(X, y, folds, base, cands, "cuda", streams=1)
+    four = search._fold_scores(X, y, folds, base, cands, "cuda", streams=4)
+    assert np.array_equal(one, four)
