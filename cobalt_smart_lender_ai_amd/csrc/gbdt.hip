@@ -57,6 +57,13 @@ struct Cand {
   int64_t gl, hl;
 };
 
+struct CandRec {  // a group's best split candidate (k_eval<true> -> k_eval_finish)
+  double gain;
+  int32_t key;
+  float cut;
+  int64_t gl, hl;
+};
+
 __device__ __forceinline__ bool cand_better(const Cand& a, const Cand& b) {
   return a.gain > b.gain || (a.gain == b.gain && a.key < b.key);
 }
@@ -122,6 +129,7 @@ struct GbdtDev {
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
   int32_t by_hess;        // timing experiment (COBALT_BUILD_BY_HESS): unfused path builds k_eval's hessian choice
+  CandRec* cand;          // [2^(max_depth-1)][64] per-group split candidates (grouped evaluation)
   int64_t n;
   int64_t ldt;            // row pitch of binsT (= the rows the context was created for; n <= ldt)
   int64_t row_offset;
@@ -595,20 +603,31 @@ __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes
   }
 }
 
-// Per-item partial histogram -> compact slab (+ the item's (G, H) totals when tot_block).
+// Per-item partial histogram -> compact slab (+ the item's (G, H) totals when tot_block). The tile's
+// compact cell offsets and copy shifts are staged in LDS once, and each cell finds its feature by a
+// binary search there (a linear scan over global hoff per cell cost ~60 us per launch on the
+// 106-feature RFE fits, where every block flushes 4 x 8k cells).
+constexpr int kMaxFeatTile = 64;
+
 __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistLanes& hl, int item, int f0, int ft,
                            int64_t tg, int64_t th, bool tot_block, int64_t (*s_tot)[16]) {
-  const int2* __restrict__ lay = d.layout + f0;
-  const int c0 = d.hoff[f0], c1 = d.hoff[f0 + ft];
+  __shared__ int s_fo[kMaxFeatTile + 1];  // compact cell offset of each tile feature (+ the end)
+  __shared__ int s_fs[kMaxFeatTile];      // its log2(copies), or -1 when masked out for this tree
+  if (threadIdx.x <= ft) s_fo[threadIdx.x] = d.hoff[f0 + threadIdx.x];
+  if (threadIdx.x < ft) s_fs[threadIdx.x] = ((hl.fbits >> threadIdx.x) & 1ull) ? d.layout[f0 + threadIdx.x].y : -1;
+  __syncthreads();
+  const int c0 = s_fo[0], c1 = s_fo[ft];
   uint64_t* slab = d.slab + (int64_t)item * d.ncells;
   for (int e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
-    int fl = 0;
-    while (fl + 1 < ft && d.hoff[f0 + fl + 1] <= e) ++fl;
-    const int b = e - d.hoff[f0 + fl];
+    int lo = 0, hi = ft - 1;  // largest fl with s_fo[fl] <= e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_fo[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const int sh = s_fs[lo];
     uint64_t v = 0;
-    if ((hl.fbits >> fl) & 1ull) {
-      const int sh = lay[fl].y;
-      const uint64_t* cell = s_hist + fl * kMaxBins + (b << sh);
+    if (sh >= 0) {
+      const uint64_t* cell = s_hist + lo * kMaxBins + ((e - s_fo[lo]) << sh);
       for (int c = 0; c < (1 << sh); ++c) v += cell[c];
     }
     slab[e] = v;
@@ -982,8 +1001,67 @@ struct EvalFeat {
   float cut[4], cutm1;  // cut of bins lane*4+k, and of bin lane*4-1 (missing-left splits at b-1)
 };
 
-__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree) {
+// Node decision from its best candidate (split or leaf; children of the last split level become leaves).
+__device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int64_t H, Cand best, float best_cut) {
+  Node* nodes = d.nodes;
+  const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
+  const float loss = (float)best.gain;
+  const bool ok = best.key != 0x7fffffff && loss > 1e-6f && loss >= (float)d.gamma;
+  const double wgt = calc_weight(Gd, Hd, d.lambda_, d.alpha, d.mcw);
+  Node& nd = nodes[n];
+  if (level == 0) { nd.G = G; nd.H = H; }
+  nd.sum_hess = (float)Hd;
+  nd.base_weight = (float)(wgt * d.eta);
+  if (ok) {
+    const int f = best.key >> 10;
+    const int r = best.key & 1023;
+    const int nb = d.nbins[f];
+    int j, dl;
+    if (r < 512) { j = r; dl = 0; } else { j = (nb - 1 - (r - 512)) - 1; dl = 1; }
+    nd.status = kSplit;
+    nd.feat = f;
+    nd.bin = j;
+    nd.default_left = dl;
+    nd.split_cond = j >= 0 ? best_cut : -FLT_MAX;
+    nd.loss_chg = loss;
+    Node& L = nodes[2 * n + 1];
+    Node& R = nodes[2 * n + 2];
+    L.status = kActive; L.G = best.gl; L.H = best.hl;
+    R.status = kActive; R.G = G - best.gl; R.H = H - best.hl;
+    // Child histogrammed from rows by the fused partition pass (k_part_hist): the one with the
+    // smaller GLOBAL hessian (known here, before the partition; identical on every rank, and the
+    // host oracle's choice). The unfused path overrides this with row counts in publish_level.
+    const int lb = best.hl <= H - best.hl ? 1 : 0;
+    L.build = lb;
+    R.build = 1 - lb;
+    if (level + 1 == d.max_depth) {  // children are at max depth: finalise them as leaves here
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        Node& ch = c == 0 ? L : R;
+        const double cg = (double)ch.G * d.ginv, chh = (double)ch.H * d.hinv;
+        const double cw = calc_weight(cg, chh, d.lambda_, d.alpha, d.mcw);
+        ch.sum_hess = (float)chh;
+        ch.base_weight = (float)(cw * d.eta);
+        ch.status = kLeaf;
+        ch.leaf_value = (float)(cw * d.eta);
+        ch.split_cond = ch.leaf_value;
+      }
+    }
+  } else {
+    nd.status = kLeaf;
+    nd.leaf_value = (float)(wgt * d.eta);
+    nd.split_cond = nd.leaf_value;
+  }
+}
+
+// kGroups: the node's features are split over gridDim.y blocks of `fg` features each (one CU per
+// group instead of one per node: the fp64 gain scan of a wide node -- 106 features in the RFE stage --
+// is issue-bound on a single CU); each group writes its best candidate and k_eval_finish reduces them.
+template <bool kGroups>
+__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg) {
   const int pos = blockIdx.x;
+  const int fbeg = kGroups ? blockIdx.y * fg : 0;
+  const int fend = kGroups ? min(d.F, fbeg + fg) : d.F;
   const int n = (1 << level) - 1 + pos;
   Node* nodes = d.nodes;
   const int pair = level == 0 ? 0 : (pos >> 1);
@@ -1003,7 +1081,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       EvalFeat& e = ef[s];
       e.f = fbase + s * nw;
       const int fc = min(e.f, d.F - 1);
-      const bool valid = e.f < d.F;
+      const bool valid = e.f < fend;
       e.on = valid && fm[fc] != 0;
       e.nb = valid ? d.nbins[fc] : 0;
       fbase_off[s] = ((int64_t)d.hoff[fc] + lane * 4) * 2;
@@ -1012,7 +1090,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       e.cutm1 = d.cuts[fc * kMaxBins + max(lane * 4 - 1, 0)];
     }
   };
-  load_meta(wave_id());
+  load_meta(fbeg + wave_id());
   // round trip 1 (uniform scalar loads)
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
@@ -1040,8 +1118,8 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   best.gl = 0;
   best.hl = 0;
   float best_cut = -FLT_MAX;
-  for (int fbase = wave_id(); fbase < d.F; fbase += 2 * nw) {  // one pass for F <= 32
-  if (fbase != wave_id()) load_meta(fbase);
+  for (int fbase = fbeg + wave_id(); fbase < fend; fbase += 2 * nw) {  // one pass for F <= 32
+  if (fbase != fbeg + wave_id()) load_meta(fbase);
   // round trip 2: the histogram bins (and the parent's, for the subtraction)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1127,53 +1205,51 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   if (threadIdx.x != 0) return;
   for (int k = 1; k < nw; ++k)
     if (cand_better(s_best[k], best)) { best = s_best[k]; best_cut = s_cut[k]; }
-  const float loss = (float)best.gain;
-  const bool ok = best.key != 0x7fffffff && loss > 1e-6f && loss >= (float)d.gamma;
-  const double wgt = calc_weight(Gd, Hd, d.lambda_, d.alpha, d.mcw);
-  Node& nd = nodes[n];
-  if (level == 0) { nd.G = G; nd.H = H; }
-  nd.sum_hess = (float)Hd;
-  nd.base_weight = (float)(wgt * d.eta);
-  if (ok) {
-    const int f = best.key >> 10;
-    const int r = best.key & 1023;
-    const int nb = d.nbins[f];
-    int j, dl;
-    if (r < 512) { j = r; dl = 0; } else { j = (nb - 1 - (r - 512)) - 1; dl = 1; }
-    nd.status = kSplit;
-    nd.feat = f;
-    nd.bin = j;
-    nd.default_left = dl;
-    nd.split_cond = j >= 0 ? best_cut : -FLT_MAX;
-    nd.loss_chg = loss;
-    Node& L = nodes[2 * n + 1];
-    Node& R = nodes[2 * n + 2];
-    L.status = kActive; L.G = best.gl; L.H = best.hl;
-    R.status = kActive; R.G = G - best.gl; R.H = H - best.hl;
-    // Child histogrammed from rows by the fused partition pass (k_part_hist): the one with the
-    // smaller GLOBAL hessian (known here, before the partition; identical on every rank, and the
-    // host oracle's choice). The unfused path overrides this with row counts in publish_level.
-    const int lb = best.hl <= H - best.hl ? 1 : 0;
-    L.build = lb;
-    R.build = 1 - lb;
-    if (level + 1 == d.max_depth) {  // children are at max depth: finalise them as leaves here
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        Node& ch = c == 0 ? L : R;
-        const double cg = (double)ch.G * d.ginv, chh = (double)ch.H * d.hinv;
-        const double cw = calc_weight(cg, chh, d.lambda_, d.alpha, d.mcw);
-        ch.sum_hess = (float)chh;
-        ch.base_weight = (float)(cw * d.eta);
-        ch.status = kLeaf;
-        ch.leaf_value = (float)(cw * d.eta);
-        ch.split_cond = ch.leaf_value;
-      }
-    }
-  } else {
-    nd.status = kLeaf;
-    nd.leaf_value = (float)(wgt * d.eta);
-    nd.split_cond = nd.leaf_value;
+  if (kGroups) {
+    CandRec& o = d.cand[(int64_t)pos * gridDim.y + blockIdx.y];
+    o.gain = best.gain;
+    o.key = best.key;
+    o.cut = best_cut;
+    o.gl = best.gl;
+    o.hl = best.hl;
+    return;
   }
+  eval_finalize(d, level, n, G, H, best, best_cut);
+}
+
+// Reduce the per-group candidates of each node of the level (one wave per node, lane = group).
+__global__ __launch_bounds__(64) void k_eval_finish(GbdtDev d, int level, int parity, int ngroups) {
+  const int pos = blockIdx.x;
+  const int n = (1 << level) - 1 + pos;
+  const Node& nd = d.nodes[n];
+  if (nd.status != kActive) return;
+  int64_t G = nd.G, H = nd.H;
+  if (level == 0) {
+    G = d.hist_b[parity][(int64_t)d.ncells * 2];
+    H = d.hist_b[parity][(int64_t)d.ncells * 2 + 1];
+  }
+  const int lane = lane_id();
+  Cand best;
+  best.gain = -INFINITY;
+  best.key = 0x7fffffff;
+  best.gl = 0;
+  best.hl = 0;
+  float best_cut = -FLT_MAX;
+  if (lane < ngroups) {
+    const CandRec& c = d.cand[(int64_t)pos * ngroups + lane];
+    best.gain = c.gain;
+    best.key = c.key;
+    best.gl = c.gl;
+    best.hl = c.hl;
+    best_cut = c.cut;
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    Cand other = cand_shfl_xor(best, o);
+    const float ocut = __shfl_xor(best_cut, o, kWave);
+    if (cand_better(other, best)) { best = other; best_cut = ocut; }
+  }
+  if (lane == 0) eval_finalize(d, level, n, G, H, best, best_cut);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1527,6 +1603,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.items_h, c->items_cap * sizeof(WorkItem)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.counters, 16 * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.cand, (size_t)c->pairs_max * 64 * sizeof(CandRec)))) return rc;
   if (cfg->comm) {  // local histograms of every node of a level (positions 0 .. 2^(max_depth-1))
     for (int k = 0; k < 2; ++k)
       if ((rc = dev_alloc(c, (void**)&d.hist_loc[k], 2 * hist_bytes))) return rc;
@@ -1610,6 +1687,11 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const bool fuse_root = !sampled && d.stride == 32 && d.F <= 24 && ftiles == 1 && d.ablate == 0 &&
                          getenv("COBALT_NO_FUSED_ROOT") == nullptr;
+  // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
+  // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
+  static const int env_fg = getenv("COBALT_EVAL_FG") ? atoi(getenv("COBALT_EVAL_FG")) : -1;
+  int eval_fg = env_fg >= 0 ? env_fg : (d.F > 32 ? 8 : 0);
+  if (eval_fg > 0) eval_fg = std::min(32, std::max(eval_fg, ceil_div(d.F, 64)));
   // rows in flight per thread in the gradient + root histogram pass (COBALT_GRAD_U=4: +1%, within noise)
   static const int grad_u = getenv("COBALT_GRAD_U") ? atoi(getenv("COBALT_GRAD_U")) : 2;
   // partition fused with the next level's histogram (same record-layout conditions); opt-in while it
@@ -1673,7 +1755,14 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
         if (rc) return rc;
       }
-      hipLaunchKernelGGL(k_eval, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t);
+      if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
+        const int ng = ceil_div(d.F, eval_fg);
+        hipLaunchKernelGGL(k_eval<true>, dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d, level,
+                           parity, t, eval_fg);
+        hipLaunchKernelGGL(k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
+      } else {
+        hipLaunchKernelGGL(k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
+      }
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
