@@ -126,7 +126,8 @@ struct GbdtDev {
   int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
-  int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush
+  int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
+                          // 4 plan only (k_hist); 11-13 partition (see k_partition)
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
   int32_t by_hess;        // timing experiment (COBALT_BUILD_BY_HESS): unfused path builds k_eval's hessian choice
   CandRec* cand;          // [2^(max_depth-1)][64] per-group split candidates (grouped evaluation)
@@ -567,18 +568,24 @@ struct HistLanes {
   uint32_t lane;
 };
 
+// Per-tile feature state for the LDS histogram lanes. Lane k loads feature f0 + k's colsample bit and
+// copy shift (one round trip, instead of 2 x ft dependent scalar loads per thread -- ~10 us per block
+// for a 32-feature tile), and ballots spread them to every lane. Called by every thread of a block.
 __device__ __forceinline__ HistLanes hist_lanes(const GbdtDev& d, int tree, int f0, int ft) {
   HistLanes hl;
-  const int2* __restrict__ lay = d.layout + f0;
-  const uint8_t* fm = d.fmask + (int64_t)tree * d.F + f0;
-  hl.fbits = 0;
-  for (int k = 0; k < ft; ++k) hl.fbits |= (uint64_t)(fm[k] != 0) << k;
+  hl.lane = lane_id();
+  const bool in = (int)hl.lane < ft;
+  const int f = f0 + (in ? (int)hl.lane : 0);
+  const bool on = in && d.fmask[(int64_t)tree * d.F + f] != 0;
+  const int sh = in ? (d.layout[f].y & 7) : 0;
+  hl.fbits = __ballot(on);
+  const uint64_t b0 = __ballot(in && (sh & 1)), b1 = __ballot(in && (sh & 2)), b2 = __ballot(in && (sh & 4));
   hl.sh0 = hl.sh1 = hl.sh2 = hl.sh3 = 0;
   for (int fl = 0; fl < ft; ++fl) {
-    const uint32_t v = (uint32_t)(lay[fl].y & 7) << (3 * (fl & 7));
+    const uint32_t v = (uint32_t)(((b0 >> fl) & 1ull) | (((b1 >> fl) & 1ull) << 1) | (((b2 >> fl) & 1ull) << 2))
+                       << (3 * (fl & 7));
     switch (fl >> 3) { case 0: hl.sh0 |= v; break; case 1: hl.sh1 |= v; break; case 2: hl.sh2 |= v; break; default: hl.sh3 |= v; }
   }
-  hl.lane = lane_id();
   hl.trash = (uint32_t)(ft * kMaxBins) + hl.lane;
   return hl;
 }
@@ -769,6 +776,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   if (blockIdx.y == 0 && threadIdx.x == 0) d.items_h[item] = w;
   const int f0 = blockIdx.y * d.feat_tile;
   if (f0 >= d.F) return;
+  if (d.ablate == 4) return;  // timing-only: plan + publish only
   const int ft = min(d.feat_tile, d.F - f0);
   const int entries = d.tile_entries[blockIdx.y] + kWave;  // + per-lane trash cells
   const HistLanes hl = hist_lanes(d, tree, f0, ft);
@@ -780,6 +788,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
 
   const int32_t* rix = d.ridx[parity];
   const bool identity = parity == 0 && w.node == 0;  // root level: ridx is the identity
+  if (d.ablate == 3) w.end = w.begin;  // timing-only: no rows
   const int lane = lane_id();
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
@@ -868,6 +877,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   __syncthreads();
   // Per-item partial histogram -> slab (plain coalesced stores; the packed u64 of the K copies can
   // be summed directly because the per-item sums obey the same < 2^31 / < 2^32 bounds).
+  if (d.ablate == 2) return;  // timing-only: no flush
   hist_flush(d, s_hist, hl, item, f0, ft, tg, th, blockIdx.y == 0, s_tot);
 }
 
