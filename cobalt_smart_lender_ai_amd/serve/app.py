@@ -12,6 +12,8 @@ Routes (identical paths, request schemas, response keys and error codes):
 * ``POST /feature_importance_bulk`` -- ``{"data": [...]}`` -> top-10 average-gain features; empty
   -> 400 ``"No data provided."``.
 * ``GET /health``                   -- additive: model / device / batcher statistics.
+* ``GET /metrics``                  -- additive: Prometheus exposition (request counts and latency
+  histograms per route, micro-batch sizes, model info), one registry per app.
 
 Model loading mirrors the reference lifespan (load at startup, fail fast with ``RuntimeError``) but
 reads the checkpoint with the static, non-executing pickle decoder and takes the path from
@@ -22,6 +24,7 @@ from __future__ import annotations
 import asyncio
 import io
 import os
+import time
 import re
 from contextlib import asynccontextmanager
 from pathlib import Path
@@ -30,6 +33,7 @@ from typing import Dict, List
 import numpy as np
 import pandas as pd
 from fastapi import FastAPI, HTTPException, Request
+from fastapi.responses import Response
 from pydantic import BaseModel, ConfigDict, Field
 
 from ..config import ServeConfig, from_env
@@ -109,9 +113,27 @@ def load_model(cfg: ServeConfig) -> Booster:
     return Booster.load_raw(data)
 
 
+class _Metrics:
+    """Prometheus instruments of one app (own registry, so several apps can live in one process)."""
+
+    def __init__(self):
+        from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram
+
+        self.registry = CollectorRegistry()
+        buckets = (1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2, 2.5e-2, 5e-2, 0.1, 0.25, 0.5, 1.0, 2.5)
+        self.requests = Counter("cobalt_requests_total", "HTTP requests", ["route", "status"], registry=self.registry)
+        self.latency = Histogram("cobalt_request_seconds", "HTTP request latency", ["route"], buckets=buckets,
+                                 registry=self.registry)
+        self.batch_rows = Histogram("cobalt_microbatch_rows", "rows per micro-batch of /predict",
+                                    buckets=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512), registry=self.registry)
+        self.rows = Counter("cobalt_scored_rows_total", "rows scored", ["route"], registry=self.registry)
+        self.model = Gauge("cobalt_model_info", "loaded model", ["trees", "features", "device"], registry=self.registry)
+
+
 def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -> FastAPI:
     cfg = cfg or from_env(ServeConfig)
     state: dict = {}
+    metrics = _Metrics()
 
     @asynccontextmanager
     async def lifespan(app: FastAPI):
@@ -122,6 +144,8 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
             await batcher.start()
             state.update(booster=bst, engine=engine, batcher=batcher,
                          features=list(bst.feature_names or [f"f{i}" for i in range(bst.num_feature)]))
+            batcher.on_batch = lambda n: metrics.batch_rows.observe(n)
+            metrics.model.labels(str(bst.num_trees), str(bst.num_feature), str(engine.device)).set(1)
             print(f"[INFO] Model and SHAP engine ready on {engine.device} ({bst.num_trees} trees).")
         except Exception as e:  # noqa: BLE001
             print(f"[ERROR] Model load failed: {e}")
@@ -131,6 +155,21 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
 
     app = FastAPI(title="Cobalt XGBoost Inference API", lifespan=lifespan)
     app.state.cobalt = state
+    app.state.metrics = metrics
+
+    @app.middleware("http")
+    async def observe(request: Request, call_next):
+        route = request.url.path
+        t0 = time.perf_counter()
+        status = 500
+        try:
+            response = await call_next(request)
+            status = response.status_code
+            return response
+        finally:
+            if route != "/metrics":
+                metrics.latency.labels(route).observe(time.perf_counter() - t0)
+                metrics.requests.labels(route, str(status)).inc()
 
     @app.post("/predict")
     async def predict_single(input_data: SingleInput):
@@ -138,6 +177,7 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
         feats = state["features"]
         x = np.array([float(row[f]) for f in feats], dtype=np.float32)
         prob, phi = await state["batcher"].submit(x)
+        metrics.rows.labels("/predict").inc()
         return {
             "prob_default": float(prob),
             "shap_values": [float(v) for v in phi],
@@ -162,6 +202,7 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
             # (SURVEY App. B.8), which stalls every concurrent /predict request behind a bulk file
             loop = asyncio.get_running_loop()
             df["prob_default"] = await loop.run_in_executor(None, state["engine"].predict_proba, X)
+            metrics.rows.labels("/predict_bulk_csv").inc(len(df))
             df_clean = df.replace([np.inf, -np.inf], np.nan).astype(object).where(
                 df.replace([np.inf, -np.inf], np.nan).notna(), "null")
             return {"predictions": df_clean.to_dict(orient="records")}
@@ -179,6 +220,12 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
             return {"top_features": [{"feature": k, "importance": v} for k, v in top]}
         except Exception as e:  # noqa: BLE001
             raise HTTPException(status_code=500, detail=f"Feature importance computation failed: {e}")
+
+    @app.get("/metrics")
+    def prometheus_metrics():
+        from prometheus_client import CONTENT_TYPE_LATEST, generate_latest
+
+        return Response(generate_latest(metrics.registry), media_type=CONTENT_TYPE_LATEST)
 
     @app.get("/health")
     def health():

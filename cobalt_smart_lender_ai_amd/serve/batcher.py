@@ -33,6 +33,7 @@ class MicroBatcher:
         self._queue: asyncio.Queue | None = None
         self._task: asyncio.Task | None = None
         self.stats = BatcherStats()
+        self.on_batch = None  # optional callback(rows) per scored batch (serving metrics)
 
     async def start(self) -> None:
         if self._task is None:
@@ -83,6 +84,8 @@ class MicroBatcher:
             self.stats.rows += len(items)
             self.stats.max_batch_seen = max(self.stats.max_batch_seen, len(items))
             self.stats.hist[len(items)] = self.stats.hist.get(len(items), 0) + 1
+            if self.on_batch is not None:
+                self.on_batch(len(items))
             for i, (_, f) in enumerate(items):
                 if not f.done():
                     f.set_result((float(probs[i]), phis[i]))

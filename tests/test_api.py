@@ -111,3 +111,16 @@ def test_tree_explainer_api(reference_booster):
     assert abs(fd["output"] - (-2.2636339)) < 1e-5
     bar_plot(e)
     summary_plot(e)
+
+
+def test_prometheus_metrics(client):
+    """Additive /metrics endpoint: per-route request counts and latency histograms, micro-batch sizes."""
+    assert client.post("/predict", json=UI_DEFAULT).status_code == 200
+    client.post("/predict", json={"loan_amnt": 1.0})  # 422
+    text = client.get("/metrics").text
+    assert 'cobalt_requests_total{route="/predict",status="200"}' in text
+    assert 'cobalt_requests_total{route="/predict",status="422"}' in text
+    assert 'cobalt_request_seconds_bucket{le="0.0001",route="/predict"}' in text
+    assert "cobalt_microbatch_rows_count" in text and "cobalt_model_info{" in text
+    rows = [ln for ln in text.splitlines() if ln.startswith('cobalt_scored_rows_total{route="/predict"}')]
+    assert rows and float(rows[0].split()[-1]) >= 1
