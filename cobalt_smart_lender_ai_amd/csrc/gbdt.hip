@@ -129,7 +129,7 @@ struct GbdtDev {
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
                           // 4 plan only (k_hist); 11-13 partition (see k_partition)
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
-  int32_t by_hess;        // timing experiment (COBALT_BUILD_BY_HESS): unfused path builds k_eval's hessian choice
+  int32_t by_hess;        // build k_eval's (global) hessian choice: DP default, COBALT_BUILD_BY_HESS on one GPU
   CandRec* cand;          // [2^(max_depth-1)][64] per-group split candidates (grouped evaluation)
   int64_t n;
   int64_t ldt;            // row pitch of binsT (= the rows the context was created for; n <= ldt)
@@ -1595,7 +1595,11 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.hinv = 1.0 / cfg->hscale;
   d.seed = cfg->seed;
   d.ablate = getenv("COBALT_HIST_ABLATE") ? atoi(getenv("COBALT_HIST_ABLATE")) : 0;
-  d.by_hess = (getenv("COBALT_BUILD_BY_HESS") && !cfg->comm) ? 1 : 0;
+  // Data parallel: every rank histograms the child with the smaller GLOBAL hessian (k_eval's choice,
+  // identical on all ranks), so the level's all-reduce sums the same child everywhere and no
+  // per-level local-left conversion (k_dp_local) is needed. On one GPU the locally smaller row
+  // count is the default (+2% histogram time otherwise); COBALT_BUILD_BY_HESS forces the hessian rule.
+  d.by_hess = (getenv("COBALT_BUILD_BY_HESS") || cfg->comm) ? 1 : 0;
   c->lds_hist = (size_t)cfg->feat_tile * kMaxBins * sizeof(uint64_t);
   int rc = 0;
   const size_t hist_bytes = (size_t)c->pairs_max * d.slot_elems * sizeof(int64_t);
@@ -1755,9 +1759,10 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
                          dim3(256), 0, stream, d, parity, fuse_part ? level : 0);
       CK_LAUNCH();
       if (dp) {
-        // unfused: ranks built their locally smaller child -> turn it into the local LEFT child;
-        // fused: every rank built the globally chosen child, all-reduced as is
-        if (!fuse_part) {
+        // row-count choice: ranks built their locally smaller child -> turn it into the local LEFT
+        // child; hessian choice (the DP default) / fused pass: every rank built the globally chosen
+        // child, all-reduced as is
+        if (!fuse_part && !d.by_hess) {
           hipLaunchKernelGGL(k_dp_local, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d,
                              level, parity);
           CK_LAUNCH();
