@@ -33,7 +33,7 @@ from typing import Dict, List
 import numpy as np
 import pandas as pd
 from fastapi import FastAPI, HTTPException, Request
-from fastapi.responses import Response
+from fastapi.responses import JSONResponse, Response
 from pydantic import BaseModel, ConfigDict, Field
 
 from ..config import ServeConfig, from_env
@@ -178,13 +178,14 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
         x = np.array([float(row[f]) for f in feats], dtype=np.float32)
         prob, phi = await state["batcher"].submit(x)
         metrics.rows.labels("/predict").inc()
-        return {
+        # a pre-built JSONResponse skips FastAPI's generic jsonable_encoder walk (same JSON body)
+        return JSONResponse({
             "prob_default": float(prob),
-            "shap_values": [float(v) for v in phi],
+            "shap_values": phi.tolist(),
             "base_value": float(state["engine"].expected_value),
             "features": feats,
             "input_row": {f: float(row[f]) for f in feats},
-        }
+        })
 
     @app.post("/predict_bulk_csv")
     async def predict_bulk_csv(request: Request):

@@ -61,15 +61,14 @@ class MicroBatcher:
         while True:
             first = await self._queue.get()
             items = [first]
-            deadline = time.perf_counter() + self.max_wait
-            while len(items) < self.max_batch:
-                timeout = deadline - time.perf_counter()
-                if timeout <= 0:
-                    break
-                try:
-                    items.append(await asyncio.wait_for(self._queue.get(), timeout))
-                except asyncio.TimeoutError:
-                    break
+            # drain what is already queued; if that is not a full batch, give concurrent requests one
+            # short window (a single sleep -- not a wait_for per item, which cost more than it saved)
+            while len(items) < self.max_batch and not self._queue.empty():
+                items.append(self._queue.get_nowait())
+            if len(items) < self.max_batch and self.max_wait > 0:
+                await asyncio.sleep(self.max_wait)
+                while len(items) < self.max_batch and not self._queue.empty():
+                    items.append(self._queue.get_nowait())
             X = np.stack([r for r, _ in items])
             t0 = time.perf_counter()
             try:
