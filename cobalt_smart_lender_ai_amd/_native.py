@@ -106,9 +106,10 @@ def load(build_if_needed: bool = True) -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        path = _build.lib_path()
+        override = os.environ.get("COBALT_NATIVE_LIB")  # e.g. the host-sanitizer build (build --sanitize)
+        path = Path(override) if override else _build.lib_path()
         try:
-            if build_if_needed and _build.is_stale() and Path(_build.HIPCC).exists():
+            if not override and build_if_needed and _build.is_stale() and Path(_build.HIPCC).exists():
                 _build.build()
             if not path.exists():
                 raise NativeUnavailable(f"{path} missing; run `python -m cobalt_smart_lender_ai_amd.build`")
