@@ -83,12 +83,36 @@ def cmd_train_nn(args) -> int:
 
 
 def cmd_serve(args) -> int:
+    import os
+    import subprocess
+    import sys
+    import tempfile
+
     import uvicorn
 
-    # N worker processes (each with its own event loop, micro-batcher and hipGraph buckets on the
-    # GPU): one Python event loop tops out near ~1k requests/s on HTTP parsing and validation
-    uvicorn.run("cobalt_smart_lender_ai_amd.serve.app:create_app", factory=True, host=args.host, port=args.port,
-                workers=args.workers)
+    # One Python event loop tops out near ~1.7k requests/s on HTTP parsing and validation. With
+    # --workers N > 1 the N uvicorn workers stay CPU-only and forward rows to ONE scorer process that
+    # owns the GPU (serve/scorer.py): one engine, one set of hipGraphs, and micro-batches that pool the
+    # requests of every worker.
+    scorer = None
+    if args.workers > 1 and not os.environ.get("COBALT_SCORER_SOCKET"):
+        sock = os.path.join(tempfile.mkdtemp(prefix="cobalt_scorer_"), "scorer.sock")
+        cmd = [sys.executable, "-m", "cobalt_smart_lender_ai_amd.serve.scorer", "--socket", sock]
+        if args.device:
+            cmd += ["--device", args.device]
+        scorer = subprocess.Popen(cmd)
+        os.environ["COBALT_SCORER_SOCKET"] = sock  # inherited by the spawned workers
+    try:
+        if args.workers > 1:
+            from .serve.workers import run_workers  # SO_REUSEPORT workers (see there: TCP_NODELAY)
+
+            return run_workers(args.host, args.port, args.workers, args.log_level)
+        uvicorn.run("cobalt_smart_lender_ai_amd.serve.app:create_app", factory=True, host=args.host,
+                    port=args.port, log_level=args.log_level)
+    finally:
+        if scorer is not None:
+            scorer.terminate()
+            scorer.wait(timeout=30)
     return 0
 
 
@@ -135,6 +159,7 @@ def main(argv: list[str] | None = None) -> int:
     s.add_argument("--host", default="0.0.0.0")
     s.add_argument("--port", type=int, default=8000)
     s.add_argument("--workers", type=int, default=int(__import__("os").environ.get("COBALT_SERVE_WORKERS", "1")))
+    s.add_argument("--log-level", default="info")
     s.set_defaults(fn=cmd_serve)
     s = sub.add_parser("dictionary", help="column descriptions (default: the 20 deployed model features)")
     s.add_argument("--xlsx", required=True, help="path to LCDataDictionary.xlsx")

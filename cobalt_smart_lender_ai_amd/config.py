@@ -92,6 +92,7 @@ class ServeConfig:
     max_wait_ms: float = 1.0
     device: str | None = None
     use_graphs: bool = True
+    scorer_socket: str | None = None            # set: score through serve/scorer.py (multi-worker)
 
 
 def _coerce(v: str, typ: Any):

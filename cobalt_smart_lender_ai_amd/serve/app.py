@@ -15,6 +15,10 @@ Routes (identical paths, request schemas, response keys and error codes):
 * ``GET /metrics``                  -- additive: Prometheus exposition (request counts and latency
   histograms per route, micro-batch sizes, model info), one registry per app.
 
+With ``COBALT_SCORER_SOCKET`` set the app holds no GPU state: it parses and validates HTTP on the CPU
+and forwards rows to the one scorer process (serve/scorer.py) that owns the device, so several
+uvicorn workers share one engine and one micro-batcher instead of time-slicing the GPU.
+
 Model loading mirrors the reference lifespan (load at startup, fail fast with ``RuntimeError``) but
 reads the checkpoint with the static, non-executing pickle decoder and takes the path from
 ``COBALT_MODEL_PATH`` (or S3 via ``COBALT_SOURCE=s3`` when boto3 is available).
@@ -139,14 +143,24 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
     async def lifespan(app: FastAPI):
         try:
             bst = booster if booster is not None else load_model(cfg)
-            engine = ScoringEngine(bst, device=cfg.device, use_graphs=cfg.use_graphs)
-            batcher = MicroBatcher(engine, max_batch=cfg.max_batch, max_wait_ms=cfg.max_wait_ms)
-            await batcher.start()
-            state.update(booster=bst, engine=engine, batcher=batcher,
+            state.update(booster=bst, expected_value=float(bst.expected_value()),
                          features=list(bst.feature_names or [f"f{i}" for i in range(bst.num_feature)]))
-            batcher.on_batch = lambda n: metrics.batch_rows.observe(n)
-            metrics.model.labels(str(bst.num_trees), str(bst.num_feature), str(engine.device)).set(1)
-            print(f"[INFO] Model and SHAP engine ready on {engine.device} ({bst.num_trees} trees).")
+            if cfg.scorer_socket:
+                from .scorer import RemoteScorer
+
+                remote = RemoteScorer(cfg.scorer_socket, bst.num_feature)
+                await remote.start()
+                state.update(engine=None, batcher=remote, remote=remote)
+                where = f"scorer {cfg.scorer_socket}"
+            else:
+                engine = ScoringEngine(bst, device=cfg.device, use_graphs=cfg.use_graphs)
+                batcher = MicroBatcher(engine, max_batch=cfg.max_batch, max_wait_ms=cfg.max_wait_ms)
+                await batcher.start()
+                batcher.on_batch = lambda n: metrics.batch_rows.observe(n)
+                state.update(engine=engine, batcher=batcher)
+                where = str(engine.device)
+            metrics.model.labels(str(bst.num_trees), str(bst.num_feature), where).set(1)
+            print(f"[INFO] Model and SHAP engine ready on {where} ({bst.num_trees} trees).")
         except Exception as e:  # noqa: BLE001
             print(f"[ERROR] Model load failed: {e}")
             raise RuntimeError("Failed to load model.") from e
@@ -182,7 +196,7 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
         return JSONResponse({
             "prob_default": float(prob),
             "shap_values": phi.tolist(),
-            "base_value": float(state["engine"].expected_value),
+            "base_value": state["expected_value"],
             "features": feats,
             "input_row": {f: float(row[f]) for f in feats},
         })
@@ -201,8 +215,11 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
             X = df.to_numpy(dtype=np.float32, na_value=np.nan)
             # scored on a worker thread: the reference runs this blocking call on the event loop
             # (SURVEY App. B.8), which stalls every concurrent /predict request behind a bulk file
-            loop = asyncio.get_running_loop()
-            df["prob_default"] = await loop.run_in_executor(None, state["engine"].predict_proba, X)
+            if "remote" in state:
+                df["prob_default"] = (await state["remote"].score_many(X, False))[0]
+            else:
+                loop = asyncio.get_running_loop()
+                df["prob_default"] = await loop.run_in_executor(None, state["engine"].predict_proba, X)
             metrics.rows.labels("/predict_bulk_csv").inc(len(df))
             df_clean = df.replace([np.inf, -np.inf], np.nan).astype(object).where(
                 df.replace([np.inf, -np.inf], np.nan).notna(), "null")
@@ -229,7 +246,12 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
         return Response(generate_latest(metrics.registry), media_type=CONTENT_TYPE_LATEST)
 
     @app.get("/health")
-    def health():
+    async def health():
+        if "remote" in state:
+            st = await state["remote"].stats()
+            return {"status": "ok", "device": st["device"], "scorer": cfg.scorer_socket,
+                    "trees": state["booster"].num_trees, "graphs": None, "batches": st["batches"],
+                    "rows": st["rows"], "max_batch_seen": st["max_batch_seen"]}
         eng = state.get("engine")
         b = state.get("batcher")
         return {

@@ -85,14 +85,21 @@ def main() -> None:
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--mode", choices=["split", "replicated"], default="split",
+                    help="workers > 1: `serve --workers N` (one GPU scorer process, SO_REUSEPORT workers) or "
+                         "`uvicorn --workers N` with one engine per worker")
     a = ap.parse_args()
     port = _port()
     env = dict(os.environ, COBALT_MODEL_PATH=str(ROOT / "src/api/models/xgb_model_tree.pkl"),
                PYTHONPATH=str(ROOT))
-    srv = subprocess.Popen([sys.executable, "-m", "uvicorn", "cobalt_smart_lender_ai_amd.serve.app:create_app",
-                            "--factory", "--host", "127.0.0.1", "--port", str(port), "--log-level", "warning",
-                            "--workers", str(a.workers)],
-                           cwd=ROOT, env=env)
+    split = a.workers > 1 and a.mode == "split"
+    if split:  # the CLI path: one GPU scorer process + N CPU-only SO_REUSEPORT workers
+        cmd = [sys.executable, "-m", "cobalt_smart_lender_ai_amd", "serve", "--host", "127.0.0.1",
+               "--port", str(port), "--log-level", "warning", "--workers", str(a.workers)]
+    else:
+        cmd = [sys.executable, "-m", "uvicorn", "cobalt_smart_lender_ai_amd.serve.app:create_app", "--factory",
+               "--host", "127.0.0.1", "--port", str(port), "--log-level", "warning", "--workers", str(a.workers)]
+    srv = subprocess.Popen(cmd, cwd=ROOT, env=env)
     url = f"http://127.0.0.1:{port}"
     try:
         import httpx
@@ -109,22 +116,25 @@ def main() -> None:
             time.sleep(0.2)
         else:
             raise RuntimeError("server did not come up")
-        time.sleep(3.0 if a.workers > 1 else 0.0)  # let the other workers finish their capture
+        time.sleep(3.0 if a.workers > 1 and not split else 0.0)  # let the other workers finish their capture
         levels = []
         for procs, conns, n in ((1, 1, 400), (4, 4, 200), (4, 16, 100), (8, 32, 40)):
             levels.append(_run_level(port, procs, conns, n))
             print(json.dumps(levels[-1]), file=sys.stderr, flush=True)
-        metrics = httpx.get(url + "/metrics").text
-        cnt = [ln for ln in metrics.splitlines() if ln.startswith("cobalt_microbatch_rows_count")]
-        tot = [ln for ln in metrics.splitlines() if ln.startswith("cobalt_microbatch_rows_sum")]
-        batches = float(cnt[0].split()[-1]) if cnt else 0.0
-        rows = float(tot[0].split()[-1]) if tot else 0.0
         health = httpx.get(url + "/health").json()
+        if split:  # the scorer batches for every worker: its own counters
+            batches, rows = float(health["batches"]), float(health["rows"])
+        else:
+            metrics = httpx.get(url + "/metrics").text
+            cnt = [ln for ln in metrics.splitlines() if ln.startswith("cobalt_microbatch_rows_count")]
+            tot = [ln for ln in metrics.splitlines() if ln.startswith("cobalt_microbatch_rows_sum")]
+            batches = float(cnt[0].split()[-1]) if cnt else 0.0
+            rows = float(tot[0].split()[-1]) if tot else 0.0
     finally:
         srv.terminate()
-        srv.wait(timeout=30)
+        srv.wait(timeout=60)
     print(json.dumps({"metric": "POST /predict (probability + TreeSHAP) over HTTP, 1 MI355X", "levels": levels,
-                      "server_workers": a.workers,
+                      "server_workers": a.workers, "mode": "split" if split else "single/replicated",
                       "mean_rows_per_microbatch": round(rows / batches, 2) if batches else None,
                       "device": health.get("device"), "hipgraphs": health.get("graphs")}), flush=True)
 

@@ -124,3 +124,54 @@ def test_prometheus_metrics(client):
     assert "cobalt_microbatch_rows_count" in text and "cobalt_model_info{" in text
     rows = [ln for ln in text.splitlines() if ln.startswith('cobalt_scored_rows_total{route="/predict"}')]
     assert rows and float(rows[0].split()[-1]) >= 1
+
+
+def test_remote_scorer_mode(reference_booster, tmp_path):
+    """Multi-worker shape: the app holds no engine and forwards rows to one scorer process over a
+    unix socket (serve/scorer.py); same golden values, bulk path and health."""
+    import asyncio
+    import threading
+
+    import pandas as pd
+
+    from cobalt_smart_lender_ai_amd.serve.engine import ScoringEngine
+    from cobalt_smart_lender_ai_amd.serve.scorer import start_server
+
+    dev = "cuda" if __import__("torch").cuda.is_available() else "cpu"
+    sock = str(tmp_path / "scorer.sock")
+    engine = ScoringEngine(reference_booster, device=dev)
+    loop = asyncio.new_event_loop()
+    ready = threading.Event()
+    stop = loop.create_future()
+
+    async def run():
+        srv = await start_server(engine, sock)
+        ready.set()
+        await stop
+        srv._cobalt_batches.cancel()
+        srv.close()
+        await srv.wait_closed()
+
+    th = threading.Thread(target=lambda: loop.run_until_complete(run()), daemon=True)
+    th.start()
+    assert ready.wait(60)
+    try:
+        app = create_app(ServeConfig(scorer_socket=sock), booster=reference_booster)
+        with TestClient(app) as c:
+            j = c.post("/predict", json=UI_DEFAULT).json()
+            assert abs(j["prob_default"] - 0.0941799) < 2e-6
+            assert abs(j["base_value"] - (-0.0027751700)) < 1e-7
+            sv = dict(zip(j["features"], j["shap_values"]))
+            assert abs(sv["last_fico_range_high"] - (-1.93206)) < 1e-4
+            rows = pd.DataFrame([UI_DEFAULT, {**UI_DEFAULT, "open_il_12m": np.nan}])[DEPLOYED_FEATURES]
+            buf = io.StringIO()
+            rows.to_csv(buf, index=False)
+            r = c.post("/predict_bulk_csv", files={"file": ("x.csv", buf.getvalue(), "text/csv")})
+            assert r.status_code == 200, r.text
+            assert abs(r.json()["predictions"][0]["prob_default"] - 0.0941799) < 2e-6
+            h = c.get("/health").json()
+            assert h["status"] == "ok" and h["rows"] >= 3 and h["batches"] >= 2
+    finally:
+        loop.call_soon_threadsafe(stop.set_result, None)
+        th.join(30)
+        loop.close()
