@@ -13,10 +13,11 @@ print("== per-kernel totals (us per tree) ==")
 g = t.groupby("name").agg(calls=("us", "size"), total_us=("us", "sum"), avg_us=("us", "mean"))
 g["per_tree_us"] = g["total_us"] / trees
 print(g.sort_values("total_us", ascending=False).head(20).round(1).to_string())
-idx = t.index[t["name"].isin(["k_grad", "k_grad_hist"])]
+base = t["name"].str.replace("void ", "", regex=False).str.split("<").str[0]
+idx = t.index[base.isin(["k_grad", "k_grad_hist"])]
 if len(idx):
     last = t.loc[idx[-1]:]
-    stop = last.index[last["name"].isin(["k_apply_tree", "__amd_rocclr_copyBuffer"])]
+    stop = last.index[base.loc[last.index].isin(["k_apply_tree", "__amd_rocclr_copyBuffer"])]
     if len(stop):
         last = last.loc[: stop[0]]
     print("== last tree timeline ==")
