@@ -111,6 +111,11 @@ def _json_line(out: str) -> dict:
     return json.loads(lines[-1])
 
 
+def _named(name: str, res: dict) -> dict:
+    """bench.py's own "config" object moves to "bench_config"; "config" names the BASELINE entry."""
+    return {"config": name, **{k: v for k, v in res.items() if k != "config"}, "bench_config": res.get("config")}
+
+
 def _run(cmd: list[str], timeout: int) -> dict:
     p = subprocess.run([sys.executable, *cmd], cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     if p.returncode != 0:
@@ -122,8 +127,8 @@ CONFIGS = {
     "plumbing-10k": lambda: plumbing_10k(),
     "cpu-hist-gbdt-10m": lambda: cpu_hist_gbdt(),
     "pipeline-100k": lambda: {"config": "pipeline-100k", **_run(["scripts/bench_pipeline.py"], 1100)},
-    "gbdt-1m": lambda: {"config": "gbdt-1m", **_run(["bench.py", "--rows", "1000000", "--steps", "3"], 600)},
-    "gbdt-10m": lambda: {"config": "gbdt-10m", **_run(["bench.py", "--steps", "3"], 600)},
+    "gbdt-1m": lambda: _named("gbdt-1m", _run(["bench.py", "--rows", "1000000", "--steps", "3"], 600)),
+    "gbdt-10m": lambda: _named("gbdt-10m", _run(["bench.py", "--steps", "3"], 600)),
     "ooc-100m": lambda: {"config": "ooc-100m",
                          **_run(["scripts/bench_external.py", "--rows", "100000000", "--compare-in-core"], 1100)},
     "score-1b": lambda: {"config": "score-1b", "note": "one 125M-row shard of the 1B-row job (8 ranks x 125M)",
@@ -142,10 +147,10 @@ def main() -> None:
         res = CONFIGS[name]()
         line = json.dumps(res)
         print(line, flush=True)
-        if a.save:
-            d = ROOT / "profiles" / "configs"
-            d.mkdir(parents=True, exist_ok=True)
-            (d / f"{name}.json").write_text(line + "\n")
+        if a.save:  # gpurun_out/ too: that is the directory a GPU-box run copies back
+            for d in (ROOT / "profiles" / "configs", ROOT / "gpurun_out" / "configs"):
+                d.mkdir(parents=True, exist_ok=True)
+                (d / f"{name}.json").write_text(line + "\n")
 
 
 if __name__ == "__main__":
