@@ -365,7 +365,10 @@ __device__ __forceinline__ int ooc_bin(double v) {
   return b < 1 ? 1 : (b >= kOocBins ? kOocBins - 1 : b);
 }
 
-__global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ page, int64_t n, int64_t r0, int F,
+// `ps` = page row stride in bytes: 32 (full row records) or the compact spill format, the F bins
+// rounded up to 4 bytes (20 B for the 20 deployed features: 37% less PCIe traffic per tree -- the
+// per-tree page stream is bound by the H2D copy).
+__global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ page, int ps, int64_t n, int64_t r0, int F,
                                                   const Node* __restrict__ prev, int max_nodes,
                                                   float* __restrict__ margin, const float* __restrict__ label,
                                                   const float* __restrict__ weight, uint64_t key, int64_t row_offset,
@@ -393,9 +396,21 @@ __global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ pa
     bool keep = false;
     uint4 ra = make_uint4(0, 0, 0, 0), rb = make_uint4(0, 0, 0, 0);
     if (in) {
-      const uint4* rec = reinterpret_cast<const uint4*>(page + i * 32);
-      ra = rec[0];
-      rb = rec[1];
+      if (ps == 32) {
+        const uint4* rec = reinterpret_cast<const uint4*>(page + i * 32);
+        ra = rec[0];
+        rb = rec[1];
+        rb.z = rb.w = 0u;  // (g, h) slot: rewritten below for kept rows
+      } else {  // compact page: ps / 4 bin words, the rest of the record is zero padding
+        const uint32_t* rw = reinterpret_cast<const uint32_t*>(page + i * ps);
+        const int nw = ps >> 2;
+        ra.x = rw[0];
+        if (nw > 1) ra.y = rw[1];
+        if (nw > 2) ra.z = rw[2];
+        if (nw > 3) ra.w = rw[3];
+        if (nw > 4) rb.x = rw[4];
+        if (nw > 5) rb.y = rw[5];
+      }
       float mf = margin[r0 + i];
       if (prev != nullptr) {
         int nx = 0;
@@ -455,15 +470,18 @@ __global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ pa
     if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
-COBALT_API int cobalt_ooc_page(const uint8_t* page, int64_t n, int64_t r0, int F, const void* prev, int max_nodes,
+COBALT_API int cobalt_ooc_page(const uint8_t* page, int page_stride, int64_t n, int64_t r0, int F, const void* prev,
+                               int max_nodes,
                                float* margin, const float* label, const float* weight, uint64_t key,
                                int64_t row_offset, double mu, double gscale, double hscale, uint8_t* srec,
                                uint8_t* sbinsT, int64_t cap, unsigned long long* counter, unsigned int* hist,
                                hipStream_t stream) {
   if (F < 1 || F > 24 || max_nodes > 2047 || n < 0) return -3;  // 32-byte records only
+  if (page_stride != 32 && (page_stride % 4 != 0 || page_stride < F || page_stride > 24)) return -3;
   if (n == 0) return 0;
   const int grid = std::max(1, std::min(ceil_div(n, 256), 256 * 8));
-  hipLaunchKernelGGL(k_ooc_page, dim3(grid), dim3(256), 0, stream, page, n, r0, F, static_cast<const Node*>(prev),
+  hipLaunchKernelGGL(k_ooc_page, dim3(grid), dim3(256), 0, stream, page, page_stride, n, r0, F,
+                     static_cast<const Node*>(prev),
                      max_nodes, margin, label, weight, key, row_offset, mu, gscale, hscale, srec, sbinsT, cap, counter,
                      hist);
   CK_LAUNCH();

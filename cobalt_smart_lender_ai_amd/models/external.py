@@ -5,7 +5,9 @@ spill (288 GB HBM per-GPU sizing)").
 The in-core trainer keeps ~72 B per row on the GPU (32-byte row record, feature-major bins, margin,
 label, weight, two row-index buffers), i.e. ~4 G rows per 288 GB MI355X. Beyond that -- or under a
 device-memory budget -- this path keeps only the margins, labels and weights on the device (12 B per
-row) and spills the 32-byte row records to pinned host pages:
+row) and spills the rows' bins to pinned host pages in a compact format (the F bins rounded up to 4
+bytes: 20 B per row for the deployed features instead of the 32-byte record, since the per-tree page
+stream is bound by the H2D copy):
 
 1. ``stream_cuts`` -- the in-core quantile sketch over the stream (same cuts as an in-core fit);
 2. every chunk is binned on the GPU and its row records are copied to a pinned host page;
@@ -42,6 +44,11 @@ _MASK64 = (1 << 64) - 1
 def ooc_key(seed: int, tree: int) -> int:
     """Per-tree key of the MVS keep decision (mirrors ``key`` passed to ``k_ooc_page``)."""
     return gbdt_host.splitmix64_int((seed ^ ((0x5851F42D4C957F2D + tree * 0x632BE59BD9B4E019) & _MASK64)) & _MASK64)
+
+
+def page_stride(n_feat: int) -> int:
+    """Bytes per row of a spilled page: the bins, rounded up to whole 32-bit words."""
+    return (n_feat + 3) // 4 * 4
 
 
 def ghat_bin(v: np.ndarray) -> np.ndarray:
@@ -144,12 +151,14 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
 
         up = _PinnedUploader(dev)
         resident = 0
+        ps = page_stride(F)
         for Xc, yc in source():
             Xc = _as_np(Xc, np.float32)
             rec, _ = gbdt_ops.bin_matrix(up.put(Xc), cuts, nbins)
+            rec = rec[:, :ps]  # bins only: k_ooc_page rebuilds the 32-byte record of a sampled row
             if resident + rec.numel() <= device_page_bytes:  # within the HBM budget: keep it there
                 resident += rec.numel()
-                pages.append((r0, rec))
+                pages.append((r0, rec.contiguous()))
             else:
                 page = torch.empty(rec.shape, dtype=torch.uint8, pin_memory=True)
                 page.copy_(rec)
@@ -299,7 +308,8 @@ class _GpuPasses:
         self.tr.set_data(self.srec, self.sbinsT, cuts.contiguous(), nbins.to(torch.int32).contiguous(),
                          torch.zeros(cap, device=dev), torch.ones(cap, device=dev), torch.zeros(cap, device=dev), fm)
         biggest = max((p.shape[0] for _, p in pages), default=1)
-        self.stage = [torch.empty((biggest, st), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.ps = page_stride(F)
+        self.stage = [torch.empty((biggest, self.ps), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.copy_stream = torch.cuda.Stream(dev)
         self.T = T
 
@@ -312,7 +322,8 @@ class _GpuPasses:
         done = [None, None]  # events: the pass that last read each staging buffer
         for k, (r0, page) in enumerate(self.pages):
             if page.is_cuda:  # HBM-resident page: no copy
-                rc = self.lib.cobalt_ooc_page(page.data_ptr(), page.shape[0], r0, self.F, prev_ptr, self.tr.max_nodes,
+                rc = self.lib.cobalt_ooc_page(page.data_ptr(), page.shape[1], page.shape[0], r0, self.F, prev_ptr,
+                                              self.tr.max_nodes,
                                               self.margin.data_ptr(), self.y.data_ptr(), self.w.data_ptr(), key, 0,
                                               float(mu), self.gscale, self.hscale, self.srec.data_ptr(),
                                               self.sbinsT.data_ptr(), self.cap, self.counter.data_ptr(),
@@ -327,7 +338,8 @@ class _GpuPasses:
                 ev = torch.cuda.Event()
                 ev.record(self.copy_stream)
             cur.wait_event(ev)
-            rc = self.lib.cobalt_ooc_page(buf.data_ptr(), page.shape[0], r0, self.F, prev_ptr, self.tr.max_nodes,
+            rc = self.lib.cobalt_ooc_page(buf.data_ptr(), page.shape[1], page.shape[0], r0, self.F, prev_ptr,
+                                          self.tr.max_nodes,
                                           self.margin.data_ptr(), self.y.data_ptr(), self.w.data_ptr(), key, 0,
                                           float(mu), self.gscale, self.hscale, self.srec.data_ptr(),
                                           self.sbinsT.data_ptr(), self.cap, self.counter.data_ptr(),

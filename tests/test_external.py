@@ -65,11 +65,12 @@ def test_external_gpu_equals_host_path():
     host = external.train_external(src, params, device="cpu", sample_rate=0.25)
     rep = external.ExternalReport()
     dev = external.train_external(src, params, device="cuda", sample_rate=0.25, report=rep)
-    assert rep.n_pages == 6 and rep.host_bytes == 60_000 * 32
+    ps = external.page_stride(X.shape[1])  # compact spill format: 20 B for 20 features
+    assert ps == 20 and rep.n_pages == 6 and rep.host_bytes == 60_000 * ps
     assert dev.save_raw("ubj") == host.save_raw("ubj")
     # half the pages resident in HBM, the rest spilled: the same model
     rep2 = external.ExternalReport()
-    mixed = external.train_external(src, params, device="cuda", sample_rate=0.25, device_page_bytes=33_000 * 32,
+    mixed = external.train_external(src, params, device="cuda", sample_rate=0.25, device_page_bytes=33_000 * ps,
                                     report=rep2)
-    assert rep2.device_page_bytes == 33_000 * 32 and rep2.host_bytes == 27_000 * 32
+    assert rep2.device_page_bytes == 33_000 * ps and rep2.host_bytes == 27_000 * ps
     assert mixed.save_raw("ubj") == host.save_raw("ubj")
