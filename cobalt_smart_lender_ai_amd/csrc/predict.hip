@@ -27,6 +27,42 @@ constexpr int kMaxPath = 16;       // max unique elements per path (incl. bias) 
 }
 
 // ------------------------------------------------------------------------------------ predictor
+// A tree walk is a chain of dependent LDS reads (node -> feature value -> next node), so one
+// thread walks kWalk trees at once: the kWalk chains' loads are independent and overlap. The leaf
+// values are still added to the margin one tree at a time in tree order (same fp32 sum).
+constexpr int kWalk = 4;
+
+template <typename Leaf>
+__device__ __forceinline__ void walk_trees(const uint2* s_nodes, const int32_t* __restrict__ tree_ptr, int nbase,
+                                           int t_begin, int t_end, const float* x, Leaf&& leaf) {
+  for (int t = t_begin; t < t_end; t += kWalk) {
+    uint32_t base[kWalk];
+    uint2 nd[kWalk];
+#pragma unroll
+    for (int k = 0; k < kWalk; ++k) {  // past the tile's end: walk tree t again, result unused
+      base[k] = (uint32_t)(tree_ptr[t + k < t_end ? t + k : t] - nbase);
+      nd[k] = s_nodes[base[k]];
+    }
+    bool more = true;
+    while (more) {
+      more = false;
+#pragma unroll
+      for (int k = 0; k < kWalk; ++k) {
+        if ((nd[k].x & 0xFFFFu) != 0xFFFFu) {
+          const int f = (nd[k].x >> 16) & 0x7FFF;
+          const float v = x[f];
+          const bool left = (v != v) ? ((nd[k].x >> 31) != 0) : (v < __uint_as_float(nd[k].y));
+          nd[k] = s_nodes[base[k] + (nd[k].x & 0xFFFFu) + (left ? 0u : 1u)];
+          more = true;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kWalk; ++k)
+      if (t + k < t_end) leaf(t + k, __uint_as_float(nd[k].y));
+  }
+}
+
 __global__ __launch_bounds__(256) void k_predict(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
                                                  const uint2* __restrict__ nodes, const int32_t* __restrict__ tree_ptr,
                                                  const int32_t* __restrict__ tile_ptr, int n_tiles, float base_margin,
@@ -52,22 +88,7 @@ __global__ __launch_bounds__(256) void k_predict(const float* __restrict__ X, in
     __syncthreads();
     for (int i = threadIdx.x; i < nn; i += blockDim.x) s_nodes[i] = nodes[nbase + i];
     __syncthreads();
-    if (row < n) {
-      for (int t = t_begin; t < t_end; ++t) {
-        const uint2* tn = s_nodes + (tree_ptr[t] - nbase);
-        uint32_t id = 0;
-        uint2 nd = tn[0];
-        while ((nd.x & 0xFFFFu) != 0xFFFFu) {
-          const int f = (nd.x >> 16) & 0x7FFF;
-          const float v = x[f];
-          const float thr = __uint_as_float(nd.y);
-          const bool left = (v != v) ? ((nd.x >> 31) != 0) : (v < thr);
-          id = (nd.x & 0xFFFFu) + (left ? 0u : 1u);
-          nd = tn[id];
-        }
-        acc += __uint_as_float(nd.y);
-      }
-    }
+    if (row < n) walk_trees(s_nodes, tree_ptr, nbase, t_begin, t_end, x, [&](int, float v) { acc += v; });
   }
   if (row < n) {
     if (out_margin) out_margin[row] = acc;
@@ -123,17 +144,8 @@ __global__ __launch_bounds__(256) void k_predict_leaves(const float* __restrict_
   __syncthreads();
   if (row >= n) return;
   const float* x = s_x + threadIdx.x * xs;
-  for (int t = t_begin; t < t_end; ++t) {
-    const uint2* tn = s_nodes + (tree_ptr[t] - nbase);
-    uint2 nd = tn[0];
-    while ((nd.x & 0xFFFFu) != 0xFFFFu) {
-      const int f = (nd.x >> 16) & 0x7FFF;
-      const float v = x[f];
-      const bool left = (v != v) ? ((nd.x >> 31) != 0) : (v < __uint_as_float(nd.y));
-      nd = tn[(nd.x & 0xFFFFu) + (left ? 0u : 1u)];
-    }
-    leaves[(int64_t)t * n + row] = __uint_as_float(nd.y);
-  }
+  walk_trees(s_nodes, tree_ptr, nbase, t_begin, t_end, x,
+             [&](int t, float v) { leaves[(int64_t)t * n + row] = v; });
 }
 
 __global__ void k_sum_leaves(const float* __restrict__ leaves, int64_t n, int T, float base_margin,

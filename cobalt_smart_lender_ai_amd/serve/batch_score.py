@@ -37,10 +37,12 @@ class GraphScorer:
                     predict_ops.predict_gpu(booster, self.x, None, out_prob=self.prob)
 
     def run(self) -> None:
-        if self.graph is not None:
-            self.graph.replay()
-        else:
-            with torch.cuda.stream(self.stream):
+        # on the scorer's stream: a graph replays on the CURRENT stream, and the chunk copies in and
+        # out are ordered on this one (replaying on the default stream raced with both)
+        with torch.cuda.stream(self.stream):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
                 predict_ops.predict_gpu(self.booster, self.x, None, out_prob=self.prob)
 
 
@@ -50,6 +52,7 @@ def score_device_matrix(booster: Booster, X: torch.Tensor, out: torch.Tensor | N
     N, F = X.shape
     out = out if out is not None else torch.empty(N, dtype=torch.float32, device=X.device)
     sc = GraphScorer(booster, min(chunk, N), F, X.device)
+    sc.stream.wait_stream(torch.cuda.current_stream(X.device))  # X may still be in flight there
     for s in range(0, N, sc.chunk):
         e = min(N, s + sc.chunk)
         with torch.cuda.stream(sc.stream):

@@ -104,3 +104,41 @@ def test_shap_pattern_tables_equal_direct_kernel(reference_booster):
         predict_ops._FORCE_DIRECT_SHAP = False
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_large_batch_predictor_matches_host(reference_booster):
+    """The row-block predictor (k_predict, batches past the small-batch path) against the host
+    predictor on NaN-bearing rows: the interleaved tree walks keep the fp32 tree-order sum."""
+    import torch
+
+    from cobalt_smart_lender_ai_amd.ops import predict_ops
+
+    n = predict_ops._SMALL_ROWS + 12_345
+    X = _rows(n, reference_booster.num_feature, seed=11)
+    Xd = torch.from_numpy(X).cuda()
+    margin = torch.empty(n, dtype=torch.float32, device="cuda")
+    prob = torch.empty(n, dtype=torch.float32, device="cuda")
+    predict_ops.predict_gpu(reference_booster, Xd, None, out_margin=margin, out_prob=prob)
+    mh = predict_margin_host(reference_booster, X)
+    np.testing.assert_array_equal(margin.cpu().numpy(), mh)
+
+
+@pytest.mark.gpu
+def test_batch_scoring_chunks_match_host(reference_booster):
+    """Chunked hipGraph batch scoring (device-resident and host-streamed, several chunks plus a
+    ragged tail) equals the host predictor: the graph replays on the scorer's stream, ordered after
+    the chunk copy and before the result copy."""
+    import torch
+
+    from cobalt_smart_lender_ai_amd.serve.batch_score import score_device_matrix, score_shard
+
+    n, chunk = 200_003, 1 << 16
+    X = _rows(n, reference_booster.num_feature, seed=5)
+    ref = sigmoid32(predict_margin_host(reference_booster, X))
+    Xd = torch.from_numpy(X).cuda()
+    Xd.mul_(1.0)  # pending work on the current stream when the scorer starts
+    pd = score_device_matrix(reference_booster, Xd, chunk=chunk).cpu().numpy()
+    np.testing.assert_allclose(pd, ref, rtol=0, atol=2e-7)
+    ph = score_shard(reference_booster, X, chunk=chunk)
+    np.testing.assert_array_equal(ph, pd)
