@@ -6,6 +6,7 @@ CPU path: the NumPy reference implementations in ``models/booster.py``.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -14,12 +15,18 @@ import torch
 from .. import _native
 from ..models.booster import Booster, Tree, predict_margin_host, sigmoid32, treeshap_host
 
-TILE_NODES = 6144
+# LDS tile capacity in nodes: a model's tile is max(this, its largest tree), at most MAX_TILE_NODES
+# (csrc/predict.hip kMaxTileNodes). 2048 measured best on MI355X (125M-row scoring, 300 depth-7
+# trees: 1024 -> 793M, 2048 -> 810M, 3072 -> 683M, 6144 -> 490M, 8192 -> 261M rows/s) -- smaller
+# tiles mean more resident blocks per CU. COBALT_PRED_TILE overrides it for sweeps.
+TILE_NODES = int(os.environ.get("COBALT_PRED_TILE", "2048"))
+MAX_TILE_NODES = 8192
 MAX_PATH = 15
 
 _native.register("cobalt_predict", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p])
 _native.register("cobalt_treeshap", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -28,8 +35,8 @@ _native.register("cobalt_treeshap_chunks", ctypes.c_int, [ctypes.c_int64, ctypes
 _native.register("cobalt_predict_small_rows", ctypes.c_int64, [])
 _native.register("cobalt_predict_small", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_void_p])
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
 _SMALL_ROWS = 131072
 _native.register("cobalt_shap_table_build", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -58,8 +65,21 @@ def _bfs_order(t: Tree) -> list[int]:
     return order
 
 
-def pack_forest(b: Booster, n_trees: int | None = None) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """(nodes uint32 [M, 2], tree_ptr int32 [T+1], tile_ptr int32 [n_tiles+1])."""
+def tile_capacity(b: Booster, n_trees: int | None = None) -> int:
+    """LDS tile capacity (nodes) for this forest: TILE_NODES, grown to fit the largest tree."""
+    trees = b.trees[: (n_trees if n_trees is not None else b.num_trees)]
+    biggest = max((len(t.left_children) for t in trees), default=0)
+    cap = max(TILE_NODES, -(-biggest // 64) * 64)
+    if cap > MAX_TILE_NODES:
+        raise ValueError(f"tree with {biggest} nodes exceeds the LDS tile ({MAX_TILE_NODES} nodes)")
+    return cap
+
+
+def pack_forest(b: Booster, n_trees: int | None = None,
+                tile_nodes: int | None = None) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(nodes uint32 [M, 2], tree_ptr int32 [T+1], tile_ptr int32 [n_tiles+1]); trees are grouped into
+    tiles of at most ``tile_nodes`` (default ``tile_capacity``) nodes."""
+    tile_nodes = tile_capacity(b, n_trees) if tile_nodes is None else tile_nodes
     trees = b.trees[: (n_trees if n_trees is not None else b.num_trees)]
     metas, vals, tree_ptr = [], [], [0]
     for t in trees:
@@ -92,9 +112,9 @@ def pack_forest(b: Booster, n_trees: int | None = None) -> tuple[np.ndarray, np.
     acc = 0
     for i in range(len(trees)):
         sz = tree_ptr[i + 1] - tree_ptr[i]
-        if sz > TILE_NODES:
+        if sz > tile_nodes:
             raise ValueError("tree exceeds the LDS tile")
-        if acc + sz > TILE_NODES:
+        if acc + sz > tile_nodes:
             tiles.append(i)
             acc = 0
         acc += sz
@@ -150,6 +170,7 @@ class _GpuForest:
     tile_ptr: torch.Tensor
     n_tiles: int
     n_trees: int
+    tile_cap: int
     elems: torch.Tensor | None = None
     path_ptr: torch.Tensor | None = None
     path_val: torch.Tensor | None = None
@@ -164,9 +185,10 @@ def gpu_forest(b: Booster, device: torch.device, n_trees: int | None = None, wit
     key = (str(device), n_trees if n_trees is not None else b.num_trees)
     gf = cache.get(key)
     if gf is None:
-        nodes, tptr, tiles = pack_forest(b, n_trees)
+        cap = tile_capacity(b, n_trees)
+        nodes, tptr, tiles = pack_forest(b, n_trees, cap)
         gf = _GpuForest(torch.from_numpy(nodes).to(device), torch.from_numpy(tptr).to(device),
-                        torch.from_numpy(tiles).to(device), len(tiles) - 1, len(tptr) - 1)
+                        torch.from_numpy(tiles).to(device), len(tiles) - 1, len(tptr) - 1, cap)
         cache[key] = gf
     if with_shap and gf.elems is None:
         el, pp, pv, ml = extract_paths(b)
@@ -224,12 +246,13 @@ def predict_gpu(b: Booster, X: torch.Tensor, n_trees: int | None = None, out_mar
         # tile-parallel path (see csrc/predict.hip): grid = row blocks x tree tiles
         leaves = torch.empty(N * gf.n_trees, dtype=torch.float32, device=X.device)
         rc = lib.cobalt_predict_small(X.data_ptr(), N, F, X.stride(0), gf.nodes.data_ptr(), gf.tree_ptr.data_ptr(),
-                                      gf.tile_ptr.data_ptr(), gf.n_tiles, gf.n_trees, b.base_margin,
+                                      gf.tile_ptr.data_ptr(), gf.n_tiles, gf.tile_cap, gf.n_trees, b.base_margin,
                                       leaves.data_ptr(), om, op, _native.stream_handle())
         _native.check(rc, "cobalt_predict_small")
         return
     rc = lib.cobalt_predict(X.data_ptr(), N, F, X.stride(0), gf.nodes.data_ptr(), gf.tree_ptr.data_ptr(),
-                            gf.tile_ptr.data_ptr(), gf.n_tiles, b.base_margin, om, op, _native.stream_handle())
+                            gf.tile_ptr.data_ptr(), gf.n_tiles, gf.tile_cap, b.base_margin, om, op,
+                            _native.stream_handle())
     _native.check(rc, "cobalt_predict")
 
 

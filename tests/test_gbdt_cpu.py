@@ -161,3 +161,20 @@ def test_collective_watchdog_aborts_and_raises():
     assert aborted == [1]
     calls = iter([False, False, True])
     pdist.wait_with_watchdog(lambda: next(calls), timeout_s=1, comm_error=lambda: 0)
+
+
+def test_predictor_tile_packing(reference_booster):
+    """Host packing for the LDS-tiled GPU predictor: every tile holds whole trees within the
+    per-model capacity, tiles cover the forest in order, nodes are in per-tree BFS order."""
+    from cobalt_smart_lender_ai_amd.ops import predict_ops
+
+    cap = predict_ops.tile_capacity(reference_booster)
+    assert predict_ops.TILE_NODES <= cap <= predict_ops.MAX_TILE_NODES
+    nodes, tree_ptr, tiles = predict_ops.pack_forest(reference_booster)
+    assert tiles[0] == 0 and tiles[-1] == reference_booster.num_trees
+    assert np.all(np.diff(tiles) > 0)
+    sizes = tree_ptr[tiles[1:]] - tree_ptr[tiles[:-1]]
+    assert sizes.max() <= cap
+    assert len(nodes) == tree_ptr[-1]
+    small = predict_ops.pack_forest(reference_booster, tile_nodes=int(np.diff(tree_ptr).max()))[2]
+    assert len(small) >= len(tiles)

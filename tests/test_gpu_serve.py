@@ -142,3 +142,27 @@ def test_batch_scoring_chunks_match_host(reference_booster):
     np.testing.assert_allclose(pd, ref, rtol=0, atol=2e-7)
     ph = score_shard(reference_booster, X, chunk=chunk)
     np.testing.assert_array_equal(ph, pd)
+
+
+@pytest.mark.gpu
+def test_deep_trees_grow_the_lds_tile():
+    """Trees larger than the default 2048-node tile (depth 12, host-trained: the GPU trainer stops at
+    depth 10 = 2047 nodes) get a larger per-model tile; both predictor paths equal the host predictor."""
+    import torch
+
+    from cobalt_smart_lender_ai_amd.models import gbdt
+    from cobalt_smart_lender_ai_amd.ops import predict_ops
+
+    rng = np.random.default_rng(3)
+    Xt = rng.normal(size=(40_000, 16)).astype(np.float32)
+    yt = ((Xt[:, 0] * Xt[:, 1] + np.sin(3 * Xt[:, 2]) + rng.normal(size=40_000)) > 0).astype(np.float32)
+    bst = gbdt.train(Xt, yt, {"max_depth": 12, "n_estimators": 4, "min_child_weight": 0.0, "gamma": 0.0},
+                     device="cpu")
+    assert predict_ops.tile_capacity(bst) > predict_ops.TILE_NODES
+    for n in (5000, predict_ops._SMALL_ROWS + 77):
+        X = rng.normal(size=(n, 16)).astype(np.float32)
+        X[rng.random((n, 16)) < 0.05] = np.nan
+        Xd = torch.from_numpy(X).cuda()
+        margin = torch.empty(n, dtype=torch.float32, device="cuda")
+        predict_ops.predict_gpu(bst, Xd, None, out_margin=margin)
+        np.testing.assert_array_equal(margin.cpu().numpy(), predict_margin_host(bst, X))
