@@ -34,9 +34,10 @@ constexpr int kMaxPath = 16;       // max unique elements per path (incl. bias) 
 // A tree walk is a chain of dependent LDS reads (node -> feature value -> next node), so one
 // thread walks kWalk trees at once: the kWalk chains' loads are independent and overlap. The leaf
 // values are still added to the margin one tree at a time in tree order (same fp32 sum).
+// kWalk is the default; COBALT_PRED_WALK=2|8 selects the other instantiations for sweeps.
 constexpr int kWalk = 4;
 
-template <typename Leaf>
+template <int kWalk = ::kWalk, typename Leaf>
 __device__ __forceinline__ void walk_trees(const uint2* s_nodes, const int32_t* __restrict__ tree_ptr, int nbase,
                                            int t_begin, int t_end, const float* x, Leaf&& leaf) {
   for (int t = t_begin; t < t_end; t += kWalk) {
@@ -67,6 +68,7 @@ __device__ __forceinline__ void walk_trees(const uint2* s_nodes, const int32_t* 
   }
 }
 
+template <int W>
 __global__ __launch_bounds__(256) void k_predict(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
                                                  const uint2* __restrict__ nodes, const int32_t* __restrict__ tree_ptr,
                                                  const int32_t* __restrict__ tile_ptr, int n_tiles, float base_margin,
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(256) void k_predict(const float* __restrict__ X, in
     __syncthreads();
     for (int i = threadIdx.x; i < nn; i += blockDim.x) s_nodes[i] = nodes[nbase + i];
     __syncthreads();
-    if (row < n) walk_trees(s_nodes, tree_ptr, nbase, t_begin, t_end, x, [&](int, float v) { acc += v; });
+    if (row < n) walk_trees<W>(s_nodes, tree_ptr, nbase, t_begin, t_end, x, [&](int, float v) { acc += v; });
   }
   if (row < n) {
     if (out_margin) out_margin[row] = acc;
@@ -109,15 +111,29 @@ COBALT_API int cobalt_predict(const float* X, int64_t n, int F, int64_t ldx, con
   const int block = 256;
   const size_t lds = (size_t)tile_cap * sizeof(uint2) + (size_t)block * (F | 1) * sizeof(float);
   if (lds > 160 * 1024) return -3;
+  static const int walk = [] {
+    const char* e = getenv("COBALT_PRED_WALK");
+    const int w = e ? atoi(e) : kWalk;
+    return (w == 2 || w == 8) ? w : kWalk;
+  }();
+  const void* fn = walk == 2 ? (const void*)k_predict<2> : walk == 8 ? (const void*)k_predict<8>
+                                                                       : (const void*)k_predict<kWalk>;
   static size_t attr_set = 64 * 1024;
   if (lds > attr_set) {
-    CK(hipFuncSetAttribute((const void*)k_predict, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr_set = lds;
   }
   const int grid = ceil_div(n, block);
-  hipLaunchKernelGGL(k_predict, dim3(grid), dim3(block), lds, stream, X, n, F, ldx,
-                     static_cast<const uint2*>(nodes), tree_ptr, tile_ptr, n_tiles, base_margin, out_margin, out_prob,
-                     tile_cap);
+  const uint2* nd = static_cast<const uint2*>(nodes);
+  if (walk == 2)
+    hipLaunchKernelGGL(k_predict<2>, dim3(grid), dim3(block), lds, stream, X, n, F, ldx, nd, tree_ptr, tile_ptr,
+                       n_tiles, base_margin, out_margin, out_prob, tile_cap);
+  else if (walk == 8)
+    hipLaunchKernelGGL(k_predict<8>, dim3(grid), dim3(block), lds, stream, X, n, F, ldx, nd, tree_ptr, tile_ptr,
+                       n_tiles, base_margin, out_margin, out_prob, tile_cap);
+  else
+    hipLaunchKernelGGL(k_predict<kWalk>, dim3(grid), dim3(block), lds, stream, X, n, F, ldx, nd, tree_ptr, tile_ptr,
+                       n_tiles, base_margin, out_margin, out_prob, tile_cap);
   CK_LAUNCH();
   return 0;
 }
