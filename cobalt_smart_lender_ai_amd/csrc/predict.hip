@@ -8,7 +8,7 @@
 // BFS order so the right child is always left+1; a node is 8 bytes
 //   uint32 meta = left_child(16 bits, 0xFFFF = leaf) | feature(15 bits) << 16 | default_left << 31
 //   float  val  = split threshold (x < val goes left) or leaf value
-// Trees are grouped into tiles of <= kTileNodes nodes that are staged in LDS; each thread walks
+// Trees are grouped into tiles of <= tile_cap nodes that are staged in LDS; each thread walks
 // one row (features staged in LDS with an odd stride, conflict-free) through every tree of the
 // tile, accumulating the margin in fp32 in tree order (XGBoost CPU predictor semantics).
 //
