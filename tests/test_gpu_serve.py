@@ -126,9 +126,9 @@ def test_large_batch_predictor_matches_host(reference_booster):
 
 @pytest.mark.gpu
 def test_batch_scoring_chunks_match_host(reference_booster):
-    """Chunked hipGraph batch scoring (device-resident and host-streamed, several chunks plus a
-    ragged tail) equals the host predictor: the graph replays on the scorer's stream, ordered after
-    the chunk copy and before the result copy."""
+    """Chunked batch scoring (device-resident in place, device-resident through graph staging, and
+    host-streamed; several chunks plus a ragged tail) equals the host predictor: graphs replay on
+    the scorer's stream, ordered after the chunk copy and before the result copy."""
     import torch
 
     from cobalt_smart_lender_ai_amd.serve.batch_score import score_device_matrix, score_shard
@@ -140,6 +140,10 @@ def test_batch_scoring_chunks_match_host(reference_booster):
     Xd.mul_(1.0)  # pending work on the current stream when the scorer starts
     pd = score_device_matrix(reference_booster, Xd, chunk=chunk).cpu().numpy()
     np.testing.assert_allclose(pd, ref, rtol=0, atol=2e-7)
+    # column-major input takes the GraphScorer staging path (static buffer + replay per chunk)
+    Xc = Xd.t().contiguous().t()
+    assert Xc.stride(1) != 1
+    np.testing.assert_array_equal(score_device_matrix(reference_booster, Xc, chunk=chunk).cpu().numpy(), pd)
     ph = score_shard(reference_booster, X, chunk=chunk)
     np.testing.assert_array_equal(ph, pd)
 
