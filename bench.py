@@ -8,11 +8,13 @@ binary:logistic, 20 features). One step = one complete fit (quantile sketch + bi
 boosting rounds + model fetch), i.e. BASELINE.md's ``rows_per_s = N_train_rows / wall_seconds(fit)``.
 
 Data: synthetic LendingClub-shaped rows (no dataset download is possible) generated on each GPU for
-its own shard by global row index. Scaling mode "weak" (default) gives every rank a 10M-row shard
-(N GPUs train one model on N x 10M rows: per-GPU work fixed, sized for 288 GB HBM -- the
-data-parallel deployment shape); "strong" keeps 10M global rows and shards them over the ranks.
-Strong scaling of a 300-tree x 7-level boosting run is bounded by its 2,100 sequential level steps
-(each needs one histogram all-reduce under DP), see docs/PERF.md for both curves.
+its own shard by global row index. Scaling mode "strong" (the default) keeps the BASELINE config's
+10M GLOBAL rows and shards them over the ranks, so every N trains the same model on the same data
+(BASELINE.json configs[2]: "10M-row GBDT data-parallel ... on 8xMI355X"). "weak" (opt-in,
+``--scaling weak``) gives every rank a 10M-row shard instead (N x 10M global rows); its JSON line
+says so in ``scaling`` and ``rows_global``. Strong scaling of a 300-tree x 7-level boosting run is
+bounded by its 2,100 sequential level steps (each needs one histogram all-reduce under DP), see
+docs/PERF.md.
 
 Launch: ``python bench.py`` (1 GPU) or ``torchrun --nproc-per-node N bench.py --gpus N``.
 Rank 0 prints one JSON line.
@@ -39,7 +41,7 @@ def main() -> None:
     ap.add_argument("--test-rows", type=int, default=1_000_000)
     ap.add_argument("--trees", type=int, default=300)
     ap.add_argument("--depth", type=int, default=7)
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--profile-fit", action="store_true", help="print per-phase timings to stderr")
     a = ap.parse_args()
@@ -128,6 +130,7 @@ def main() -> None:
                 "trees": a.trees,
                 "max_depth": a.depth,
             },
+            "rows_global": n_global,
             "auc": None if auc is None else round(auc, 5),
             "test_rows": a.test_rows,
             "fit_breakdown_ms": {

@@ -140,6 +140,33 @@ struct GbdtDev {
   int32_t ncells;         // sum of nbins: real bins only, so low-cardinality features cost 2-3 cells
   double eta, lambda_, alpha, gamma, mcw, subsample, gscale, hscale, ginv, hinv;
   uint64_t seed;
+  uint64_t* stamps;       // COBALT_STAMPS diagnostics: [launch][kStampBlocks][2] block {start, end} in 10 ns
+                          // ticks; nullptr in normal runs and in unsampled trees
+  int32_t seq;            // launch index into `stamps` (set by the host before every launch)
+};
+
+// In-kernel timing (diagnostic switch COBALT_STAMPS, off by default): the block's first thread
+// stores when the block started and each wave's lane 0 raises the block's end time, into a slot of
+// the block's own ([launch][kStampBlocks][2] ticks of the 100 MHz clock), so the diagnostic adds no
+// contended atomics. Only a few sampled trees are stamped (the host clears d.stamps otherwise).
+constexpr int kStampBlocks = 4096;
+constexpr int kStampSlot = 8;  // per block: start, end, probes 1..6 (thread 0)
+struct BlockStamp {
+  unsigned long long* p;
+  __device__ __forceinline__ explicit BlockStamp(const GbdtDev& d) : p(nullptr) {
+    const int b = blockIdx.x + blockIdx.y * gridDim.x;
+    if (d.stamps && b < kStampBlocks) {
+      p = reinterpret_cast<unsigned long long*>(d.stamps) + ((int64_t)d.seq * kStampBlocks + b) * kStampSlot;
+      if (threadIdx.x == 0) p[0] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  // thread 0's time at probe point k (1..6) of the kernel body
+  __device__ __forceinline__ void probe(int k) {
+    if (p && threadIdx.x == 0) p[1 + k] = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ __forceinline__ ~BlockStamp() {
+    if (p && (threadIdx.x & (kWave - 1)) == 0) atomicMax(p + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -244,6 +271,7 @@ __device__ __forceinline__ float tree_leaf(const GbdtDev& d, int64_t r, const ui
 // subsampling, quantises and packs them into the row record (the root level reads rows in
 // identity order, so ridx needs no reset).
 __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tree) {
+  BlockStamp stamp_(d);
   extern __shared__ uint32_t s_tree[];
   {  // zero the root histogram slot
     int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
@@ -320,6 +348,7 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
 
 // Add tree `t`'s leaf values to the margins (used after the last boosting round).
 __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
+  BlockStamp stamp_(d);
   extern __shared__ uint32_t s_tree[];
   uint32_t* s_meta = s_tree;
   float* s_leaf = reinterpret_cast<float*>(s_tree + d.max_nodes);
@@ -333,6 +362,7 @@ __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
 // Start of a tree grown from precomputed gradients (external-memory path): node-table reset and the
 // root histogram slot zeroed (k_hist_reduce accumulates into it; k_grad does this on the normal path).
 __global__ __launch_bounds__(256) void k_tree_begin(GbdtDev d) {
+  BlockStamp stamp_(d);
   int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
        e += (int64_t)gridDim.x * blockDim.x)
@@ -678,6 +708,7 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
 template <int U>
 __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
+  BlockStamp stamp_(d);
   extern __shared__ uint64_t s_dyn[];
   __shared__ int64_t s_tot[2][16];
   const int entries = d.tile_entries[0] + kWave;
@@ -703,6 +734,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   }
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   __syncthreads();
+  stamp_.probe(1);
   const int item = blockIdx.x;
   const int64_t begin = (int64_t)item * chunk, end = min(d.n, begin + chunk);
   if (threadIdx.x == 0) {
@@ -771,12 +803,14 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
     }
   }
   __syncthreads();
+  stamp_.probe(2);
   hist_flush(d, s_hist, hl, item, 0, ft, tg, th, true, s_tot);
 }
 
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 
 __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk) {
+  BlockStamp stamp_(d);
   extern __shared__ uint64_t s_hist[];
   __shared__ int64_t s_tot[2][16];
   __shared__ int s_plan[5];
@@ -784,6 +818,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   const int n_ent = level == 0 ? 1 : (1 << (level - 1));
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
                                 s_plan);
+  stamp_.probe(1);
   if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total, d.by_hess != 0);
   if (pl.node < 0) return;
   WorkItem w;
@@ -803,6 +838,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
 
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   __syncthreads();
+  stamp_.probe(2);
 
   const int32_t* rix = d.ridx[parity];
   const bool identity = parity == 0 && w.node == 0;  // root level: ridx is the identity
@@ -893,6 +929,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   }
   }
   __syncthreads();
+  stamp_.probe(3);
   // Per-item partial histogram -> slab (plain coalesced stores; the packed u64 of the K copies can
   // be summed directly because the per-item sums obey the same < 2^31 / < 2^32 bounds).
   if (d.ablate == 2) return;  // timing-only: no flush
@@ -905,9 +942,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
 constexpr int kRedItems = 16;
 
 __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int publish) {
+  BlockStamp stamp_(d);
   // fused partition path: block (0, 0) publishes the level's node ranges from the finished claims
   if (publish > 0 && blockIdx.x == 0 && blockIdx.y == 0) publish_level(d, publish, -1, true);
   const int n_items = d.counters[0];
+  stamp_.probe(1);
   const int i0 = blockIdx.x * kRedItems;
   if (i0 >= n_items) return;
   const int cnt = min(n_items - i0, kRedItems);
@@ -937,6 +976,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
   for (int k = 0; k < kRedItems; ++k)
     if (k >= cnt) { g[k] = 0; h[k] = 0; slot[k] = slot[cnt - 1]; }
   // items of one slot are consecutive: flush one atomic pair per (run, slot)
+  stamp_.probe(2);
   int cur = slot[0];
   int64_t sg = 0, sh = 0;
 #pragma unroll
@@ -968,6 +1008,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
 // replaces an all-reduce of the children's row counts per level (one collective, and one
 // cross-rank synchronisation, fewer per level). Grid: (pair, 256-cell block); level 0 keeps the root.
 __global__ __launch_bounds__(256) void k_dp_local(GbdtDev d, int level, int parity) {
+  BlockStamp stamp_(d);
   const int p = blockIdx.x;
   const int64_t e = ((int64_t)blockIdx.y * blockDim.x + threadIdx.x) * 2;  // (g, h) of one cell
   if (e >= d.slot_elems) return;
@@ -1087,6 +1128,7 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
 // is issue-bound on a single CU); each group writes its best candidate and k_eval_finish reduces them.
 template <bool kGroups>
 __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg) {
+  BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   const int fbeg = kGroups ? blockIdx.y * fg : 0;
   const int fend = kGroups ? min(d.F, fbeg + fg) : d.F;
@@ -1130,6 +1172,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     H = hb[(int64_t)d.ncells * 2 + 1];
   }
   if (status != kActive) return;
+  stamp_.probe(1);
   __shared__ Cand s_best[16];
   __shared__ float s_cut[16];
   const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
@@ -1222,6 +1265,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     }
   }
   }
+  stamp_.probe(2);
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) {
     Cand other = cand_shfl_xor(best, o);
@@ -1230,6 +1274,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   }
   if (lane == 0) { s_best[wave_id()] = best; s_cut[wave_id()] = best_cut; }
   __syncthreads();
+  stamp_.probe(3);
   if (threadIdx.x != 0) return;
   for (int k = 1; k < nw; ++k)
     if (cand_better(s_best[k], best)) { best = s_best[k]; best_cut = s_cut[k]; }
@@ -1243,10 +1288,12 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     return;
   }
   eval_finalize(d, level, n, G, H, best, best_cut);
+  stamp_.probe(4);
 }
 
 // Reduce the per-group candidates of each node of the level (one wave per node, lane = group).
 __global__ __launch_bounds__(64) void k_eval_finish(GbdtDev d, int level, int parity, int ngroups) {
+  BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   const int n = (1 << level) - 1 + pos;
   const Node& nd = d.nodes[n];
@@ -1305,6 +1352,7 @@ __device__ __forceinline__ bool goes_left(const uint8_t* col, int r, int j, bool
 template <int kPartWaves>
 __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int parity, int64_t zero_next, int level,
                                                                int chunk) {
+  BlockStamp stamp_(d);
   __shared__ int32_t s_cnt[2][kPartWaves];
   __shared__ int32_t s_base[2];
   __shared__ int s_plan[5];
@@ -1320,6 +1368,7 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
     const Node& n = d.nodes[first + e];
     return (n.status == kSplit && n.count > 0) ? PlanEntry{first + e, 0, n.start, n.count} : PlanEntry{-1, 0, 0, 0};
   }, s_plan);
+  stamp_.probe(1);
   if (pl.node < 0) return;
   WorkItem w;
   w.node = pl.node;
@@ -1358,6 +1407,7 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   }
   if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nr; }
   __syncthreads();
+  stamp_.probe(2);
   if (threadIdx.x == 0) {
     int tl = 0, tr = 0;
     for (int k = 0; k < kPartWaves; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
@@ -1371,6 +1421,7 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
     }
   }
   __syncthreads();
+  stamp_.probe(3);
   int bl = s_base[0], br = s_base[1];
   for (int k = 0; k < wv; ++k) { bl += s_cnt[0][k]; br += s_cnt[1][k]; }
   const int rend = nd.start + nd.count - 1;
@@ -1404,6 +1455,7 @@ constexpr int kPartHistRows = kPartHistWaves * kPartHistSteps * kWave;  // 8192 
 template <int kPW, int kPS>
 __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, int64_t zero_next, int level,
                                                         int chunk, int tree) {
+  BlockStamp stamp_(d);
   extern __shared__ uint64_t s_hist[];
   __shared__ int32_t s_cnt[2][kPW];
   __shared__ int32_t s_base[2];
@@ -1538,7 +1590,68 @@ struct GbdtCtx {
   int applied = 0;         // number of leading trees whose leaves are already in the margins
   int grown = 0;            // number of trees grown so far
   std::vector<void*> allocs;
+  // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
+  const char* stamp_path = nullptr;
+  int stamp_cap = 0;
+  uint64_t* stamp_buf = nullptr;
+  std::vector<const char*> stamp_names;
 };
+
+// Next launch's stamp slot (0 when stamping is off or the tree is not sampled: d.stamps == nullptr).
+static int stamp_next(GbdtCtx* c, const char* name) {
+  if (!c->stamp_path || !c->d.stamps) return 0;
+  if ((int)c->stamp_names.size() >= c->stamp_cap) { c->d.stamps = nullptr; return 0; }
+  c->stamp_names.push_back(name);
+  return (int)c->stamp_names.size() - 1;
+}
+// Launch with a stamp slot (COBALT_STAMPS); arguments as hipLaunchKernelGGL.
+#define GLAUNCH(tag, ...)               \
+  do {                                  \
+    c->d.seq = stamp_next(c, tag);      \
+    hipLaunchKernelGGL(__VA_ARGS__);    \
+  } while (0)
+
+// Trees whose launches are stamped: every 64th from tree 5 (and tree 0 of short fits).
+static bool stamp_tree(GbdtCtx* c, int t) { return c->stamp_path && (t % 64 == 5 || (c->grown < 5 && t == 0)); }
+
+static int stamp_begin(GbdtCtx* c, hipStream_t stream) {
+  if (!c->stamp_path) return 0;
+  c->stamp_names.clear();
+  CK(hipMemsetAsync(c->stamp_buf, 0, (size_t)c->stamp_cap * kStampBlocks * kStampSlot * sizeof(uint64_t), stream));
+  return 0;
+}
+
+static int stamp_dump(GbdtCtx* c, hipStream_t stream) {
+  if (!c->stamp_path || c->stamp_names.empty()) return 0;
+  const int n = (int)c->stamp_names.size();
+  std::vector<uint64_t> v((size_t)n * kStampBlocks * kStampSlot);
+  CK(hipStreamSynchronize(stream));
+  CK(hipMemcpy(v.data(), c->stamp_buf, v.size() * 8, hipMemcpyDeviceToHost));
+  FILE* f = fopen(c->stamp_path, "a");
+  if (!f) return 0;
+  fprintf(f, "# launch name first_start last_end last_start blocks probe1..6 (mean ticks after block start)\n");
+  for (int i = 0; i < n; ++i) {
+    uint64_t st = ~0ull, en = 0, ls = 0, nb = 0;
+    double pr[6] = {0, 0, 0, 0, 0, 0};
+    int pn[6] = {0, 0, 0, 0, 0, 0};
+    for (int b = 0; b < kStampBlocks; ++b) {
+      const uint64_t* q = &v[((size_t)i * kStampBlocks + b) * kStampSlot];
+      if (!q[0]) continue;
+      ++nb;
+      st = std::min(st, q[0]);
+      ls = std::max(ls, q[0]);
+      en = std::max(en, q[1]);
+      for (int k = 0; k < 6; ++k)
+        if (q[2 + k]) { pr[k] += (double)(q[2 + k] - q[0]); ++pn[k]; }
+    }
+    fprintf(f, "%d %s %llu %llu %llu %llu", i, c->stamp_names[i], (unsigned long long)(nb ? st : 0),
+            (unsigned long long)en, (unsigned long long)ls, (unsigned long long)nb);
+    for (int k = 0; k < 6; ++k) fprintf(f, " %.1f", pn[k] ? pr[k] / pn[k] : -1.0);
+    fprintf(f, "\n");
+  }
+  fclose(f);
+  return 0;
+}
 
 static int pow2_clamp(int64_t v, int lo, int hi) {
   int c = lo;
@@ -1646,6 +1759,14 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.hoff, (F + 1) * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.tile_entries, ntiles * sizeof(int32_t)))) return rc;
+  d.stamps = nullptr;
+  d.seq = 0;
+  if (getenv("COBALT_STAMPS")) {
+    c->stamp_path = getenv("COBALT_STAMPS");
+    c->stamp_cap = 512;
+    if ((rc = dev_alloc(c, (void**)&c->stamp_buf, (size_t)c->stamp_cap * kStampBlocks * kStampSlot * sizeof(uint64_t))))
+      return rc;
+  }
   *out = c;
   return 0;
 }
@@ -1713,6 +1834,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const int ftiles = ceil_div(d.F, d.feat_tile);
   const size_t tree_lds = (size_t)c->max_nodes * 8;
   if (t0 != c->grown) return -11;  // trees must be grown in order
+  if (int rc = stamp_begin(c, stream)) return rc;
   // any native communicator turns on the data-parallel protocol (a 1-rank one exercises it on 1 GPU)
   const bool dp = c->cfg.comm != nullptr;
   d.dp = dp ? 1 : 0;
@@ -1743,18 +1865,19 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     if (t >= c->cfg.max_trees) return -10;
     d.nodes = d.nodes_buf[t & 1];
     d.prev_nodes = d.nodes_buf[(t + 1) & 1];
+    d.stamps = stamp_tree(c, t) ? c->stamp_buf : nullptr;
     const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
     if (sampled)
-      hipLaunchKernelGGL(k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
-                         stream, d);
+      GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
+              stream, d);
     else if (fuse_root && grad_u == 4)
-      hipLaunchKernelGGL(k_grad_hist<4>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
-                         d, t, apply, root_chunk);
+      GLAUNCH("k_grad_hist", k_grad_hist<4>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
+              d, t, apply, root_chunk);
     else if (fuse_root)
-      hipLaunchKernelGGL(k_grad_hist<2>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
-                         d, t, apply, root_chunk);
+      GLAUNCH("k_grad_hist", k_grad_hist<2>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
+              d, t, apply, root_chunk);
     else
-      hipLaunchKernelGGL(k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
+      GLAUNCH("k_grad", k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
     if (apply >= 0 && !sampled) c->applied = t;
     CK_LAUNCH();
     for (int level = 0; level < D; ++level) {
@@ -1764,25 +1887,25 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       if (fuse_part && level > 0) {  // partition of level - 1 and this level's histogram in one pass
         const int pl = level - 1;
         ub = ceil_div(d.n, kPartHistRows) + (1 << pl);
-        hipLaunchKernelGGL((k_part_hist<kPartHistWaves, kPartHistSteps>), dim3(ub), dim3(kPartHistWaves * kWave),
-                           c->lds_hist, stream, d, pl & 1, (int64_t)(1 << pl) * d.slot_elems, pl, kPartHistRows, t);
+        GLAUNCH("k_part_hist", (k_part_hist<kPartHistWaves, kPartHistSteps>), dim3(ub), dim3(kPartHistWaves * kWave),
+                c->lds_hist, stream, d, pl & 1, (int64_t)(1 << pl) * d.slot_elems, pl, kPartHistRows, t);
       } else {
         const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
         ub = ceil_div(d.n, chh) + (1 << level);
         if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-          hipLaunchKernelGGL(k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level,
-                             chh);
+          GLAUNCH("k_hist", k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level,
+                  chh);
       }
-      hipLaunchKernelGGL(k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
-                         dim3(256), 0, stream, d, parity, fuse_part ? level : 0);
+      GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
+              dim3(256), 0, stream, d, parity, fuse_part ? level : 0);
       CK_LAUNCH();
       if (dp) {
         // row-count choice: ranks built their locally smaller child -> turn it into the local LEFT
         // child; hessian choice (the DP default) / fused pass: every rank built the globally chosen
         // child, all-reduced as is
         if (!fuse_part && !d.by_hess) {
-          hipLaunchKernelGGL(k_dp_local, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d,
-                             level, parity);
+          GLAUNCH("k_dp_local", k_dp_local, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d,
+                  level, parity);
           CK_LAUNCH();
         }
         int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
@@ -1790,20 +1913,20 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       }
       if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
         const int ng = ceil_div(d.F, eval_fg);
-        hipLaunchKernelGGL(k_eval<true>, dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d, level,
-                           parity, t, eval_fg);
-        hipLaunchKernelGGL(k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
+        GLAUNCH("k_eval", k_eval<true>, dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d, level,
+                parity, t, eval_fg);
+        GLAUNCH("k_eval_finish", k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
       } else {
-        hipLaunchKernelGGL(k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
+        GLAUNCH("k_eval", k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
       }
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
         const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;
         if (part_wide(d))
-          hipLaunchKernelGGL(k_partition<16>, dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next, level, chp);
+          GLAUNCH("k_partition", k_partition<16>, dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next, level, chp);
         else
-          hipLaunchKernelGGL(k_partition<4>, dim3(ubp), dim3(4 * kWave), 0, stream, d, parity, zero_next, level, chp);
+          GLAUNCH("k_partition", k_partition<4>, dim3(ubp), dim3(4 * kWave), 0, stream, d, parity, zero_next, level, chp);
       }
       CK_LAUNCH();
     }
@@ -1818,11 +1941,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   }
   // bring the margins up to date with the last grown tree
   if (c->applied < c->grown) {
-    hipLaunchKernelGGL(k_apply_tree, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, c->grown - 1);
+    GLAUNCH("k_apply_tree", k_apply_tree, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, c->grown - 1);
     CK_LAUNCH();
     c->applied = c->grown;
   }
-  return 0;
+  d.stamps = nullptr;
+  return stamp_dump(c, stream);
 }
 
 COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream) {

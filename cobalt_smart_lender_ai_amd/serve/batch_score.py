@@ -60,7 +60,8 @@ def score_device_matrix(booster: Booster, X: torch.Tensor, out: torch.Tensor | N
     out = out if out is not None else torch.empty(N, dtype=torch.float32, device=X.device)
     if N == 0:
         return out
-    if X.dtype == torch.float32 and X.stride(1) == 1 and out.is_contiguous():
+    if (X.dtype == torch.float32 and X.stride(1) == 1 and out.is_contiguous()
+            and out.dtype == torch.float32 and out.device == X.device):
         predict_ops.gpu_forest(booster, X.device)  # pack + upload the forest outside the capture
         cur = torch.cuda.current_stream(X.device)
         side = torch.cuda.Stream(X.device)
