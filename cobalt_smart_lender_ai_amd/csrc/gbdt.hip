@@ -619,13 +619,29 @@ struct HistLanes {
 // Per-tile feature state for the LDS histogram lanes. Lane k loads feature f0 + k's colsample bit and
 // copy shift (one round trip, instead of 2 x ft dependent scalar loads per thread -- ~10 us per block
 // for a 32-feature tile), and ballots spread them to every lane. Called by every thread of a block.
-__device__ __forceinline__ HistLanes hist_lanes(const GbdtDev& d, int tree, int f0, int ft) {
+// The loads are split from the ballots (hist_lanes_load / hist_lanes_finish) so a kernel can issue
+// them together with its other independent loads (work plan, flush offsets): one round trip for all.
+struct HistLaneRaw {
+  bool on;
+  int sh;
+};
+
+__device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tree, int f0, int ft) {
+  const int lane = lane_id();
+  const bool in = lane < ft;
+  const int f = f0 + (in ? lane : 0);
+  HistLaneRaw r;
+  r.on = in && d.fmask[(int64_t)tree * d.F + f] != 0;
+  r.sh = in ? (d.layout[f].y & 7) : 0;
+  return r;
+}
+
+__device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, int ft) {
   HistLanes hl;
   hl.lane = lane_id();
   const bool in = (int)hl.lane < ft;
-  const int f = f0 + (in ? (int)hl.lane : 0);
-  const bool on = in && d.fmask[(int64_t)tree * d.F + f] != 0;
-  const int sh = in ? (d.layout[f].y & 7) : 0;
+  const bool on = raw.on;
+  const int sh = raw.sh;
   hl.fbits = __ballot(on);
   const uint64_t b0 = __ballot(in && (sh & 1)), b1 = __ballot(in && (sh & 2)), b2 = __ballot(in && (sh & 4));
   hl.sh0 = hl.sh1 = hl.sh2 = hl.sh3 = 0;
@@ -636,6 +652,10 @@ __device__ __forceinline__ HistLanes hist_lanes(const GbdtDev& d, int tree, int 
   }
   hl.trash = (uint32_t)(ft * kMaxBins) + hl.lane;
   return hl;
+}
+
+__device__ __forceinline__ HistLanes hist_lanes(const GbdtDev& d, int tree, int f0, int ft) {
+  return hist_lanes_finish(hist_lanes_load(d, tree, f0, ft), ft);
 }
 
 // Add one 32-byte record (bins in a.xyzw / b.xy, packed (g, h) in b.wz) to the LDS histogram.
@@ -664,13 +684,34 @@ __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes
 // 106-feature RFE fits, where every block flushes 4 x 8k cells).
 constexpr int kMaxFeatTile = 64;
 
+// Flush metadata of a tile, staged into LDS by the kernel prologue (its loads share the round trip of
+// the work plan; the prologue's barrier publishes it): s_fo = compact cell offset of each tile feature
+// (+ the end), s_fs = its log2(copies), or -1 when masked out for this tree.
+struct FlushMeta {
+  int fo, fs;
+};
+
+__device__ __forceinline__ FlushMeta flush_meta_load(const GbdtDev& d, int tree, int f0, int ft) {
+  FlushMeta m{0, -1};
+  const int t = threadIdx.x;
+  if (t <= ft) m.fo = d.hoff[f0 + t];
+  if (t < ft) m.fs = d.fmask[(int64_t)tree * d.F + f0 + t] != 0 ? d.layout[f0 + t].y : -1;
+  return m;
+}
+
+__device__ __forceinline__ void flush_meta_store(const FlushMeta& m, int ft, int* s_fo, int* s_fs) {
+  const int t = threadIdx.x;
+  if (t <= ft) s_fo[t] = m.fo;
+  if (t < ft) s_fs[t] = m.fs;
+}
+
 __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistLanes& hl, int item, int f0, int ft,
-                           int64_t tg, int64_t th, bool tot_block, int64_t (*s_tot)[16]) {
-  __shared__ int s_fo[kMaxFeatTile + 1];  // compact cell offset of each tile feature (+ the end)
-  __shared__ int s_fs[kMaxFeatTile];      // its log2(copies), or -1 when masked out for this tree
-  if (threadIdx.x <= ft) s_fo[threadIdx.x] = d.hoff[f0 + threadIdx.x];
-  if (threadIdx.x < ft) s_fs[threadIdx.x] = ((hl.fbits >> threadIdx.x) & 1ull) ? d.layout[f0 + threadIdx.x].y : -1;
-  __syncthreads();
+                           int64_t tg, int64_t th, bool tot_block, int64_t (*s_tot)[16], const int* s_fo,
+                           const int* s_fs) {
+  // Each cell finds its feature by a binary search over the LDS-staged offsets and sums its copies.
+  // (A wave-segmented form -- every thread reads one LDS entry and xor-shuffles the copies together --
+  // measured slower at 1M rows: 20.3 vs 18.7 us per k_hist, the 64-bit shuffles of the 64-copy binary
+  // features go through ds_bpermute and cost more LDS cycles than the reads they replace.)
   const int c0 = s_fo[0], c1 = s_fo[ft];
   uint64_t* slab = d.slab + (int64_t)item * d.ncells;
   for (int e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
@@ -711,7 +752,12 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_dyn[];
   __shared__ int64_t s_tot[2][16];
-  const int entries = d.tile_entries[0] + kWave;
+  __shared__ int s_fo[kMaxFeatTile + 1], s_fs[kMaxFeatTile];
+  const int ft = d.F;
+  const int entries = ft * kMaxBins + kWave;  // one tile: tile_entries[0] == F * 256
+  // independent metadata loads first (they share the round trip of the previous tree's node table)
+  const HistLaneRaw lraw = hist_lanes_load(d, tree, 0, ft);
+  const FlushMeta fmeta = flush_meta_load(d, tree, 0, ft);
   uint64_t* s_hist = s_dyn;
   uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries);
   float* s_leaf = reinterpret_cast<float*>(s_meta + d.max_nodes);
@@ -733,6 +779,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
     if (threadIdx.x == 0) d.counters[0] = gridDim.x;
   }
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
+  flush_meta_store(fmeta, ft, s_fo, s_fs);
   __syncthreads();
   stamp_.probe(1);
   const int item = blockIdx.x;
@@ -742,8 +789,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
     w.node = 0; w.slot = 0; w.begin = (int32_t)begin; w.end = (int32_t)end;
     d.items_h[item] = w;
   }
-  const int ft = d.F;
-  const HistLanes hl = hist_lanes(d, tree, 0, ft);
+  const HistLanes hl = hist_lanes_finish(lraw, ft);
   const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
@@ -804,7 +850,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   }
   __syncthreads();
   stamp_.probe(2);
-  hist_flush(d, s_hist, hl, item, 0, ft, tg, th, true, s_tot);
+  hist_flush(d, s_hist, hl, item, 0, ft, tg, th, true, s_tot, s_fo, s_fs);
 }
 
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
@@ -814,8 +860,19 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   extern __shared__ uint64_t s_hist[];
   __shared__ int64_t s_tot[2][16];
   __shared__ int s_plan[5];
+  __shared__ int s_fo[kMaxFeatTile + 1], s_fs[kMaxFeatTile];
   const int item = blockIdx.x;
   const int n_ent = level == 0 ? 1 : (1 << (level - 1));
+  const int f0 = blockIdx.y * d.feat_tile;  // < F: gridDim.y = ceil(F / feat_tile)
+  const int ft = min(d.feat_tile, d.F - f0);
+  // Prologue: the tile's lane setup and flush offsets do not depend on the node table, so their loads
+  // go out with the plan's (one round trip instead of three), and the LDS histogram is zeroed while
+  // they are in flight (block_plan's barrier publishes both).
+  const HistLaneRaw lraw = hist_lanes_load(d, tree, f0, ft);
+  const FlushMeta fmeta = flush_meta_load(d, tree, f0, ft);
+  const int entries = ft * kMaxBins + kWave;  // tile_entries[y] == ft * 256, + per-lane trash cells
+  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
+  flush_meta_store(fmeta, ft, s_fo, s_fs);
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
                                 s_plan);
   stamp_.probe(1);
@@ -827,17 +884,10 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   w.begin = pl.begin;
   w.end = pl.end;
   if (blockIdx.y == 0 && threadIdx.x == 0) d.items_h[item] = w;
-  const int f0 = blockIdx.y * d.feat_tile;
-  if (f0 >= d.F) return;
   if (d.ablate == 4) return;  // timing-only: plan + publish only
-  const int ft = min(d.feat_tile, d.F - f0);
-  const int entries = d.tile_entries[blockIdx.y] + kWave;  // + per-lane trash cells
-  const HistLanes hl = hist_lanes(d, tree, f0, ft);
+  const HistLanes hl = hist_lanes_finish(lraw, ft);
   const uint64_t fbits = hl.fbits;
   const uint32_t sh0 = hl.sh0, sh1 = hl.sh1, sh2 = hl.sh2, sh3 = hl.sh3;
-
-  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
-  __syncthreads();
   stamp_.probe(2);
 
   const int32_t* rix = d.ridx[parity];
@@ -933,7 +983,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   // Per-item partial histogram -> slab (plain coalesced stores; the packed u64 of the K copies can
   // be summed directly because the per-item sums obey the same < 2^31 / < 2^32 bounds).
   if (d.ablate == 2) return;  // timing-only: no flush
-  hist_flush(d, s_hist, hl, item, f0, ft, tg, th, blockIdx.y == 0, s_tot);
+  hist_flush(d, s_hist, hl, item, f0, ft, tg, th, blockIdx.y == 0, s_tot, s_fo, s_fs);
 }
 
 // Reduce the per-item slabs into the level's histogram slots: thread = one compact (feature, bin)
@@ -1071,7 +1121,9 @@ struct EvalFeat {
 };
 
 // Node decision from its best candidate (split or leaf; children of the last split level become leaves).
-__device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int64_t H, Cand best, float best_cut) {
+// `nb_known` >= 0: the winning feature's bin count (the compact evaluator has it in LDS), else loaded.
+__device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int64_t H, Cand best, float best_cut,
+                              int nb_known = -1) {
   Node* nodes = d.nodes;
   const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
   const float loss = (float)best.gain;
@@ -1084,7 +1136,7 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
   if (ok) {
     const int f = best.key >> 10;
     const int r = best.key & 1023;
-    const int nb = d.nbins[f];
+    const int nb = nb_known >= 0 ? nb_known : d.nbins[f];
     int j, dl;
     if (r < 512) { j = r; dl = 0; } else { j = (nb - 1 - (r - 512)) - 1; dl = 1; }
     nd.status = kSplit;
@@ -1327,6 +1379,199 @@ __global__ __launch_bounds__(64) void k_eval_finish(GbdtDev d, int level, int pa
   if (lane == 0) eval_finalize(d, level, n, G, H, best, best_cut);
 }
 
+// Compact split evaluation (F <= kEvalMaxF): the node's candidates are enumerated over its compact
+// histogram cells (sum of nbins: ~1.3k for the 20 deployed features, of which 8 are binary) instead of
+// F x 256 bin slots (5.1k), so the fp64 gain scan -- which made k_eval compute-bound on its single CU
+// (~6 us of the ~14 us per level) -- shrinks ~4x. Thread = kEvalCPT consecutive cells; a block-wide
+// int64 prefix scan over all cells, minus the prefix at each feature's first cell, gives every
+// candidate's left sums (cells are spread evenly, ceil(ncells / 1024) per thread, so all 16 waves
+// share the gain work). Gains, keys, tie-breaks and the finalisation are those of k_eval, so the
+// trees are bit-identical. Latency: one round trip for the node record + feature table, one for the
+// cells (+ the parent's for the subtraction) and their cut values, then LDS only.
+constexpr int kEvalThreads = 1024;
+constexpr int kEvalCPT = 8;        // cells per thread: ncells <= 8192
+constexpr int kEvalMaxF = 32;
+
+__global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int level, int parity, int tree) {
+  BlockStamp stamp_(d);
+  __shared__ int s_hoff[kEvalMaxF + 1];
+  __shared__ int s_nb[kEvalMaxF];
+  __shared__ int s_on[kEvalMaxF];
+  __shared__ int64_t s_wg[kEvalThreads / kWave], s_wh[kEvalThreads / kWave];
+  __shared__ int64_t s_bg[kEvalMaxF + 1], s_bh[kEvalMaxF + 1];  // prefix before each feature's first cell
+  __shared__ Cand s_best[kEvalThreads / kWave];
+  __shared__ float s_cut[kEvalThreads / kWave];
+  const int pos = blockIdx.x;
+  const int n = (1 << level) - 1 + pos;
+  const int F = d.F;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int64_t SE = d.slot_elems;
+  const int pair = level == 0 ? 0 : (pos >> 1);
+  const int64_t* hb = d.hist_b[parity] + pair * SE;
+  int64_t* hs = d.hist_s[parity] + pair * SE;
+  // round trip 1: feature table (LDS) + node record (uniform)
+  if (t <= F) s_hoff[t] = d.hoff[t];
+  if (t < F) {
+    s_nb[t] = d.nbins[t];
+    s_on[t] = d.fmask[(int64_t)tree * F + t] != 0;
+  }
+  const Node* nodes = d.nodes;
+  const int status = nodes[n].status;
+  const bool built = nodes[n].build != 0;
+  int64_t G = nodes[n].G, H = nodes[n].H;
+  int pbuild = 1;
+  if (level > 0) pbuild = nodes[(1 << (level - 1)) - 1 + (pos >> 1)].build;
+  if (level == 0) {
+    G = hb[(int64_t)d.ncells * 2];
+    H = hb[(int64_t)d.ncells * 2 + 1];
+  }
+  if (status != kActive) return;  // uniform across the block
+  __syncthreads();
+  stamp_.probe(1);
+  const int nc = s_hoff[F];
+  const int cpt = (nc + kEvalThreads - 1) / kEvalThreads;  // cells per thread: every wave gets work
+  const int c0 = t * cpt;
+  const int64_t* parent = nullptr;
+  if (!built) {
+    const int ppos = pos >> 1;
+    const int ppair = level == 1 ? 0 : (ppos >> 1);
+    parent = (pbuild ? d.hist_b[parity ^ 1] : d.hist_s[parity ^ 1]) + ppair * SE;
+  }
+  // feature of the thread's first cell (largest f with s_hoff[f] <= c0)
+  int f0 = 0;
+  {
+    int lo = 0, hi = F - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_hoff[mid] <= c0) lo = mid; else hi = mid - 1;
+    }
+    f0 = lo;
+  }
+  // round trip 2: cells, parent cells, cut values of the cells (and of the bin before the first one)
+  int64_t g[kEvalCPT], h[kEvalCPT];
+  float cut[kEvalCPT];
+  float cutm1 = -FLT_MAX;
+  {
+    int f = f0;
+#pragma unroll
+    for (int k = 0; k < kEvalCPT; ++k) {
+      const int c = c0 + k;
+      const bool in = k < cpt && c < nc;
+      while (f + 1 < F && s_hoff[f + 1] <= c) ++f;
+      const int b = c - s_hoff[f];
+      const int64_t bg = in ? hb[2 * c] : 0, bh = in ? hb[2 * c + 1] : 0;
+      const int64_t pg = (in && !built) ? parent[2 * c] : 0, ph = (in && !built) ? parent[2 * c + 1] : 0;
+      g[k] = built ? bg : pg - bg;
+      h[k] = built ? bh : ph - bh;
+      cut[k] = in ? d.cuts[f * kMaxBins + b] : FLT_MAX;
+    }
+    const int b0 = c0 - s_hoff[f0];
+    if (c0 < nc && b0 > 0) cutm1 = d.cuts[f0 * kMaxBins + b0 - 1];
+  }
+  if (!built) {  // materialise the sibling histogram for the next level
+#pragma unroll
+    for (int k = 0; k < kEvalCPT; ++k) {
+      const int c = c0 + k;
+      if (k < cpt && c < nc) {
+        hs[2 * c] = g[k];
+        hs[2 * c + 1] = h[k];
+      }
+    }
+  }
+  // block-wide inclusive prefix scan of (g, h) over the cells; the per-cell prefixes are rebuilt from
+  // the thread's exclusive base where needed (fewer live registers than keeping them)
+  int64_t tg = 0, th = 0;
+#pragma unroll
+  for (int k = 0; k < kEvalCPT; ++k) { tg += g[k]; th += h[k]; }
+  const int64_t ig = wave_incl_scan(tg), ih = wave_incl_scan(th);
+  if (lane == kWave - 1) { s_wg[wv] = ig; s_wh[wv] = ih; }
+  __syncthreads();
+  int64_t bg = ig - tg, bh = ih - th;  // exclusive within the wave
+  for (int k = 0; k < wv; ++k) { bg += s_wg[k]; bh += s_wh[k]; }
+  // segment bases: the exclusive prefix at each feature's first cell, and the grand total
+  {
+    int f = f0;
+    int64_t rg = bg, rh = bh;
+#pragma unroll
+    for (int k = 0; k < kEvalCPT; ++k) {
+      const int c = c0 + k;
+      while (f + 1 < F && s_hoff[f + 1] <= c) ++f;
+      if (k < cpt && c < nc && c == s_hoff[f]) { s_bg[f] = rg; s_bh[f] = rh; }
+      rg += g[k];
+      rh += h[k];
+      if (k < cpt && c == nc - 1) { s_bg[F] = rg; s_bh[F] = rh; }
+    }
+  }
+  __syncthreads();
+  stamp_.probe(2);
+  const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
+  const double parent_gain = calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw);
+  Cand best;
+  best.gain = -INFINITY;
+  best.key = 0x7fffffff;
+  best.gl = 0;
+  best.hl = 0;
+  float best_cut = -FLT_MAX;
+  {
+    int f = f0;
+    int64_t rg = bg, rh = bh;  // global inclusive prefix of the current cell
+#pragma unroll
+    for (int k = 0; k < kEvalCPT; ++k) {
+      const int c = c0 + k;
+      rg += g[k];
+      rh += h[k];
+      while (f + 1 < F && s_hoff[f + 1] <= c) ++f;
+      if (k >= cpt || c >= nc || !s_on[f]) continue;
+      const int b = c - s_hoff[f];
+      const int nb = s_nb[f];
+      const int64_t GLi = rg - s_bg[f], HLi = rh - s_bh[f];
+      const int64_t mg = G - (s_bg[f + 1] - s_bg[f]), mh = H - (s_bh[f + 1] - s_bh[f]);
+      // direction 0: missing -> right, left = bins <= b
+      {
+        const double gl = (double)GLi * d.ginv, hl = (double)HLi * d.hinv;
+        const double gr = (double)(G - GLi) * d.ginv, hr = (double)(H - HLi) * d.hinv;
+        if (hl >= d.mcw && hr >= d.mcw) {
+          Cand cd;
+          cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+          cd.key = f * 1024 + b;
+          cd.gl = GLi;
+          cd.hl = HLi;
+          if (cand_better(cd, best)) { best = cd; best_cut = cut[k]; }
+        }
+      }
+      // direction 1: missing -> left, left = bins <= b-1 (+ missing)
+      if (mg != 0 || mh != 0) {
+        const int64_t GL = GLi - g[k] + mg, HL = HLi - h[k] + mh;
+        const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
+        const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
+        if (hl >= d.mcw && hr >= d.mcw) {
+          Cand cd;
+          cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+          cd.key = f * 1024 + 512 + (nb - 1 - b);
+          cd.gl = GL;
+          cd.hl = HL;
+          if (cand_better(cd, best)) { best = cd; best_cut = b == 0 ? -FLT_MAX : (k == 0 ? cutm1 : cut[k - 1]); }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    Cand other = cand_shfl_xor(best, o);
+    const float ocut = __shfl_xor(best_cut, o, kWave);
+    if (cand_better(other, best)) { best = other; best_cut = ocut; }
+  }
+  if (lane == 0) { s_best[wv] = best; s_cut[wv] = best_cut; }
+  __syncthreads();
+  stamp_.probe(3);
+  if (t != 0) return;
+  for (int k = 1; k < kEvalThreads / kWave; ++k)
+    if (cand_better(s_best[k], best)) { best = s_best[k]; best_cut = s_cut[k]; }
+  const int wf = best.key != 0x7fffffff ? (best.key >> 10) : 0;
+  eval_finalize(d, level, n, G, H, best, best_cut, s_nb[wf]);
+  stamp_.probe(4);
+}
+
 // ------------------------------------------------------------------------------------------
 // Partition planning + row partition (K18) + leaf margin update (K19)
 // ------------------------------------------------------------------------------------------
@@ -1491,6 +1736,8 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
   const int entries = d.tile_entries[0] + kWave;  // + per-lane trash cells
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   const HistLanes hl = hist_lanes(d, tree, 0, F);
+  __shared__ int s_fo[kMaxFeatTile + 1], s_fs[kMaxFeatTile];
+  flush_meta_store(flush_meta_load(d, tree, 0, F), F, s_fo, s_fs);  // published by the barrier below
 
   // pass 1: row ids + split-feature bins -> directions and per-wave counts (rows stay in registers)
   const bool identity = parity == 0 && q == 0;
@@ -1572,7 +1819,7 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
     bl += __popcll(lm);
     br += __popcll(rm);
   }
-  hist_flush(d, s_hist, hl, item, 0, F, tg, th, true, s_tot);
+  hist_flush(d, s_hist, hl, item, 0, F, tg, th, true, s_tot, s_fo, s_fs);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1846,6 +2093,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   static const int env_fg = getenv("COBALT_EVAL_FG") ? atoi(getenv("COBALT_EVAL_FG")) : -1;
   int eval_fg = env_fg >= 0 ? env_fg : (d.F > 32 ? 8 : 0);
   if (eval_fg > 0) eval_fg = std::min(32, std::max(eval_fg, ceil_div(d.F, 64)));
+  // compact-cell evaluation for narrow data (COBALT_EVAL_COMPACT=1; default: the F x 256-slot k_eval)
+  // Opt-in: measured 14.2 vs 13.5 us per node-level at 1M rows and 106 vs 109 us per tree at 10M
+  // (the fp64 gain scan is not what bounds k_eval; its dependent LDS / shuffle / sync steps are).
+  const int env_compact = getenv("COBALT_EVAL_COMPACT") ? atoi(getenv("COBALT_EVAL_COMPACT")) : 0;
+  const bool eval_compact = eval_fg == 0 && env_compact != 0 && d.F <= kEvalMaxF &&
+                            d.ncells <= kEvalThreads * kEvalCPT;
   // rows in flight per thread in the gradient + root histogram pass (COBALT_GRAD_U=4: +1%, within noise)
   static const int grad_u = getenv("COBALT_GRAD_U") ? atoi(getenv("COBALT_GRAD_U")) : 2;
   // partition fused with the next level's histogram (same record-layout conditions); opt-in while it
@@ -1916,6 +2169,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         GLAUNCH("k_eval", k_eval<true>, dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d, level,
                 parity, t, eval_fg);
         GLAUNCH("k_eval_finish", k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
+      } else if (eval_compact) {
+        GLAUNCH("k_eval", k_eval_compact, dim3(1 << level), dim3(kEvalThreads), 0, stream, d, level, parity, t);
       } else {
         GLAUNCH("k_eval", k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
       }

@@ -356,6 +356,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                 segment_done(seg_nodes, s1)
         finally:
             tr.close()
+        rep.extra["margin"] = margin  # training margins incl. every tree (device tensor)
     else:
         cuts_np = bd.cuts.cpu().numpy()
         nb_np = bd.nbins.cpu().numpy()

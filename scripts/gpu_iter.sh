@@ -1,0 +1,11 @@
+#!/bin/bash
+# One trainer iteration on the GPU box: GBDT GPU tests, 1M / 10M benches, in-kernel stamps.
+# usage: gpu_iter.sh [pytest-selection...]
+set -o pipefail
+S=scripts/gpu_step.sh
+sel=${@:-tests/test_gpu_gbdt.py}
+bash $S iter_tests 500 python -u -m pytest $sel -x -q --timeout 600 --timeout-method thread || exit $?
+bash $S iter_bench1m 200 python bench.py --rows 1000000 --steps 3 --warmup 1 || exit $?
+bash $S iter_bench10m 300 python bench.py --steps 3 --warmup 1 || exit $?
+bash scripts/gpu_stamps.sh || exit $?
+grep -h "^{" gpurun_out/iter_bench*.log | cut -c1-220

@@ -65,6 +65,35 @@ def test_gpu_trees_identical_to_host_oracle(kw):
         assert np.array_equal(tg.sum_hessian, tc.sum_hessian)
 
 
+@pytest.mark.timeout(600)
+def test_gpu_large_n_kernel_shapes_identical_to_host_oracle():
+    """Above 4M rows the trainer switches kernel shapes (k_partition<4>, 8192-row root items,
+    16384-row work chunks -- the headline 10M-row configuration). Two depth-7 trees on 4.3M rows
+    must equal the NumPy oracle's byte for byte, and the training margins must equal the predictor's."""
+    n = 4_300_000
+    X, y = synth.make_lendingclub(n, seed=31)
+    spw = float((y == 0).sum() / (y == 1).sum())
+    p = gbdt.GBDTParams(n_estimators=2, max_depth=7, learning_rate=0.3, gamma=1.0, scale_pos_weight=spw,
+                        random_state=78)
+    rep = gbdt.FitReport()
+    bg = gbdt.train(X.cuda(), y.cuda(), p, device="cuda", report=rep)
+    bc = gbdt.train(X, y, p, device="cpu")
+    assert bg.save_raw("ubj") == bc.save_raw("ubj")
+    mg = bg.predict_margin(X.cuda())
+    assert torch.equal(rep.extra["margin"], mg)
+
+
+@pytest.mark.timeout(300)
+def test_gpu_10m_training_margins_equal_predictor():
+    """The headline shapes (10M rows, depth 7): the margins the trainer keeps for its gradients are
+    exactly what the predictor computes from the fetched trees."""
+    X, y = synth.make_lendingclub(10_000_000, seed=0, device="cuda")
+    rep = gbdt.FitReport()
+    b = gbdt.train(X, y, gbdt.GBDTParams(n_estimators=5, max_depth=7, learning_rate=0.05, gamma=5.0,
+                                         scale_pos_weight=6.7), device="cuda", report=rep)
+    assert torch.equal(rep.extra["margin"], b.predict_margin(X))
+
+
 def test_gpu_training_margin_consistent_with_predictor():
     X, y = _data(20_000, seed=2)
     b = gbdt.train(X, y, gbdt.GBDTParams(n_estimators=10, max_depth=6), device="cuda")
@@ -273,3 +302,13 @@ def test_concurrent_search_fits_equal_sequential():
     one = search._fold_scores(X, y, folds, base, cands, "cuda", streams=1)
     four = search._fold_scores(X, y, folds, base, cands, "cuda", streams=4)
     assert np.array_equal(one, four)
+
+
+def test_gpu_compact_eval_identical_to_host_oracle(monkeypatch):
+    """The opt-in compact-cell split evaluator (COBALT_EVAL_COMPACT=1, k_eval_compact) grows the same
+    trees as the host oracle (and hence as the default F x 256-slot k_eval)."""
+    monkeypatch.setenv("COBALT_EVAL_COMPACT", "1")
+    X, y = _data(50_000, seed=4)
+    p = gbdt.GBDTParams(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9,
+                        colsample_bytree=0.7, reg_alpha=0.2, scale_pos_weight=6.0, random_state=3)
+    assert gbdt.train(X, y, p, device="cuda").save_raw("ubj") == gbdt.train(X, y, p, device="cpu").save_raw("ubj")
