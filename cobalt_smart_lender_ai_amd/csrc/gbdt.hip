@@ -5,7 +5,8 @@
 // notebooks/04_model_training.ipynb:1877-2016).
 //
 // Design (MI355X-first, not a translation of XGBoost's CPU/CUDA code):
-//  * Features are pre-quantised to uint8 bins (255 real bins + 255 = missing), stored twice:
+//  * Features are pre-quantised to uint8 bins (<= 255 real bins + code 255 = missing; 256 real bins
+//    for a feature without missing values, see HistLanes.fullbits), stored twice:
 //    row-major [N][stride] for histogram gathers (one row = a few dwords) and feature-major
 //    [F][N] for the partition step (one byte per row, coalesced within a node).
 //  * Gradients are quantised to fixed point and packed into one u64 per row
@@ -92,7 +93,7 @@ struct GbdtConfig {
   int32_t chunk;         // rows per histogram / partition work item (<= 16384)
   int32_t feat_tile;     // features per histogram block (multiple of 4)
   double eta, lambda_, alpha, gamma, min_child_weight, subsample;
-  double gscale, hscale; // g_q = rint(g * gscale), h_q = rint(h * hscale)
+  double gscale, hscale; // g_q = floor(g * gscale + u), h_q = floor(h * hscale + u) (quantize_gh)
   float base_margin;
   int32_t world_size;
   uint64_t seed;
@@ -220,6 +221,29 @@ __global__ __launch_bounds__(256) void k_bin(const float* __restrict__ X, int64_
 // ------------------------------------------------------------------------------------------
 // Per-tree initialisation + binary:logistic gradients (K14)
 // ------------------------------------------------------------------------------------------
+// Gradient fixed point (models/gbdt_host.py gradients_host is the oracle): |g| <= w_max and
+// h <= w_max / 4 are scaled to 17 bits and rounded UNBIASED, q = floor(x * scale + u) with u ~ U[0,1)
+// drawn from a per-(tree, global row) hash -- E[q] = x * scale, so small hessians are not flushed
+// to 0 and rounding errors of histogram sums average out instead of accumulating a bias. The draw is
+// deterministic (same trees on every device and rank count). Bounds: a <= 16384-row histogram block
+// sums to |sum g| < 2^31 and sum h <= 2^31, so the packed u64 (signed g high, h low) never carries.
+constexpr int64_t kGClip = (1 << 17) - 1, kHClip = 1 << 17;
+constexpr uint64_t kDitherSalt = 0xD1B54A32D192ED03ull;
+
+__device__ __forceinline__ uint64_t tree_key_of(uint64_t seed, int tree) {
+  return splitmix64(seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
+}
+
+__device__ __forceinline__ void quantize_gh(double g, double h, double gscale, double hscale, uint64_t dkey,
+                                            int64_t grow, int64_t& gq, int64_t& hq) {
+  const uint64_t r = splitmix64(dkey ^ (uint64_t)grow);
+  const double ug = (double)(uint32_t)(r >> 32) * (1.0 / 4294967296.0);
+  const double uh = (double)(uint32_t)r * (1.0 / 4294967296.0);
+  gq = (int64_t)floor(g * gscale + ug);
+  hq = (int64_t)floor(h * hscale + uh);
+  gq = gq > kGClip ? kGClip : (gq < -kGClip ? -kGClip : gq);
+  hq = hq > kHClip ? kHClip : (hq < 0 ? 0 : hq);
+}
 // Reset the node table of a new tree (root active with all local rows) and the per-node counters.
 __device__ void init_tree_block(const GbdtDev& d) {
   for (int i = threadIdx.x; i < d.max_nodes; i += blockDim.x) {
@@ -291,7 +315,8 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
     __syncthreads();
   }
   if (blockIdx.x == 0) init_tree_block(d);  // the new tree's node table (no other block reads it)
-  const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
+  const uint64_t tree_key = tree_key_of(d.seed, tree);
+  const uint64_t dkey = splitmix64(tree_key ^ kDitherSalt);
   const bool rec32 = d.stride == 32 && d.F <= 24;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -331,10 +356,8 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
       const uint64_t hsh = splitmix64(tree_key ^ (uint64_t)(d.row_offset + i));
       if (!(uniform01(hsh) < d.subsample)) { g = 0.0; h = 0.0; }
     }
-    int64_t gq = (int64_t)rint(g * d.gscale);
-    int64_t hq = (int64_t)rint(h * d.hscale);
-    gq = gq > 65536 ? 65536 : (gq < -65536 ? -65536 : gq);
-    hq = hq > 65536 ? 65536 : (hq < 0 ? 0 : hq);
+    int64_t gq, hq;
+    quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq);
     if (rec32) {
       rb.z = (uint32_t)hq;
       rb.w = (uint32_t)(int32_t)gq;
@@ -611,6 +634,7 @@ __device__ void publish_level(const GbdtDev& d, int level, int total, bool keep_
 // LDS histogram helpers shared by k_hist and k_grad_hist (32-byte record fast path).
 struct HistLanes {
   uint64_t fbits;                 // colsample mask of the tile's features
+  uint64_t fullbits;              // 256-bin features (no missing values): code 255 is a real bin
   uint32_t sh0, sh1, sh2, sh3;    // 3-bit copy shifts per feature, 8 features per word (SGPRs)
   uint32_t trash;                 // per-lane trash cell (missing values, disabled features)
   uint32_t lane;
@@ -622,7 +646,7 @@ struct HistLanes {
 // The loads are split from the ballots (hist_lanes_load / hist_lanes_finish) so a kernel can issue
 // them together with its other independent loads (work plan, flush offsets): one round trip for all.
 struct HistLaneRaw {
-  bool on;
+  bool on, full;
   int sh;
 };
 
@@ -632,7 +656,9 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   const int f = f0 + (in ? lane : 0);
   HistLaneRaw r;
   r.on = in && d.fmask[(int64_t)tree * d.F + f] != 0;
-  r.sh = in ? (d.layout[f].y & 7) : 0;
+  const int ly = in ? d.layout[f].y : 0;
+  r.sh = ly & 7;
+  r.full = (ly & 8) != 0;
   return r;
 }
 
@@ -643,6 +669,7 @@ __device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, i
   const bool on = raw.on;
   const int sh = raw.sh;
   hl.fbits = __ballot(on);
+  hl.fullbits = __ballot(raw.full);
   const uint64_t b0 = __ballot(in && (sh & 1)), b1 = __ballot(in && (sh & 2)), b2 = __ballot(in && (sh & 4));
   hl.sh0 = hl.sh1 = hl.sh2 = hl.sh3 = 0;
   for (int fl = 0; fl < ft; ++fl) {
@@ -672,7 +699,8 @@ __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes
       const int q = fl >> 2;
       const uint32_t word = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : b.y;
       const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
-      const uint32_t cell = (bb != kMissingBin && fen) ? cbase + (bb << sh) : hl.trash;
+      const bool real = bb != kMissingBin || ((hl.fullbits >> fl) & 1ull);
+      const uint32_t cell = (real && fen) ? cbase + (bb << sh) : hl.trash;
       atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp);
     }
   }
@@ -695,7 +723,7 @@ __device__ __forceinline__ FlushMeta flush_meta_load(const GbdtDev& d, int tree,
   FlushMeta m{0, -1};
   const int t = threadIdx.x;
   if (t <= ft) m.fo = d.hoff[f0 + t];
-  if (t < ft) m.fs = d.fmask[(int64_t)tree * d.F + f0 + t] != 0 ? d.layout[f0 + t].y : -1;
+  if (t < ft) m.fs = d.fmask[(int64_t)tree * d.F + f0 + t] != 0 ? (d.layout[f0 + t].y & 7) : -1;
   return m;
 }
 
@@ -790,7 +818,8 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
     d.items_h[item] = w;
   }
   const HistLanes hl = hist_lanes_finish(lraw, ft);
-  const uint64_t tree_key = splitmix64(d.seed ^ (0xA5A5A5A5ull + (uint64_t)tree * 0x632BE59BD9B4E019ull));
+  const uint64_t tree_key = tree_key_of(d.seed, tree);
+  const uint64_t dkey = splitmix64(tree_key ^ kDitherSalt);
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
   for (int64_t i0 = begin + threadIdx.x; i0 < end; i0 += U * B) {
@@ -836,10 +865,8 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
         const uint64_t hsh = splitmix64(tree_key ^ (uint64_t)(d.row_offset + i));
         if (!(uniform01(hsh) < d.subsample)) { g = 0.0; h = 0.0; }
       }
-      int64_t gq = (int64_t)rint(g * d.gscale);
-      int64_t hq = (int64_t)rint(h * d.hscale);
-      gq = gq > 65536 ? 65536 : (gq < -65536 ? -65536 : gq);
-      hq = hq > 65536 ? 65536 : (hq < 0 ? 0 : hq);
+      int64_t gq, hq;
+      quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq);
       rb[u].z = (uint32_t)hq;
       rb[u].w = (uint32_t)(int32_t)gq;
       reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
@@ -960,6 +987,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
       }
       const uint32_t shc = c == 0 ? sh0 : (c == 1 ? sh1 : (c == 2 ? sh2 : sh3));
       const uint32_t fbc = (uint32_t)(fbits >> (c * 8)) & 0xFFu;
+      const uint32_t flc = (uint32_t)(hl.fullbits >> (c * 8)) & 0xFFu;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         if ((fbc >> k) & 1u) {
@@ -969,7 +997,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
           for (int u = 0; u < U; ++u) {
             // branch-free: missing values (and padded rows, gp == 0) add into a per-lane trash cell
             const uint32_t b = ((k < 4 ? lo[u] : hi[u]) >> (8 * (k & 3))) & 0xffu;
-            const uint32_t cell = b != kMissingBin ? cbase + (b << sh) : trash;
+            const uint32_t cell = (b != kMissingBin || ((flc >> k) & 1u)) ? cbase + (b << sh) : trash;
             if (d.ablate == 1) tg += cell; else
             atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp[u]);
           }
@@ -2040,10 +2068,11 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   for (int t = 0; t < ntiles; ++t) {
     int off = 0;
     for (int f = t * ft; f < std::min(F, (t + 1) * ft); ++f) {
-      const int b = std::max(1, std::min(255, nb[f]));
+      const int b = std::max(1, std::min(256, nb[f]));
       int sh = 0;
       while (sh < 6 && (b << (sh + 1)) <= kMaxBins) ++sh;  // copies = 2^sh, nb * copies <= 256
-      lay[f] = make_int2((f - t * ft) * kMaxBins, sh);
+      // bit 3: a 256-bin feature (no missing values; code 255 is its real bin 255)
+      lay[f] = make_int2((f - t * ft) * kMaxBins, sh | (b >= 256 ? 8 : 0));
       off += kMaxBins;
     }
     ent[t] = off;
@@ -2051,7 +2080,7 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   }
   CK(hipMemcpy(c->d.layout, lay.data(), F * sizeof(int2), hipMemcpyHostToDevice));
   std::vector<int32_t> hoff(F + 1, 0);
-  for (int f = 0; f < F; ++f) hoff[f + 1] = hoff[f] + std::max(1, std::min(255, nb[f]));
+  for (int f = 0; f < F; ++f) hoff[f + 1] = hoff[f] + std::max(1, std::min(256, nb[f]));
   CK(hipMemcpy(c->d.hoff, hoff.data(), (F + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
   c->d.ncells = hoff[F];
   c->d.slot_elems = (int64_t)(hoff[F] + 1) * 2;

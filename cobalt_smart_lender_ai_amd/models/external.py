@@ -190,7 +190,7 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
     base_margin = Booster([], base_score=base_score, num_feature=F).base_margin
     wmax = float(w.max()) if N else 1.0
     # |g / p| and h / p are both <= max(|g|, h, mu) <= w_max once mu is capped at w_max
-    gscale = hscale = float(2 ** gbdt_host.QBITS) / wmax
+    gscale = hscale = float(2 ** 16) / wmax  # the page kernel clips at +-2^16 (k_ooc_page)
     T, D = int(params.n_estimators), int(params.max_depth)
     seed = int(params.random_state)
     fmask = feature_masks(T, F, float(params.colsample_bytree), seed)

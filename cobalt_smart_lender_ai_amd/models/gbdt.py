@@ -54,6 +54,12 @@ class GBDTParams:
     random_state: int = 0
     base_score: float | None = None
     sketch_rows: int = 1 << 18
+    # quantile-sketch weights: "sample" = the sample weights (XGBoost hist semantics, the reference's
+    # tree_method), "hessian" = first-round hessians (sample weight x scale_pos_weight for positives,
+    # XGBoost approx semantics); sketch_mode "summary" merges per-rank QuantileSummary objects
+    # instead of all-gathering the global sample (see models/sketch.py)
+    sketch_weight: str = "sample"
+    sketch_mode: str = "sample"
 
     @classmethod
     def from_kwargs(cls, **kw) -> "GBDTParams":
@@ -146,9 +152,46 @@ class BinnedData:
     t_bin: float = 0.0
 
 
+def _allreduce_max_flags(flags: torch.Tensor, dist, dev) -> torch.Tensor:
+    t = flags.to(torch.float32).to(dist._coll_device(dev))
+    dist.allreduce(t, "max")
+    return t.to(dev) > 0
+
+
+def _summary_cuts(samp: torch.Tensor, wsamp: torch.Tensor | None, max_bin: int, has_missing: torch.Tensor,
+                  dist, dev) -> tuple[torch.Tensor, torch.Tensor]:
+    """sketch_mode="summary": every rank summarises its own sample, the summaries are all-gathered
+    (a few KB per feature instead of the raw rows) and merged identically on every rank."""
+    summ = sketch.QuantileSummary.build(samp.cpu().numpy(), None if wsamp is None else wsamp.cpu().numpy())
+    off, vals, wts, _ = summ.to_arrays()
+    if dist is not None and dist.world > 1:
+        per = int(dist.allreduce_scalar(float(len(vals)), "max", dev))  # common padded length
+        ent = torch.full((per, 2), float("nan"), dtype=torch.float64)
+        ent[: len(vals), 0] = torch.from_numpy(vals.astype(np.float64))
+        ent[: len(vals), 1] = torch.from_numpy(wts.astype(np.float64))
+        offs = torch.from_numpy(off.astype(np.float64))[:, None]
+        all_ent = dist.allgather_rows(ent.to(dist._coll_device(dev))).cpu().numpy()
+        all_off = dist.allgather_rows(offs.to(dist._coll_device(dev))).cpu().numpy()[:, 0].astype(np.int64)
+        F1 = len(off)
+        parts = []
+        for r in range(dist.world):
+            o = all_off[r * F1:(r + 1) * F1]
+            e = all_ent[r * per:r * per + int(o[-1])]
+            parts.append(sketch.QuantileSummary.from_arrays(o, e[:, 0].astype(np.float32), e[:, 1].astype(np.int64),
+                                                            np.zeros(F1 - 1, dtype=bool)))
+        summ = sketch.QuantileSummary.merge(parts)
+    summ.has_missing = has_missing.cpu().numpy().astype(bool)
+    c, nb = summ.cuts(max_bin)
+    return torch.from_numpy(c).to(dev), torch.from_numpy(nb).to(dev)
+
+
 def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int = 1 << 18, device=None, dist=None,
-                n_rows_global: int | None = None, row_offset: int = 0) -> BinnedData:
-    """Quantile sketch (K12) on a global strided sample + binning (K13)."""
+                n_rows_global: int | None = None, row_offset: int = 0, sketch_weights=None,
+                sketch_mode: str = "sample") -> BinnedData:
+    """Weighted quantile sketch (K12) on a global strided sample + binning (K13).
+
+    ``sketch_weights`` ([N_local], optional): per-row sketch weights (see models/sketch.py).
+    A feature gets 256 bins only if it has no missing value in the FULL data (all ranks)."""
     dev = _resolve_device(device, X)
     world = dist.world if dist is not None else 1
     Xt = _to_tensor(X, dev)
@@ -156,11 +199,22 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int = 1 << 18, device=Non
     n_glob = n_rows_global if n_rows_global is not None else (
         int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
     ts = time.perf_counter()
+    has_missing = torch.isnan(Xt).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
+    if world > 1:
+        has_missing = _allreduce_max_flags(has_missing, dist, dev)
     stride = sketch.sample_stride(n_glob, sketch_rows)
     samp = sketch.local_sample(Xt, row_offset, stride)
-    if world > 1:
-        samp = dist.allgather_rows(samp)
-    cuts, nbins = sketch.compute_cuts(samp, max_bin)
+    wsamp = None
+    if sketch_weights is not None:
+        wsamp = sketch.local_sample(_to_tensor(sketch_weights, dev).reshape(-1, 1), row_offset, stride)[:, 0]
+    if sketch_mode == "summary":
+        cuts, nbins = _summary_cuts(samp, wsamp, max_bin, has_missing, dist, dev)
+    else:
+        if world > 1:
+            samp = dist.allgather_rows(samp)
+            if wsamp is not None:
+                wsamp = dist.allgather_rows(wsamp.reshape(-1, 1), pad_value=0.0)[:, 0]
+        cuts, nbins = sketch.compute_cuts(samp, max_bin, wsamp, has_missing)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t_sketch = time.perf_counter() - ts
@@ -175,6 +229,19 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int = 1 << 18, device=Non
         bd.bins_host = sketch.bin_matrix_host(Xt.cpu().numpy(), cuts.cpu().numpy(), nbins.cpu().numpy())
     bd.t_bin = time.perf_counter() - tb
     return bd
+
+
+def sketch_weights_for(params: "GBDTParams", y, sample_weight=None, device=None):
+    """Per-row sketch weights for ``params.sketch_weight`` (None = unweighted)."""
+    mode = getattr(params, "sketch_weight", "sample")
+    if mode == "sample":
+        return sample_weight
+    if mode != "hessian":
+        raise ValueError(f"sketch_weight must be 'sample' or 'hessian', got {mode!r}")
+    yt = _to_tensor(y, device).reshape(-1)
+    w = _to_tensor(sample_weight, device).reshape(-1) if sample_weight is not None else torch.ones_like(yt)
+    spw = float(params.scale_pos_weight if params.scale_pos_weight is not None else 1.0)
+    return w * torch.where(yt == 1.0, torch.tensor(spw, device=yt.device), torch.tensor(1.0, device=yt.device))
 
 
 def subset_rows(bd: BinnedData, rows: np.ndarray) -> BinnedData:
@@ -193,7 +260,8 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
           feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
           dist=None, n_rows_global: int | None = None, row_offset: int = 0,
           report: FitReport | None = None, init_booster: Booster | None = None,
-          checkpoint_path: str | None = None, checkpoint_every: int = 0, resume: bool = True) -> Booster:
+          checkpoint_path: str | None = None, checkpoint_every: int = 0, resume: bool = True,
+          exact_fp64: bool = False) -> Booster:
     """Fit a binary:logistic GBDT. With ``dist`` (a :class:`~..parallel.dist.DistContext`) each rank
     passes its local row shard (``row_offset`` = global index of its first row).
 
@@ -201,7 +269,10 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
     (XGBoost's ``xgb_model=``). ``checkpoint_path`` + ``checkpoint_every`` write the model every that
     many trees (atomic replace, rank 0); with ``resume`` an existing checkpoint there is loaded and
     training continues to ``n_estimators`` trees in total -- bit-identical to an uninterrupted fit,
-    because sampling is keyed by the global tree index and the margins are re-predicted in tree order."""
+    because sampling is keyed by the global tree index and the margins are re-predicted in tree order.
+
+    ``exact_fp64`` (CPU only): unquantised fp64 gradients and histograms -- the accuracy reference of
+    the fixed-point trainer (tests/test_quantization.py)."""
     if params is None:
         params = GBDTParams()
     elif isinstance(params, dict):
@@ -225,10 +296,12 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
             init_margin = torch.as_tensor(init_margin)
         init_margin = init_margin.to(dev, torch.float32).contiguous()
     bd = bin_dataset(X, max_bin=params.max_bin, sketch_rows=params.sketch_rows, device=device, dist=dist,
-                     n_rows_global=n_rows_global, row_offset=row_offset)
+                     n_rows_global=n_rows_global, row_offset=row_offset,
+                     sketch_weights=sketch_weights_for(params, y, sample_weight, dev),
+                     sketch_mode=params.sketch_mode)
     bst = train_binned(bd, y, params, sample_weight=sample_weight, feature_names=feature_names,
                        feature_types=feature_types, dist=dist, report=report, init_booster=init_booster,
-                       init_margin=init_margin, total_trees=total, checkpoint=ckpt)
+                       init_margin=init_margin, total_trees=total, checkpoint=ckpt, exact_fp64=exact_fp64)
     if report is not None:
         report.t_total = time.perf_counter() - t0
     return bst
@@ -238,7 +311,8 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                  feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
                  feature_mask: np.ndarray | None = None, dist=None, report: FitReport | None = None,
                  init_booster: Booster | None = None, init_margin: torch.Tensor | None = None,
-                 total_trees: int | None = None, checkpoint: "Checkpointer | None" = None) -> Booster:
+                 total_trees: int | None = None, checkpoint: "Checkpointer | None" = None,
+                 exact_fp64: bool = False) -> Booster:
     """Boost on pre-binned data. ``feature_mask`` (bool [F]) restricts the fit to a feature subset
     (the trees still index the full feature space, so a subset fit costs no re-binning).
     ``init_booster`` + ``init_margin`` (its margins on these rows) continue an existing model: grow
@@ -322,7 +396,10 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                                   reg_lambda=float(params.reg_lambda), reg_alpha=float(params.reg_alpha),
                                   gamma=float(params.gamma), min_child_weight=float(params.min_child_weight),
                                   subsample=float(params.subsample), seed=int(params.random_state),
-                                  gscale=gscale, hscale=hscale)
+                                  gscale=1.0 if exact_fp64 else gscale, hscale=1.0 if exact_fp64 else hscale,
+                                  quant=not exact_fp64)
+    if exact_fp64 and dev.type != "cpu":
+        raise ValueError("exact_fp64 is the host (CPU) reference trainer")
     tp = rep.mark("labels_weights", tp, dev)
     tb = time.perf_counter()
     if dev.type == "cuda":
@@ -475,12 +552,13 @@ class GBDTClassifier:
     _param_names = ["n_estimators", "max_depth", "learning_rate", "gamma", "min_child_weight", "reg_lambda",
                     "reg_alpha", "subsample", "colsample_bytree", "max_bin", "scale_pos_weight", "random_state",
                     "base_score", "eval_metric", "use_label_encoder", "device", "importance_type", "n_jobs",
-                    "sketch_rows"]
+                    "sketch_rows", "sketch_weight"]
 
     def __init__(self, n_estimators=None, max_depth=None, learning_rate=None, gamma=None, min_child_weight=None,
                  reg_lambda=None, reg_alpha=None, subsample=None, colsample_bytree=None, max_bin=None,
                  scale_pos_weight=None, random_state=None, base_score=None, eval_metric=None,
-                 use_label_encoder=None, device=None, importance_type=None, n_jobs=None, sketch_rows=None):
+                 use_label_encoder=None, device=None, importance_type=None, n_jobs=None, sketch_rows=None,
+                 sketch_weight=None):
         self.n_estimators = n_estimators
         self.max_depth = max_depth
         self.learning_rate = learning_rate
@@ -500,6 +578,7 @@ class GBDTClassifier:
         self.importance_type = importance_type
         self.n_jobs = n_jobs
         self.sketch_rows = sketch_rows
+        self.sketch_weight = sketch_weight
 
     # sklearn protocol
     def get_params(self, deep: bool = True) -> dict[str, Any]:

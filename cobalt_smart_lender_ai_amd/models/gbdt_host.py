@@ -25,7 +25,9 @@ from .booster import NODE_DTYPE
 
 FLT_MAX = np.float32(np.finfo(np.float32).max)
 MASK64 = (1 << 64) - 1
-QBITS = 16          # |g_q| <= 2^16, h_q <= 2^16 (see GbdtConfig quantisation in ops/gbdt_ops.py)
+QBITS = 17          # |g_q| < 2^17, h_q <= 2^17: a <= 16384-row histogram block sums to < 2^31
+G_CLIP = (1 << QBITS) - 1
+H_CLIP = 1 << QBITS
 
 
 def splitmix64_np(x: np.ndarray) -> np.ndarray:
@@ -48,6 +50,19 @@ def tree_key(seed: int, tree: int) -> int:
     return splitmix64_int((seed ^ ((0xA5A5A5A5 + tree * 0x632BE59BD9B4E019) & MASK64)) & MASK64)
 
 
+def dither_key(seed: int, tree: int) -> int:
+    """Per-tree key of the gradient quantiser's dither (csrc/gbdt.hip quantize_gh)."""
+    return splitmix64_int((tree_key(seed, tree) ^ 0xD1B54A32D192ED03) & MASK64)
+
+
+def dither_uniforms(seed: int, tree: int, global_rows: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Two independent U[0,1) per row (high / low 32 bits of one splitmix64 draw)."""
+    hsh = splitmix64_np(np.uint64(dither_key(seed, tree)) ^ global_rows.astype(np.uint64))
+    ug = (hsh >> np.uint64(32)).astype(np.float64) * (1.0 / 4294967296.0)
+    uh = (hsh & np.uint64(0xFFFFFFFF)).astype(np.float64) * (1.0 / 4294967296.0)
+    return ug, uh
+
+
 def row_sample_mask(seed: int, tree: int, global_rows: np.ndarray, rate: float) -> np.ndarray:
     h = splitmix64_np(np.uint64(tree_key(seed, tree)) ^ global_rows.astype(np.uint64))
     u = (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
@@ -66,11 +81,13 @@ class HostGbdtParams:
     seed: int
     gscale: float
     hscale: float
+    quant: bool = True   # False: unquantised fp64 gradients and histograms (accuracy reference)
 
 
 def quant_scales(w_max: float) -> tuple[float, float]:
-    """Fixed-point scales: |g| <= w and h <= w/4, so both quantised magnitudes stay <= 2^16 and a
-    16384-row histogram block sums to < 2^30 (packed-u64 LDS accumulation on the GPU)."""
+    """Fixed-point scales: |g| <= w and h <= w/4, so both quantised magnitudes stay <= 2^17 and a
+    16384-row histogram block sums to < 2^31 -- the packed-u64 LDS accumulation on the GPU keeps h in
+    the low 32 bits (no carry into g) and g as a signed 32-bit high half."""
     w_max = float(w_max) if w_max > 0 else 1.0
     return float(2 ** QBITS) / w_max, float(2 ** (QBITS + 2)) / w_max
 
@@ -103,25 +120,36 @@ def gradients_host(margin: np.ndarray, label: np.ndarray, weight: np.ndarray, p:
         keep = row_sample_mask(p.seed, tree, row_offset + np.arange(len(m), dtype=np.int64), p.subsample)
         g = np.where(keep, g, 0.0)
         h = np.where(keep, h, 0.0)
-    gq = np.clip(np.rint(g * p.gscale), -65536, 65536).astype(np.int64)
-    hq = np.clip(np.rint(h * p.hscale), 0, 65536).astype(np.int64)
+    if not p.quant:
+        return g, h
+    # unbiased fixed point: floor(x * scale + u), u ~ U[0,1) from a per-(tree, global row) hash, so
+    # E[q] = x * scale exactly -- small hessians are not flushed to 0 and the rounding error of a sum
+    # averages out instead of accumulating a bias; deterministic (same on every device / rank count)
+    ug, uh = dither_uniforms(p.seed, tree, row_offset + np.arange(len(m), dtype=np.int64))
+    gq = np.clip(np.floor(g * p.gscale + ug), -G_CLIP, G_CLIP).astype(np.int64)
+    hq = np.clip(np.floor(h * p.hscale + uh), 0, H_CLIP).astype(np.int64)
     return gq, hq
 
 
-def _node_hist(bins, rows, gq, hq, fmask) -> np.ndarray:
+def _node_hist(bins, rows, gq, hq, fmask, nbins=None) -> np.ndarray:
+    """Histogram of one node. Code 255 is the missing bin, except for 256-bin features (no missing
+    values), where it is the real bin 255."""
     F = bins.shape[1]
-    out = np.zeros((F + 1, 256, 2), dtype=np.int64)
+    dt = np.int64 if np.issubdtype(gq.dtype, np.integer) else np.float64
+    out = np.zeros((F + 1, 256, 2), dtype=dt)
     g = gq[rows]
     h = hq[rows]
     for f in range(F):
         if not fmask[f]:
             continue
         b = bins[rows, f].astype(np.int64)
-        m = b != 255
-        out[f, :, 0] = np.bincount(b[m], weights=g[m].astype(np.float64), minlength=256)[:256].astype(np.int64)
-        out[f, :, 1] = np.bincount(b[m], weights=h[m].astype(np.float64), minlength=256)[:256].astype(np.int64)
-    out[F, 0, 0] = int(g.sum())
-    out[F, 0, 1] = int(h.sum())
+        m = (b != 255) | (nbins is not None and int(nbins[f]) >= 256)
+        out[f, :, 0] = np.bincount(b[m], weights=g[m].astype(np.float64), minlength=256)[:256].astype(dt)
+        out[f, :, 1] = np.bincount(b[m], weights=h[m].astype(np.float64), minlength=256)[:256].astype(dt)
+        if F < 255:  # rows with a missing value of f (exact counts; survive the subtraction trick)
+            out[F, 1 + f, 0] = len(m) - int(np.count_nonzero(m))
+    out[F, 0, 0] = g.sum()
+    out[F, 0, 1] = h.sum()
     return out
 
 
@@ -138,10 +166,12 @@ def _eval_node(hist, G, H, nbins, fmask, p: HostGbdtParams):
         nb = int(nbins[f])
         hg, hh = hist[f, :, 0], hist[f, :, 1]
         cg, ch = np.cumsum(hg), np.cumsum(hh)
-        mg, mh = G - int(cg[-1]), H - int(ch[-1])
+        mg, mh = G - cg[-1].item(), H - ch[-1].item()
         b = np.arange(nb)
         cands = [(cg[:nb], ch[:nb], f * 1024 + b)]
-        if mg != 0 or mh != 0:
+        # fp64 mode: G - sum(bins) is not exactly 0 without missing values, so use the missing count
+        has_missing = mg != 0 or mh != 0 if p.quant else (F >= 255 or hist[F, 1 + f, 0] > 0)
+        if has_missing:
             cands.append((cg[:nb] - hg[:nb] + mg, ch[:nb] - hh[:nb] + mh, f * 1024 + 512 + (nb - 1 - b)))
         for GL, HL, key in cands:
             gl = GL.astype(np.float64) * ginv
@@ -160,7 +190,7 @@ def _eval_node(hist, G, H, nbins, fmask, p: HostGbdtParams):
             sel = np.nonzero(gain == mx)[0]
             i = sel[np.argmin(key[sel])]
             if mx > best_gain or (mx == best_gain and key[i] < best_key):
-                best_gain, best_key, best_gl, best_hl = float(mx), int(key[i]), int(GL[i]), int(HL[i])
+                best_gain, best_key, best_gl, best_hl = float(mx), int(key[i]), GL[i].item(), HL[i].item()
     if best_key == np.iinfo(np.int32).max:
         return None, Gd, Hd
     return (best_gain, best_key, best_gl, best_hl), Gd, Hd
@@ -182,6 +212,7 @@ def grow_tree_host(bins: np.ndarray, cuts: np.ndarray, nbins: np.ndarray, gq: np
     nodes[0]["status"] = 1
     nodes[0]["build"] = 1
     nodes[0]["count"] = N
+    GH = np.zeros((max_nodes, 2), dtype=np.int64 if p.quant else np.float64)  # node (G, H) sums
     rows: dict[int, np.ndarray] = {0: np.arange(N, dtype=np.int64)}
     hist_prev: dict[int, np.ndarray] = {}
     for level in range(D + 1):
@@ -192,7 +223,7 @@ def grow_tree_host(bins: np.ndarray, cuts: np.ndarray, nbins: np.ndarray, gq: np
                 if nodes[q]["status"] != 2:
                     continue
                 L, R = 2 * q + 1, 2 * q + 2
-                left_small = nodes[L]["H"] <= nodes[R]["H"]
+                left_small = GH[L, 1] <= GH[R, 1]
                 nodes[L]["build"] = 1 if left_small else 0
                 nodes[R]["build"] = 0 if left_small else 1
         hist_cur: dict[int, np.ndarray] = {}
@@ -201,10 +232,10 @@ def grow_tree_host(bins: np.ndarray, cuts: np.ndarray, nbins: np.ndarray, gq: np
             if level == 0:
                 built = [0]
             nslots = 1 if level == 0 else (1 << (level - 1))
-            slots = np.zeros((nslots, F + 1, 256, 2), dtype=np.int64)
+            slots = np.zeros((nslots, F + 1, 256, 2), dtype=GH.dtype)
             for n in built:
                 slot = 0 if level == 0 else ((n - first) >> 1)
-                slots[slot] = _node_hist(bins, rows.get(n, np.zeros(0, np.int64)), gq, hq, fmask)
+                slots[slot] = _node_hist(bins, rows.get(n, np.zeros(0, np.int64)), gq, hq, fmask, nbins)
             if allreduce is not None:
                 slots = allreduce(slots)
             for n in level_nodes:
@@ -217,13 +248,12 @@ def grow_tree_host(bins: np.ndarray, cuts: np.ndarray, nbins: np.ndarray, gq: np
                     par = (n - 1) // 2
                     hist_cur[n] = hist_prev[par] - slots[slot]
             if level == 0:
-                nodes[0]["G"] = int(hist_cur[0][F, 0, 0])
-                nodes[0]["H"] = int(hist_cur[0][F, 0, 1])
+                GH[0] = hist_cur[0][F, 0]
         for n in level_nodes:
             nd = nodes[n]
             if nd["status"] != 1:
                 continue
-            G, H = int(nd["G"]), int(nd["H"])
+            G, H = GH[n, 0].item(), GH[n, 1].item()
             if level < D:
                 best, Gd, Hd = _eval_node(hist_cur[n], G, H, nbins, fmask, p)
             else:
@@ -252,8 +282,9 @@ def grow_tree_host(bins: np.ndarray, cuts: np.ndarray, nbins: np.ndarray, gq: np
                 nodes[n]["split_cond"] = cuts[f, j] if j >= 0 else -FLT_MAX
                 nodes[n]["loss_chg"] = np.float32(gain)
                 L, R = 2 * n + 1, 2 * n + 2
-                nodes[L]["status"], nodes[L]["G"], nodes[L]["H"] = 1, GL, HL
-                nodes[R]["status"], nodes[R]["G"], nodes[R]["H"] = 1, G - GL, H - HL
+                nodes[L]["status"], nodes[R]["status"] = 1, 1
+                GH[L] = (GL, HL)
+                GH[R] = (G - GL, H - HL)
                 b = bins[r, f]
                 go_left = np.where(b == 255, dl == 1, b.astype(np.int64) <= j)
                 rows[L] = r[go_left]
@@ -268,4 +299,6 @@ def grow_tree_host(bins: np.ndarray, cuts: np.ndarray, nbins: np.ndarray, gq: np
                 if len(r):
                     margin[r] = (margin[r] + lv).astype(np.float32)
         hist_prev = hist_cur
+    if p.quant:
+        nodes["G"], nodes["H"] = GH[:, 0], GH[:, 1]
     return nodes

@@ -99,18 +99,25 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
     stride = sketch.sample_stride(n_glob, sketch_rows)
     F = None
     parts, seen = [], 0
+    miss = None  # per-feature NaN presence over the WHOLE stream (decides 255 vs 256 bins)
     for Xc, _ in source():
         Xc = _as_np(Xc, np.float32)
         F = Xc.shape[1] if F is None else F
         first = (-(row_offset + seen)) % stride
         parts.append(Xc[first::stride])
+        m = np.isnan(Xc).any(0)
+        miss = m if miss is None else (miss | m)
         seen += len(Xc)
     if seen != N:
         raise ValueError(f"the stream yielded {seen} rows, expected {N}")
     samp = torch.as_tensor(np.concatenate(parts) if parts else np.zeros((0, F or 0), np.float32), device=dev)
+    has_missing = torch.as_tensor(miss if miss is not None else np.zeros(F or 0, bool), device=dev)
     if world > 1:
         samp = dist.allgather_rows(samp)
-    cuts, nbins = sketch.compute_cuts(samp, max_bin)
+        hm = has_missing.to(torch.float32).to(dist._coll_device(dev))
+        dist.allreduce(hm, "max")
+        has_missing = hm.to(dev) > 0
+    cuts, nbins = sketch.compute_cuts(samp, max_bin, None, has_missing)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return cuts, nbins, N, n_glob, F

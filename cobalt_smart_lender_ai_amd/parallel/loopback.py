@@ -71,15 +71,19 @@ class LoopbackContext(DistContext):
 
 def run_ranks(world: int, fn: Callable[[LoopbackContext], Any], device: str | torch.device = "cuda:0",
               timeout: float = 600.0) -> list[Any]:
-    """Run ``fn(ctx)`` for ranks 0..world-1 concurrently (threads) and return their results."""
-    from .. import _native
-
-    lib = _native.lib()
+    """Run ``fn(ctx)`` for ranks 0..world-1 concurrently (threads) and return their results.
+    ``device="cpu"``: host-only ranks (no native communicator; the small collectives still meet)."""
     dev = torch.device(device)
+    gpu = dev.type == "cuda"
+    lib = None
     grp = ctypes.c_void_p()
-    rc = lib.cobalt_comm_loop_group(world, ctypes.byref(grp))
-    if rc:
-        raise RuntimeError(f"cobalt_comm_loop_group failed ({rc})")
+    if gpu:
+        from .. import _native
+
+        lib = _native.lib()
+        rc = lib.cobalt_comm_loop_group(world, ctypes.byref(grp))
+        if rc:
+            raise RuntimeError(f"cobalt_comm_loop_group failed ({rc})")
     pg = _Group(world, timeout)
     results: list[Any] = [None] * world
     errors: list[BaseException | None] = [None] * world
@@ -88,10 +92,13 @@ def run_ranks(world: int, fn: Callable[[LoopbackContext], Any], device: str | to
         h = ctypes.c_void_p()
         ctx = None
         try:
-            if lib.cobalt_comm_loop_rank(grp, r, ctypes.byref(h)):
+            if gpu and lib.cobalt_comm_loop_rank(grp, r, ctypes.byref(h)):
                 raise RuntimeError("cobalt_comm_loop_rank failed")
             ctx = LoopbackContext(rank=r, world=world, local_rank=dev.index or 0, backend="loopback",
-                                  native_comm=h.value, group=pg)
+                                  native_comm=h.value if gpu else None, group=pg)
+            if not gpu:
+                results[r] = fn(ctx)
+                return
             torch.cuda.set_device(dev)
             with torch.cuda.stream(torch.cuda.Stream(dev)):
                 results[r] = fn(ctx)
@@ -108,8 +115,9 @@ def run_ranks(world: int, fn: Callable[[LoopbackContext], Any], device: str | to
         t.start()
     for t in threads:
         t.join()
-    torch.cuda.synchronize(dev)
-    lib.cobalt_comm_loop_group_free(grp)
+    if gpu:
+        torch.cuda.synchronize(dev)
+        lib.cobalt_comm_loop_group_free(grp)
     failed = [e for e in errors if e is not None]
     if failed:  # the root cause first (peers fail with barrier / communicator errors after it)
         first = next((e for e in failed if not isinstance(e, threading.BrokenBarrierError)), failed[0])

@@ -312,3 +312,22 @@ def test_gpu_compact_eval_identical_to_host_oracle(monkeypatch):
     p = gbdt.GBDTParams(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9,
                         colsample_bytree=0.7, reg_alpha=0.2, scale_pos_weight=6.0, random_state=3)
     assert gbdt.train(X, y, p, device="cuda").save_raw("ubj") == gbdt.train(X, y, p, device="cpu").save_raw("ubj")
+
+
+@pytest.mark.timeout(900)
+def test_gpu_quantised_1000_trees_match_fp64_reference():
+    """1000 rounds at eta 0.3 (depth 6): the GPU's 17-bit dithered fixed-point trainer against the
+    unquantised fp64 host trainer -- held-out AUC within 0.002 (tests/test_quantization.py covers the
+    100-round RFE defaults on CPU)."""
+    from cobalt_smart_lender_ai_amd.metrics.auc import roc_auc
+
+    X, y = synth.make_lendingclub(70_000, seed=19)
+    Xtr, ytr, Xte, yte = X[:40_000], y[:40_000], X[40_000:], y[40_000:]
+    spw = float((ytr == 0).sum() / (ytr == 1).sum())
+    p = gbdt.GBDTParams(n_estimators=1000, max_depth=6, learning_rate=0.3, scale_pos_weight=spw, random_state=42)
+    bg = gbdt.train(Xtr, ytr, p, device="cuda")
+    bf = gbdt.train(Xtr.numpy(), ytr.numpy(), p, device="cpu", exact_fp64=True)
+    ag = roc_auc(yte, bg.predict_proba(Xte.cuda()).cpu())
+    af = roc_auc(yte, bf.predict_proba(Xte.numpy(), device="cpu"))
+    print(f"[quant-1000] gpu auc {ag:.5f} fp64 auc {af:.5f}")
+    assert abs(ag - af) <= 0.002

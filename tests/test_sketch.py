@@ -1,0 +1,131 @@
+"""Weighted quantile sketch (K12): NumPy oracle parity, 256-bin features, data-parallel invariance and
+the mergeable summary (reference: XGBClassifier hist, max_bin=256 -- the shipped pkl's Config,
+src/model_train_test/model_tree_train_test.py:111-118)."""
+import numpy as np
+import pytest
+import torch
+
+from cobalt_smart_lender_ai_amd.models import gbdt, sketch
+
+
+def _mixed(n, seed=0):
+    rng = np.random.default_rng(seed)
+    X = np.stack([
+        rng.lognormal(9, 0.6, n),                      # continuous, no missing -> 256 bins
+        rng.normal(size=n),                            # continuous, with missing -> 255 bins
+        rng.integers(0, 12, n).astype(float),          # low cardinality -> one bin per value
+        (rng.random(n) < 0.3).astype(float),           # binary
+    ], 1).astype(np.float32)
+    X[rng.random(n) < 0.1, 1] = np.nan
+    return X
+
+
+def test_unweighted_cuts_are_order_statistics():
+    X = _mixed(50_000, 1)
+    c, nb = sketch.compute_cuts(torch.from_numpy(X), 256)
+    c1, nb1 = sketch.compute_cuts(torch.from_numpy(X), 256, weights=torch.ones(len(X)))
+    assert torch.equal(c, c1) and torch.equal(nb, nb1)
+    for f, maxb in ((0, 256), (1, 255)):
+        xs = np.sort(X[~np.isnan(X[:, f]), f])
+        ref = []
+        for j in range(1, maxb):
+            v = xs[(j * len(xs)) // maxb]
+            if v > xs[0] and (not ref or v != ref[-1]):
+                ref.append(v)
+        assert int(nb[f]) == len(ref) + 1
+        assert np.array_equal(c[f, : len(ref)].numpy(), np.asarray(ref, np.float32))
+    assert int(nb[0]) == 256 and int(nb[1]) == 255  # 256 real bins only without missing values
+    assert int(nb[2]) == 12 and int(nb[3]) == 2
+
+
+def test_weighted_cuts_match_numpy_oracle():
+    X = _mixed(40_000, 2)
+    rng = np.random.default_rng(3)
+    w = np.where(rng.random(len(X)) < 0.13, 6.74642229, 1.0) * rng.uniform(0.5, 1.5, len(X))
+    c, nb = sketch.compute_cuts(torch.from_numpy(X), 256, weights=torch.from_numpy(w))
+    for f, maxb in ((0, 256), (1, 255)):
+        ref = sketch.weighted_quantile_cuts_np(X[:, f], w, maxb)
+        assert int(nb[f]) == len(ref) + 1
+        assert np.array_equal(c[f, : len(ref)].numpy(), ref)
+    # heavier weights pull the cuts: a weighted sketch differs from the unweighted one
+    cu, _ = sketch.compute_cuts(torch.from_numpy(X), 256)
+    assert not torch.equal(c[0], cu[0])
+
+
+def test_hessian_sketch_weights_scale_positives():
+    y = np.array([0, 1, 1, 0], np.float32)
+    p = gbdt.GBDTParams(scale_pos_weight=6.5, sketch_weight="hessian")
+    w = gbdt.sketch_weights_for(p, y, None, "cpu")
+    assert np.allclose(w.numpy(), [1, 6.5, 6.5, 1])
+    assert gbdt.sketch_weights_for(gbdt.GBDTParams(), y, None, "cpu") is None
+    with pytest.raises(ValueError):
+        gbdt.sketch_weights_for(gbdt.GBDTParams(sketch_weight="bogus"), y, None, "cpu")
+
+
+def test_host_binning_and_training_with_256_bin_features():
+    X = _mixed(20_000, 4)
+    y = (np.nan_to_num(X[:, 1]) + 0.002 * X[:, 0] / 1e3 > 0.5).astype(np.float32)
+    bd = gbdt.bin_dataset(X, device="cpu")
+    assert int(bd.nbins[0]) == 256
+    assert bd.bins_host[:, 0].max() == 255          # code 255 is a real bin of feature 0
+    assert np.isnan(X[:, 1]).any() and (bd.bins_host[np.isnan(X[:, 1]), 1] == 255).all()
+    b = gbdt.train(X, y, gbdt.GBDTParams(n_estimators=5, max_depth=4), device="cpu")
+    from cobalt_smart_lender_ai_amd.models.booster import predict_margin_host
+
+    rep = gbdt.FitReport()
+    b = gbdt.train(X, y, gbdt.GBDTParams(n_estimators=5, max_depth=4), device="cpu", report=rep)
+    assert np.array_equal(rep.extra["margin"], predict_margin_host(b, X))
+    for t in b.trees:  # splits on the no-missing 256-bin feature send missing values right
+        sel = (t.left_children != -1) & (t.split_indices == 0)
+        assert (t.default_left[sel] == 0).all()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_data_parallel_cuts_equal_single_rank(world, weighted):
+    from cobalt_smart_lender_ai_amd.parallel import loopback
+    from cobalt_smart_lender_ai_amd.parallel.dist import shard_range
+
+    n = 30_000
+    X = _mixed(n, 5)
+    X[n - 7, 0] = np.nan  # one missing value on the LAST rank only: every rank must use 255 bins
+    w = np.random.default_rng(6).uniform(0.1, 3.0, n) if weighted else None
+    ref = gbdt.bin_dataset(X, device="cpu", sketch_rows=4096, sketch_weights=w)
+    assert int(ref.nbins[0]) == 255
+
+    def rank_fn(ctx):
+        s, e = shard_range(n, ctx.rank, ctx.world)
+        bd = gbdt.bin_dataset(X[s:e], device="cpu", sketch_rows=4096, dist=ctx, n_rows_global=n, row_offset=s,
+                              sketch_weights=None if w is None else w[s:e])
+        return bd.cuts, bd.nbins
+
+    for c, nb in loopback.run_ranks(world, rank_fn, device="cpu"):
+        assert torch.equal(c, ref.cuts) and torch.equal(nb, ref.nbins)
+
+
+def test_quantile_summary_merge_is_rank_consistent_and_accurate():
+    from cobalt_smart_lender_ai_amd.parallel import loopback
+    from cobalt_smart_lender_ai_amd.parallel.dist import shard_range
+
+    n = 60_000
+    X = _mixed(n, 7)
+    exact = sketch.compute_cuts(torch.from_numpy(X), 256)
+
+    def rank_fn(ctx):
+        s, e = shard_range(n, ctx.rank, ctx.world)
+        bd = gbdt.bin_dataset(X[s:e], device="cpu", sketch_rows=n, dist=ctx, n_rows_global=n, row_offset=s,
+                              sketch_mode="summary")
+        return bd.cuts, bd.nbins
+
+    outs = loopback.run_ranks(4, rank_fn, device="cpu")
+    for c, nb in outs[1:]:
+        assert torch.equal(c, outs[0][0]) and torch.equal(nb, outs[0][1])
+    c, nb = outs[0]
+    # low-cardinality features are exact; continuous ones within ~1/8 bin of the exact quantiles
+    assert torch.equal(c[2:], exact[0][2:]) and torch.equal(nb[2:], exact[1][2:])
+    for f in (0, 1):
+        xs = np.sort(X[~np.isnan(X[:, f]), f])
+        k = int(nb[f]) - 1
+        ranks = np.searchsorted(xs, c[f, :k].numpy(), side="left") / len(xs)
+        target = np.arange(1, k + 1) / (k + 1)
+        assert np.max(np.abs(ranks - target)) < 2.0 / 256
