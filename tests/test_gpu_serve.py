@@ -170,3 +170,26 @@ def test_deep_trees_grow_the_lds_tile():
         margin = torch.empty(n, dtype=torch.float32, device="cuda")
         predict_ops.predict_gpu(bst, Xd, None, out_margin=margin)
         np.testing.assert_array_equal(margin.cpu().numpy(), predict_margin_host(bst, X))
+
+
+def test_host_stream_scorer_files_equal_device_path(reference_booster, tmp_path):
+    """The host/disk-resident pipeline (memory-mapped shards -> pinned slots -> H2D -> graph -> D2H)
+    scores exactly what the device-resident path scores, across file boundaries, partial last
+    chunks and slot reuse."""
+    from cobalt_smart_lender_ai_amd.dataio import synth
+    from cobalt_smart_lender_ai_amd.serve import batch_score as bs
+
+    parts, paths = [], []
+    for i, n in enumerate([1_300_000, 700_001, 1_000_000]):
+        X = synth.make_lendingclub(n, seed=i, row_offset=i * 2_000_000)[0].numpy()
+        p = tmp_path / f"s{i}.npy"
+        np.save(p, X)
+        parts.append(X)
+        paths.append(str(p))
+    meta = bs.score_files(reference_booster, paths, tmp_path / "out", 0, 1, "cuda", chunk=300_000, slots=3,
+                          stage_threads=4)
+    assert meta["rows"] == 3_000_001
+    got = bs.gather_scores(tmp_path / "out")
+    Xd = torch.from_numpy(np.concatenate(parts)).cuda()
+    ref = bs.score_device_matrix(reference_booster, Xd).cpu().numpy()
+    assert np.array_equal(got, ref)
