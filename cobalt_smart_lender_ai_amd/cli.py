@@ -64,8 +64,17 @@ def cmd_train(args) -> int:
         cfg.search_n_iter = args.n_iter
     if args.gpus is not None:
         cfg.fits_in_parallel = args.gpus
-    df = st.read_csv(cfg.input_key)
-    m = run_training(df, cfg, store=st, local_dir=args.local_dir, device=args.device)
+    from .parallel.taskpool import GpuTaskPool, resolve_workers
+
+    # the search's worker processes are spawned first, before this process touches the GPU
+    nw = resolve_workers(cfg.fits_in_parallel)
+    pool = GpuTaskPool(nw) if nw > 1 else None
+    try:
+        df = st.read_csv(cfg.input_key)
+        m = run_training(df, cfg, store=st, local_dir=args.local_dir, device=args.device, pool=pool)
+    finally:
+        if pool is not None:
+            pool.close()
     print(json.dumps({k: m[k] for k in ("auc", "best_params", "timing_s", "selected_features")}, indent=2))
     return 0
 

@@ -42,8 +42,27 @@ def _matrix(df: pd.DataFrame) -> np.ndarray:
 
 
 def run_training(df_tree: pd.DataFrame, cfg: TrainConfig | None = None, store: ArtifactStore | None = None,
-                 local_dir: str | Path = "models", device=None, rfe_params: dict | None = None) -> dict:
+                 local_dir: str | Path = "models", device=None, rfe_params: dict | None = None,
+                 pool=None) -> dict:
+    """``pool``: a :class:`~..parallel.taskpool.GpuTaskPool` for the search's task-parallel fits.
+    Without one, ``cfg.fits_in_parallel`` > 1 (None = all visible GPUs) creates a pool here -- before
+    this function's own GPU work, so the workers are spawned from a process without HIP state (when
+    the caller has not touched the GPU yet either; ``cli train`` guarantees that)."""
+    from ..parallel.taskpool import GpuTaskPool, resolve_workers
+
     cfg = cfg or TrainConfig()
+    own_pool = None
+    if pool is None and resolve_workers(cfg.fits_in_parallel) > 1:
+        pool = own_pool = GpuTaskPool(resolve_workers(cfg.fits_in_parallel))
+    try:
+        return _run_training(df_tree, cfg, store, local_dir, device, rfe_params, pool)
+    finally:
+        if own_pool is not None:
+            own_pool.close()
+
+
+def _run_training(df_tree: pd.DataFrame, cfg: TrainConfig, store: ArtifactStore | None, local_dir, device,
+                  rfe_params: dict | None, pool) -> dict:
     t0 = time.perf_counter()
     df = df_tree.drop(columns=LEAKAGE_COLUMNS, errors="ignore")
     n_nan = int(df["loan_default"].isna().sum())
@@ -74,7 +93,7 @@ def run_training(df_tree: pd.DataFrame, cfg: TrainConfig | None = None, store: A
     ts = time.perf_counter()
     sr = randomized_search(_matrix(Xtr[selected]), ytr, cfg.search_space, base, n_iter=cfg.search_n_iter,
                            cv=cfg.search_cv_folds, random_state=cfg.search_random_state, device=device,
-                           n_gpus=cfg.fits_in_parallel or 1)
+                           n_gpus=1, pool=pool)
     t_search = time.perf_counter() - ts
     log.info("Best score (AUC): %s", sr.best_score_)
     log.info("Best params: %s", sr.best_params_)

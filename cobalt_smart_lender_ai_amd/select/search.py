@@ -94,36 +94,45 @@ def _fold_scores(X, y, folds, base: dict, candidates: list[dict], device, stream
 
 
 def _worker(args):
-    X, y, folds, base, cands, gpu = args
-    if gpu is not None and torch.cuda.is_available():
-        torch.cuda.set_device(gpu)
-        dev = f"cuda:{gpu}"
-    else:
-        dev = "cpu"
-    return _fold_scores(X, y, folds, base, cands, dev)
+    """Pool task: the fold scores of a candidate subset on this worker's GPU (parallel/taskpool.py)."""
+    from ..parallel.taskpool import worker_device
+
+    X, y, folds, base, cands = args
+    return _fold_scores(X, y, folds, base, cands, worker_device())
 
 
 def randomized_search(X, y, param_distributions: dict, base_params: dict, n_iter: int = 20, cv: int = 3,
-                      random_state: int | None = 22, device=None, n_gpus: int = 1) -> SearchResult:
+                      random_state: int | None = 22, device=None, n_gpus: int | None = 1,
+                      pool=None) -> SearchResult:
+    """``pool`` (a :class:`~..parallel.taskpool.GpuTaskPool`, created before this process touched the
+    GPU) runs the (candidate x fold) fits task-parallel, candidates dealt round-robin to its workers;
+    otherwise ``n_gpus`` > 1 (None = all visible) creates one for this call."""
+    from ..parallel.taskpool import GpuTaskPool, visible_gpus
+
     X = np.asarray(X, dtype=np.float32)
     y = np.asarray(y, dtype=np.float32)
     cands = sample_candidates(param_distributions, n_iter, random_state)
     folds = stratified_kfold_indices(y, cv)
     t0 = time.perf_counter()
-    ngpu = min(n_gpus, torch.cuda.device_count()) if torch.cuda.is_available() else 0
-    if ngpu > 1:
-        import multiprocessing as mp
-
-        shards = [list(range(i, len(cands), ngpu)) for i in range(ngpu)]
-        ctx = mp.get_context("spawn")
-        with ctx.Pool(ngpu) as pool:
-            parts = pool.map(_worker, [(X, y, folds, base_params, [cands[j] for j in sh], g)
-                                       for g, sh in enumerate(shards)])
-        scores = np.zeros((len(cands), len(folds)))
-        for sh, part in zip(shards, parts):
-            scores[sh] = part
-    else:
-        scores = _fold_scores(X, y, folds, base_params, cands, device)
+    own = None
+    if pool is None:
+        ngpu = visible_gpus() if n_gpus is None else min(int(n_gpus), visible_gpus())
+        if ngpu > 1:
+            pool = own = GpuTaskPool(ngpu, ngpu)
+    try:
+        if pool is not None:
+            nw = pool.workers
+            shards = [list(range(i, len(cands), nw)) for i in range(nw)]
+            shards = [sh for sh in shards if sh]
+            parts = pool.map(_worker, [(X, y, folds, base_params, [cands[j] for j in sh]) for sh in shards])
+            scores = np.zeros((len(cands), len(folds)))
+            for sh, part in zip(shards, parts):
+                scores[sh] = part
+        else:
+            scores = _fold_scores(X, y, folds, base_params, cands, device)
+    finally:
+        if own is not None:
+            own.close()
     mean = scores.mean(1)
     # sklearn ranks with method="min": equal scores share the best rank
     order = np.argsort(-mean, kind="stable")
