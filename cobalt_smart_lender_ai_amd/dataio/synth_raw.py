@@ -19,7 +19,61 @@ PURPOSE = ["debt_consolidation", "credit_card", "home_improvement", "other", "ma
            "small_business", "car", "vacation", "moving", "house", "wedding", "renewable_energy"]
 
 
-def make_raw_lendingclub(n: int, seed: int = 0, n_dups: int = 3) -> pd.DataFrame:
+# Further numeric columns of the LendingClub export (names from its data dictionary), used to widen the
+# synthetic frame to the real export's 143 columns (``n_cols``); (name, missing share, generator kind)
+EXTRA_NUMERIC = [
+    ("tot_coll_amt", 0.03, "logn"), ("tot_cur_bal", 0.03, "logn"), ("total_rev_hi_lim", 0.03, "logn"),
+    ("acc_open_past_24mths", 0.02, "pois4"), ("avg_cur_bal", 0.03, "logn"), ("bc_open_to_buy", 0.04, "logn"),
+    ("bc_util", 0.04, "pct"), ("mo_sin_old_il_acct", 0.06, "pois120"), ("mo_sin_rcnt_rev_tl_op", 0.03, "pois12"),
+    ("mo_sin_rcnt_tl", 0.03, "pois8"), ("mths_since_recent_bc", 0.04, "pois24"),
+    ("mths_since_recent_inq", 0.12, "pois6"), ("num_accts_ever_120_pd", 0.03, "pois0"),
+    ("num_actv_bc_tl", 0.03, "pois4"), ("num_actv_rev_tl", 0.03, "pois6"), ("num_bc_sats", 0.03, "pois4"),
+    ("num_bc_tl", 0.03, "pois8"), ("num_il_tl", 0.03, "pois8"), ("num_op_rev_tl", 0.03, "pois8"),
+    ("num_rev_tl_bal_gt_0", 0.03, "pois6"), ("num_sats", 0.03, "pois12"), ("num_tl_120dpd_2m", 0.06, "pois0"),
+    ("num_tl_30dpd", 0.03, "pois0"), ("num_tl_90g_dpd_24m", 0.03, "pois0"), ("num_tl_op_past_12m", 0.03, "pois2"),
+    ("pct_tl_nvr_dlq", 0.03, "pct"), ("percent_bc_gt_75", 0.04, "pct"), ("tax_liens", 0.0, "pois0"),
+    ("tot_hi_cred_lim", 0.03, "logn"), ("total_bal_ex_mort", 0.03, "logn"), ("total_bc_limit", 0.03, "logn"),
+    ("total_il_high_credit_limit", 0.03, "logn"), ("open_act_il", 0.3, "pois2"), ("open_rv_12m", 0.3, "pois1"),
+    ("open_rv_24m", 0.3, "pois2"), ("total_bal_il", 0.3, "logn"), ("total_cu_tl", 0.3, "pois1"),
+    ("inq_fi", 0.3, "pois1"), ("collections_12_mths_ex_med", 0.0, "pois0"), ("delinq_amnt", 0.0, "pois0"),
+    ("mths_since_last_major_derog", 0.74, "pois40"), ("mths_since_last_record", 0.84, "pois60"),
+    ("policy_code", 0.0, "one"), ("revol_bal_joint", 0.95, "logn"), ("sec_app_fico_range_low", 0.95, "fico"),
+    ("sec_app_fico_range_high", 0.95, "fico"), ("sec_app_inq_last_6mths", 0.95, "pois1"),
+    ("sec_app_mort_acc", 0.95, "pois1"), ("sec_app_open_acc", 0.95, "pois12"), ("sec_app_revol_util", 0.95, "pct"),
+    ("sec_app_open_act_il", 0.95, "pois2"), ("sec_app_num_rev_accts", 0.95, "pois12"),
+    ("sec_app_chargeoff_within_12_mths", 0.95, "pois0"), ("sec_app_collections_12_mths_ex_med", 0.95, "pois0"),
+    ("dti_joint", 0.93, "dti"), ("deferral_term", 0.95, "three"), ("hardship_amount", 0.95, "logn"),
+    ("hardship_length", 0.95, "three"), ("hardship_dpd", 0.95, "pois8"),
+    ("orig_projected_additional_accrued_interest", 0.96, "logn"), ("hardship_payoff_balance_amount", 0.95, "logn"),
+    ("hardship_last_payment_amount", 0.95, "logn"), ("settlement_amount", 0.97, "logn"),
+    ("settlement_percentage", 0.97, "pct"), ("settlement_term", 0.97, "pois12"), ("out_prncp_inv", 0.0, "logn"),
+    ("total_pymnt_inv", 0.0, "logn"), ("member_id", 1.0, "one"), ("open_il_6m", 0.3, "pois1"),
+    ("mths_since_rcnt_il", 0.32, "pois20"), ("sec_app_mths_since_last_major_derog", 0.98, "pois40"),
+    ("num_tl_120dpd_6m", 0.06, "pois0"), ("settlement_days", 0.97, "pois30"),
+]
+
+
+def _extra_column(rng: np.random.Generator, n: int, kind: str) -> np.ndarray:
+    if kind == "logn":
+        v = np.round(np.exp(8 + 1.2 * rng.standard_normal(n)))
+    elif kind.startswith("pois"):
+        v = rng.poisson(float(kind[4:]) or 0.05, n).astype(float)
+    elif kind == "pct":
+        v = np.clip(np.round(60 + 30 * rng.standard_normal(n), 1), 0, 100)
+    elif kind == "fico":
+        v = np.clip(np.round((690 + 40 * rng.standard_normal(n)) / 5) * 5, 540, 850)
+    elif kind == "dti":
+        v = np.round(np.clip(18 + 8 * rng.standard_normal(n), 0, 60), 2)
+    elif kind == "three":
+        v = np.full(n, 3.0)
+    else:
+        v = np.ones(n)
+    return v
+
+
+def make_raw_lendingclub(n: int, seed: int = 0, n_dups: int = 3, n_cols: int | None = None) -> pd.DataFrame:
+    """``n`` raw rows (+ ``n_dups`` exact duplicates); ``n_cols`` widens the frame with further numeric
+    LendingClub columns (EXTRA_NUMERIC) up to that many columns (the full export has 143)."""
     rng = np.random.default_rng(seed)
     grade = rng.choice(list("ABCDEFG"), n, p=[0.19, 0.29, 0.28, 0.14, 0.06, 0.03, 0.01])
     gi = np.searchsorted(np.array(list("ABCDEFG")), grade)
@@ -106,6 +160,16 @@ def make_raw_lendingclub(n: int, seed: int = 0, n_dups: int = 3) -> pd.DataFrame
         "hardship_status": hard,
         "debt_settlement_flag": rng.choice(["N", "Y"], n, p=[0.98, 0.02]),
     })
+    if n_cols is not None and n_cols > df.shape[1]:
+        extra = {}
+        for name, miss, kind in EXTRA_NUMERIC[: n_cols - df.shape[1]]:
+            v = _extra_column(rng, n, kind)
+            if miss >= 1.0:
+                v[:] = np.nan
+            elif miss > 0:
+                v[rng.random(n) < miss] = np.nan
+            extra[name] = v
+        df = pd.concat([df, pd.DataFrame(extra)], axis=1)
     # a few columns with 1-9 NaNs (exercises the script preset's row drop)
     for c, k in (("delinq_2yrs", 3), ("inq_last_6mths", 5), ("open_acc", 2)):
         df.loc[rng.choice(n, k, replace=False), c] = np.nan

@@ -14,6 +14,9 @@
                  GPU (serve/batch_score.py; ranks are independent, so 8 GPUs = 8 x the shard rate)
   cpu-hist-gbdt-10m  CPU reference point for the headline metric (scikit-learn's OpenMP histogram
                  GBDT on the same 10M rows; the reference publishes no throughput)
+  prep-full      the reference's full-data preprocessing (clean_data.py full + feature_engineering.py) on a
+                 2.9M-row x 143-column synthetic raw export: pandas path vs the device-resident path
+                 (scripts/bench_prep.py)
   pipeline-100k  the reference's training job (RFE 106 -> 20 + 20 x 3-fold search + refit) end to end
                  on a 100k-row synthetic sample (scripts/bench_pipeline.py)
 """
@@ -131,6 +134,7 @@ CONFIGS = {
     "gbdt-10m": lambda: _named("gbdt-10m", _run(["bench.py", "--steps", "3"], 600)),
     "ooc-100m": lambda: {"config": "ooc-100m",
                          **_run(["scripts/bench_external.py", "--rows", "100000000", "--compare-in-core"], 1100)},
+    "prep-full": lambda: {"config": "prep-full", **_run(["scripts/bench_prep.py"], 1100)},
     "score-1b": lambda: {"config": "score-1b", "note": "one 125M-row shard of the 1B-row job (8 ranks x 125M)",
                          **_run(["-m", "cobalt_smart_lender_ai_amd.serve.batch_score", "--rows-per-gpu",
                                  "125000000"], 600)},

@@ -55,3 +55,24 @@ def test_prep_kernels_match_host():
     assert torch.equal(ig.cpu(), ic)
     codes = torch.from_numpy(rng.integers(-1, 6, 10_000).astype(np.int32))
     assert torch.equal(prep_ops.onehot(codes.cuda(), 6).cpu(), prep_ops.onehot(codes, 6))
+
+
+@pytest.mark.timeout(900)
+def test_gpu_device_resident_prep_equals_pandas_at_1m_rows(tmp_path):
+    """>= 1M raw rows x 143 columns: the device-resident pipeline (pyarrow ingest -> HBM -> stage 1 ->
+    stage 2 -> features on the GPU) produces exactly the pandas path's cleaned, tree and NN frames."""
+    import pyarrow as pa
+    import pyarrow.csv as pcsv
+
+    from cobalt_smart_lender_ai_amd.dataio.synth_raw import make_raw_lendingclub
+    from test_device_prep import assert_frames_equal, device_path, pandas_path
+
+    raw = make_raw_lendingclub(1_000_000, seed=8, n_cols=143)
+    csv = tmp_path / "raw.csv"
+    pcsv.write_csv(pa.Table.from_pandas(raw, preserve_index=False), str(csv))
+    del raw
+    got = device_path(str(csv), "cuda")
+    ref = pandas_path(csv)
+    for g, r in zip(got, ref):
+        assert_frames_equal(g, r)
+    assert len(ref[2]) > 900_000
