@@ -156,6 +156,29 @@ __global__ __launch_bounds__(256) void k_minmax_apply(const double* __restrict__
   }
 }
 
+
+// K10 (ingest): 64-bit hash of every string of an Arrow string column, one thread per string, so a
+// near-unique text column (url, titles) never needs a host dictionary: the hash stands in for the
+// value in null counts and row dedupe (equal strings -> equal hash; candidate duplicates are verified
+// exactly on the host). Mirrors prep_ops._string_hash_host: h = len ^ seed, then splitmix64 over the
+// little-endian 8-byte words (zero padded); 0 is reserved for missing.
+__global__ __launch_bounds__(256) void k_str_hash(const uint8_t* __restrict__ data, const int64_t* __restrict__ off,
+                                                  const uint8_t* __restrict__ valid, int64_t n,
+                                                  unsigned long long* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) { out[i] = 0ull; continue; }
+    const int64_t b = off[i], e = off[i + 1];
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)(e - b);
+    for (int64_t p = b; p < e; p += 8) {
+      uint64_t w = 0;
+      const int m = (int)((e - p) < 8 ? (e - p) : 8);
+      for (int j = 0; j < m; ++j) w |= (uint64_t)data[p + j] << (8 * j);
+      h = splitmix64(h ^ w);
+    }
+    out[i] = h ? h : 1ull;
+  }
+}
+
 static dim3 col_grid(int64_t n, int C) {
   return dim3(std::max(1, std::min(ceil_div(n, 256), 512)), C);
 }
@@ -224,6 +247,14 @@ COBALT_API int cobalt_minmax_apply(const double* X, int64_t n, int C, const doub
                                    hipStream_t s) {
   if (n <= 0 || C <= 0) return 0;
   hipLaunchKernelGGL(k_minmax_apply, col_grid(n, C), dim3(256), 0, s, X, n, mn, mx, out, C);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_str_hash(const uint8_t* data, const int64_t* off, const uint8_t* valid, int64_t n,
+                               unsigned long long* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_str_hash, dim3(std::min(ceil_div(n, 256), 8192)), dim3(256), 0, s, data, off, valid, n, out);
   CK_LAUNCH();
   return 0;
 }

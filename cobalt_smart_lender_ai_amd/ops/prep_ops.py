@@ -22,6 +22,7 @@ _native.register("cobalt_rows_equal", _I, [_V, _I64, _I, _V, _V, _I64, _V, _V])
 _native.register("cobalt_onehot", _I, [_V, _I64, _I, _I, _V, _V])
 _native.register("cobalt_col_moments", _I, [_V, _I64, _I, _V, _V])
 _native.register("cobalt_minmax_apply", _I, [_V, _I64, _I, _V, _V, _V, _V])
+_native.register("cobalt_str_hash", _I, [_V, _V, _V, _I64, _V, _V])
 
 
 def _cuda(t: torch.Tensor) -> bool:
@@ -218,3 +219,69 @@ def minmax_scale(X: torch.Tensor, mn: torch.Tensor, mx: torch.Tensor) -> torch.T
     rng = (mx - mn).numpy()
     sc = np.where(rng > 0, 1.0 / np.where(rng > 0, rng, 1.0), 0.0)
     return torch.from_numpy(((X.numpy() - mn.numpy()[:, None]) * sc[:, None]).T.astype(np.float32))
+
+
+_MASK64 = (1 << 64) - 1
+
+
+def _splitmix_np(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def _string_hash_host(data: np.ndarray, off: np.ndarray, valid: np.ndarray | None) -> np.ndarray:
+    """NumPy twin of k_str_hash (vectorised over strings, looping over 8-byte word positions)."""
+    n = len(off) - 1
+    b, e = off[:-1].astype(np.int64), off[1:].astype(np.int64)
+    ln = e - b
+    h = np.uint64(0x9E3779B97F4A7C15) ^ ln.astype(np.uint64)
+    nw = (ln + 7) // 8
+    dpad = np.concatenate([data, np.zeros(8, np.uint8)])
+    for k in range(int(nw.max()) if n else 0):
+        act = nw > k
+        w = np.zeros(n, dtype=np.uint64)
+        for j in range(8):
+            p = b + 8 * k + j
+            ok = act & (p < e)
+            w |= np.where(ok, dpad[np.where(ok, p, len(data))], 0).astype(np.uint64) << np.uint64(8 * j)
+        h = np.where(act, _splitmix_np(h ^ w), h)
+    h = np.where(h == 0, np.uint64(1), h)
+    if valid is not None:
+        h = np.where(valid, h, np.uint64(0))
+    return h.view(np.int64)
+
+
+def string_hash(col, device) -> torch.Tensor:
+    """int64 [N] hashes of an Arrow string (Chunked)Array; 0 = missing. GPU: k_str_hash per chunk."""
+    import pyarrow as pa
+
+    dev = torch.device(device)
+    chunks = col.chunks if hasattr(col, "chunks") else [col]
+    outs = []
+    for ch in chunks:
+        n = len(ch)
+        if n == 0:
+            continue
+        large = pa.types.is_large_string(ch.type)
+        bufs = ch.buffers()
+        ity = np.int64 if large else np.int32
+        off = np.frombuffer(bufs[1], dtype=ity, count=n + 1, offset=ch.offset * np.dtype(ity).itemsize).astype(np.int64)
+        base = int(off[0])
+        data = np.frombuffer(bufs[2], dtype=np.uint8)[base:int(off[-1])] if bufs[2] is not None else np.zeros(0, np.uint8)
+        off = off - base
+        valid = ch.is_valid().to_numpy(zero_copy_only=False) if ch.null_count else None
+        if dev.type == "cuda":
+            d = torch.from_numpy(np.ascontiguousarray(data)).to(dev) if len(data) else torch.zeros(1, dtype=torch.uint8,
+                                                                                             device=dev)
+            o = torch.from_numpy(off).to(dev)
+            v = torch.from_numpy(valid.astype(np.uint8)).to(dev) if valid is not None else None
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+            _native.check(_lib().cobalt_str_hash(d.data_ptr(), o.data_ptr(), v.data_ptr() if v is not None else None,
+                                                 n, out.data_ptr(), _s()), "str_hash")
+            outs.append(out)
+        else:
+            outs.append(torch.from_numpy(_string_hash_host(data, off, valid)))
+    return torch.cat(outs) if outs else torch.zeros(0, dtype=torch.int64, device=dev)

@@ -34,16 +34,20 @@ PANDAS_NA = ["", "#N/A", "#N/A N/A", "#NA", "-1.#IND", "-1.#QNAN", "-NaN", "-nan
 
 @dataclass
 class DCol:
-    kind: str                 # "f" float64 values, "c" int32 dictionary codes (-1 = missing), "b" uint8 flags
+    kind: str                 # "f" float64 values, "c" int32 dictionary codes (-1 = missing), "b" uint8 flags,
+                              # "h" int64 device hashes of a near-unique string column (0 = missing)
     data: torch.Tensor        # [N] on the frame's device
     dtype: str                # pandas dtype on export: "float64" | "int64" | "bool" | "object"
     vocab: list | None = None  # "c": code -> value
+    src: object = None        # "h": the host Arrow column (ORIGINAL rows; decoded lazily through rowid)
 
     def null_mask(self) -> torch.Tensor:
         if self.kind == "f":
             return torch.isnan(self.data)
         if self.kind == "c":
             return self.data < 0
+        if self.kind == "h":
+            return self.data == 0
         return torch.zeros_like(self.data, dtype=torch.bool)
 
     @property
@@ -54,10 +58,12 @@ class DCol:
 class DeviceFrame:
     """Ordered columns of equal length on one device (see module doc)."""
 
-    def __init__(self, cols: dict[str, DCol], n: int, device: torch.device):
+    def __init__(self, cols: dict[str, DCol], n: int, device: torch.device, rowid: torch.Tensor | None = None):
         self.cols = dict(cols)
         self.n = int(n)
         self.device = torch.device(device)
+        # original (ingest) row of every row -- lets hashed string columns be decoded lazily
+        self.rowid = rowid if rowid is not None else torch.arange(self.n, device=self.device)
 
     # ------------------------------------------------------------------ structure
     @property
@@ -78,7 +84,7 @@ class DeviceFrame:
         return self.cols[name]
 
     def copy(self) -> "DeviceFrame":
-        return DeviceFrame(self.cols, self.n, self.device)
+        return DeviceFrame(self.cols, self.n, self.device, self.rowid)
 
     def drop(self, names, errors: str = "ignore") -> "DeviceFrame":
         names = [names] if isinstance(names, str) else list(names)
@@ -87,25 +93,58 @@ class DeviceFrame:
             if miss:
                 raise KeyError(f"{miss} not found in axis")
         s = set(names)
-        return DeviceFrame({k: v for k, v in self.cols.items() if k not in s}, self.n, self.device)
+        return DeviceFrame({k: v for k, v in self.cols.items() if k not in s}, self.n, self.device, self.rowid)
 
     def assign(self, **cols: DCol) -> "DeviceFrame":
         """DataFrame.assign: an existing name keeps its position, a new one is appended."""
         out = dict(self.cols)
         out.update(cols)
-        return DeviceFrame(out, self.n, self.device)
+        return DeviceFrame(out, self.n, self.device, self.rowid)
+
+    def host_strings(self, name: str, rows: torch.Tensor | None = None):
+        """Values of a hashed ("h") string column for the current rows (or ``rows`` of them)."""
+        import pyarrow.compute as pc
+
+        c = self.cols[name]
+        rid = self.rowid if rows is None else self.rowid[rows]
+        return pc.take(c.src, rid.cpu().numpy())
+
+    def as_categorical(self, name: str) -> DCol:
+        """A string column as dictionary codes ("c"); a hashed column is decoded + encoded on demand."""
+        import pyarrow.compute as pc
+
+        c = self.cols[name]
+        if c.kind != "h":
+            return c
+        enc = pc.dictionary_encode(self.host_strings(name))
+        enc = enc.unify_dictionaries() if hasattr(enc, "unify_dictionaries") else enc
+        chunks = enc.chunks if hasattr(enc, "chunks") else [enc]
+        vocab = chunks[0].dictionary.to_pylist() if chunks else []
+        idx = np.concatenate([ch.indices.fill_null(-1).to_numpy(zero_copy_only=False).astype(np.int32)
+                              for ch in chunks] + [np.zeros(0, np.int32)])
+        return DCol("c", torch.from_numpy(idx).to(self.device), "object", vocab)
 
     # ------------------------------------------------------------------ ingest / export
     @classmethod
-    def from_arrow(cls, table, device) -> "DeviceFrame":
+    def from_arrow(cls, table, device, hash_unique_share: float = 0.2) -> "DeviceFrame":
+        """Upload an Arrow table. String columns whose first 20k values are more than
+        ``hash_unique_share`` distinct are hashed on the device (kind "h") instead of dictionary-encoded
+        on the host (a near-unique column costs ~2 s per million rows to encode, ~1 ms to hash)."""
         import pyarrow as pa
         import pyarrow.compute as pc
+
+        from ..ops import prep_ops as _po
 
         dev = torch.device(device)
         n = table.num_rows
         cols: dict[str, DCol] = {}
         for name, col in zip(table.column_names, table.columns):
             t = col.type
+            if (pa.types.is_string(t) or pa.types.is_large_string(t)) and n >= 1000:
+                head = col.slice(0, min(n, 20_000))
+                if pc.count_distinct(head).as_py() > hash_unique_share * len(head):
+                    cols[name] = DCol("h", _po.string_hash(col, dev), "object", src=col)
+                    continue
             if pa.types.is_string(t) or pa.types.is_large_string(t) or pa.types.is_dictionary(t):
                 enc = col if pa.types.is_dictionary(t) else pc.dictionary_encode(col)
                 enc = enc.unify_dictionaries() if hasattr(enc, "unify_dictionaries") else enc
@@ -156,6 +195,10 @@ class DeviceFrame:
     def to_pandas(self) -> pd.DataFrame:
         out = {}
         for name, c in self.cols.items():
+            if c.kind == "h":
+                out[name] = pd.Series(self.host_strings(name).to_pandas(), dtype=object).where(
+                    lambda v: v.notna(), np.nan)
+                continue
             a = c.data.cpu().numpy()
             if c.kind == "c":
                 voc = np.array(list(c.vocab) + [np.nan], dtype=object)
@@ -212,6 +255,7 @@ class DeviceFrame:
         m = int(idx.numel())
         if m == self.n:
             return self.copy()
+        rowid = self.rowid.index_select(0, idx)
         out = {}
         groups: dict[str, list[str]] = {}
         for nm, c in self.cols.items():
@@ -221,18 +265,31 @@ class DeviceFrame:
             g = blk.index_select(1, idx)
             for i, nm in enumerate(names):
                 out[nm] = replace(self.cols[nm], data=g[i])
-        return DeviceFrame({nm: out[nm] for nm in self.cols}, m, self.device)
+        return DeviceFrame({nm: out[nm] for nm in self.cols}, m, self.device, rowid)
 
     def duplicated(self) -> torch.Tensor:
         """``df.duplicated(keep='first')`` over all columns: device row hash + sort + exact pairwise
         verification (K9). Codes compare exactly as their strings (one vocabulary per column)."""
         if self.n == 0:
             return torch.zeros(0, dtype=torch.bool, device=self.device)
-        blk = torch.empty((len(self.cols), self.n), dtype=torch.float64, device=self.device)
-        for i, c in enumerate(self.cols.values()):
-            blk[i] = c.data.to(torch.float64) if c.kind != "c" else torch.where(
-                c.data < 0, float("nan"), c.data.to(torch.float64))
-        dup, _ = prep_ops.duplicated_numeric(blk)
+        rows = []
+        for c in self.cols.values():
+            if c.kind == "c":
+                rows.append(torch.where(c.data < 0, float("nan"), c.data.to(torch.float64)))
+            elif c.kind == "h":  # two exact 32-bit halves of the hash
+                rows.append((c.data & 0xFFFFFFFF).to(torch.float64))
+                rows.append((c.data >> 32).to(torch.float64))
+            else:
+                rows.append(c.data.to(torch.float64))
+        dup, (a, b) = prep_ops.duplicated_numeric(torch.stack(rows))
+        hashed = [nm for nm, c in self.cols.items() if c.kind == "h"]
+        if hashed and a.numel():  # hashes stand in for strings: verify candidate pairs exactly
+            for nm in hashed:
+                sa = self.host_strings(nm, a).to_pylist()
+                sb = self.host_strings(nm, b).to_pylist()
+                bad = [k for k, (x, y) in enumerate(zip(sa, sb)) if x != y]
+                if bad:
+                    dup[b[torch.tensor(bad, device=b.device)]] = False
         return dup
 
 

@@ -30,8 +30,9 @@ from .features import DUMMY_COLUMNS, LEAKAGE_STAGE2, LOAN_STATUS_MAP, LOG_COLUMN
 log = logging.getLogger(__name__)
 
 
-def _is_missing(v) -> bool:
-    return v is None or (isinstance(v, float) and np.isnan(v))
+def _col(df: DeviceFrame, name: str) -> DCol:
+    """A column, hashed strings ("h") decoded to dictionary codes (only stages that need the values)."""
+    return df.as_categorical(name)
 
 
 # ------------------------------------------------------------------------------------------ stage 1
@@ -73,12 +74,13 @@ def device_clean_data_flow(df: DeviceFrame, preset: str = "script", null_thresho
         subset = [c for c, k in nulls.items() if k < 10]
         out = out.take(out.row_null_counts(subset) == 0)
     if "hardship_status" in out:
-        out = out.assign(hardship_status=_fill_cat(out["hardship_status"], "No Hardship"))
+        out = out.assign(hardship_status=_fill_cat(_col(out, "hardship_status"), "No Hardship"))
     if "term" in out:
-        nm = int(out["term"].null_mask().sum()) if out["term"].kind == "c" else 0
-        out = out.assign(term=_parse_term(out["term"], nm))
+        term = _col(out, "term")
+        nm = int(term.null_mask().sum()) if term.kind == "c" else 0
+        out = out.assign(term=_parse_term(term, nm))
     if "int_rate" in out:
-        out = out.assign(int_rate=_parse_percent(out["int_rate"]))
+        out = out.assign(int_rate=_parse_percent(_col(out, "int_rate")))
     nulls = out.null_counts()
     drop = [c for c, k in nulls.items() if k / max(len(out), 1) * 100.0 > null_threshold]
     log.info("Dropping columns with >%s%% missing: %s", null_threshold, drop)
@@ -126,16 +128,16 @@ def device_clean_lending_data(df: DeviceFrame, reference_date: datetime | str | 
     non_na = out.shape[1] - out.row_null_counts(None)
     out = out.take(non_na >= keep_min)
     if "emp_length" in out:
-        c = out["emp_length"]
+        c = _col(out, "emp_length")
         if c.kind == "c":
             num = gather_vocab(c, _emp_length_table(c.vocab))
         else:  # numeric emp_length: astype("string") -> the digits of its text
             num = torch.floor(c.data).where(~torch.isnan(c.data), c.data)
         out = out.drop(["emp_length"]).assign(emp_length_num=DCol("f", num, "float64"))
-    if "revol_util" in out and out["revol_util"].kind == "c":
-        out = out.assign(revol_util=_parse_percent(out["revol_util"]))
+    if "revol_util" in out and out["revol_util"].kind in ("c", "h"):
+        out = out.assign(revol_util=_parse_percent(_col(out, "revol_util")))
     if "earliest_cr_line" in out:
-        c = out["earliest_cr_line"]
+        c = _col(out, "earliest_cr_line")
         today = pd.Timestamp(reference_date) if reference_date is not None else pd.Timestamp(datetime.today())
         if c.kind == "c":
             dates = pd.to_datetime(pd.Series(c.vocab, dtype=object), format="%b-%Y", errors="coerce")
@@ -146,7 +148,7 @@ def device_clean_lending_data(df: DeviceFrame, reference_date: datetime | str | 
         dt = "int64" if not bool(torch.isnan(days).any()) else "float64"
         out = out.drop(["earliest_cr_line"]).assign(earliest_cr_line_days=DCol("f", days, dt))
     if "loan_status" in out:
-        c = out["loan_status"]
+        c = _col(out, "loan_status")
         if c.kind == "c":
             tab = np.array([LOAN_STATUS_MAP.get(v, np.nan) for v in c.vocab], dtype=np.float64)
             lab = gather_vocab(c, tab)
@@ -196,7 +198,7 @@ def _dummies(df: DeviceFrame) -> DeviceFrame:
         raise KeyError(f"None of {missing} are in the columns")
     out = df.drop(DUMMY_COLUMNS)
     for c in DUMMY_COLUMNS:
-        levels, codes = _sorted_levels(df[c])
+        levels, codes = _sorted_levels(_col(df, c))
         if len(levels) <= 1:
             continue
         oh = prep_ops.onehot(codes, len(levels), True)        # K7: [N, L-1] uint8 (drop_first)
@@ -221,8 +223,8 @@ def _nn_dataset(df_log: DeviceFrame) -> DeviceFrame:
     dti = nn["dti"].data
     dmed = prep_ops.median(dti.to(torch.float64).unsqueeze(0))[0]
     nn = nn.assign(dti=DCol("f", torch.where(torch.isnan(dti), dmed, dti), "float64"))
-    for c in [k for k, v in nn.cols.items() if v.kind == "c"]:
-        col = nn[c]
+    for c in [k for k, v in nn.cols.items() if v.kind in ("c", "h")]:
+        col = _col(nn, c)
         # LabelEncoder().fit_transform(astype(str)): missing values are the string "nan"
         strs = [str(v) for v in col.vocab] + ["nan"]
         present = torch.unique(torch.where(col.data < 0, len(col.vocab), col.data.long())).cpu().numpy()
