@@ -43,14 +43,14 @@ def cmd_synth(args) -> int:
 def cmd_clean(args) -> int:
     from .pipeline.prep_flow import run_clean
 
-    run_clean(_store(args), use_sample=not args.full, device=args.device, preset=args.preset)
+    run_clean(_store(args), use_sample=not args.full, device=args.device, preset=args.preset, engine=args.engine)
     return 0
 
 
 def cmd_features(args) -> int:
     from .pipeline.prep_flow import run_features
 
-    run_features(_store(args), device=args.device, reference_date=args.reference_date)
+    run_features(_store(args), device=args.device, reference_date=args.reference_date, engine=args.engine)
     return 0
 
 
@@ -150,9 +150,12 @@ def main(argv: list[str] | None = None) -> int:
     s = sub.add_parser("clean")
     s.add_argument("--full", action="store_true")
     s.add_argument("--preset", default="script", choices=["script", "notebook"])
+    s.add_argument("--engine", default=None, choices=["device", "pandas"],
+                   help="device-resident frame (default on a GPU) or the pandas path")
     s.set_defaults(fn=cmd_clean)
     s = sub.add_parser("features")
     s.add_argument("--reference-date", default=None)
+    s.add_argument("--engine", default=None, choices=["device", "pandas"])
     s.set_defaults(fn=cmd_features)
     s = sub.add_parser("train")
     s.add_argument("--local-dir", default="models")
