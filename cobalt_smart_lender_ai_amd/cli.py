@@ -125,6 +125,24 @@ def cmd_serve(args) -> int:
     return 0
 
 
+def cmd_dvc(args) -> int:
+    """DVC-compatible versioning of raw data files (dataio/dvc.py): add / status / push / pull."""
+    from .dataio import dvc
+
+    st = _store(args)
+    for target in args.targets:
+        if args.action == "add":
+            print(dvc.add(target))
+        elif args.action == "status":
+            for p, s in dvc.status(target).items():
+                print(f"{s}\t{p}")
+        elif args.action == "push":
+            print("\n".join(dvc.push(target, st, prefix=args.prefix)))
+        else:
+            print("\n".join(str(p) for p in dvc.pull(target, st, prefix=args.prefix)))
+    return 0
+
+
 def cmd_dictionary(args) -> int:
     from .dataio import dictionary, synth
 
@@ -173,6 +191,11 @@ def main(argv: list[str] | None = None) -> int:
     s.add_argument("--workers", type=int, default=int(__import__("os").environ.get("COBALT_SERVE_WORKERS", "1")))
     s.add_argument("--log-level", default="info")
     s.set_defaults(fn=cmd_serve)
+    s = sub.add_parser("dvc", help="DVC-compatible data versioning: add | status | push | pull")
+    s.add_argument("action", choices=["add", "status", "push", "pull"])
+    s.add_argument("targets", nargs="+", help="data files (add) or .dvc pointers")
+    s.add_argument("--prefix", default="dataset/", help="remote key prefix (the reference's DVC remote path)")
+    s.set_defaults(fn=cmd_dvc)
     s = sub.add_parser("dictionary", help="column descriptions (default: the 20 deployed model features)")
     s.add_argument("--xlsx", required=True, help="path to LCDataDictionary.xlsx")
     s.add_argument("columns", nargs="*")
