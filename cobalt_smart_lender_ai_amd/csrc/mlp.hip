@@ -354,6 +354,157 @@ __global__ __launch_bounds__(NT) void k_mlp_forward(const float* __restrict__ X,
     __syncthreads();
   }
 }
+
+// ---------------------------------------------------------------------------- MFMA bulk inference
+// k_mlp_forward_mfma: every wave owns 32-row tiles and runs the whole network on fp32 MFMA
+// (v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation) with activations never leaving
+// registers. Each layer is computed transposed, hT = W^T . xT, so the batch rows are the MFMA's N
+// dimension: the accumulator of layer L (lane l holds column n = l & 31, output rows
+// (v & 3) + 8 (v >> 2) + 4 (l >> 5), v < 16) is directly the B operand of layer L + 1 when the K
+// steps of layer L + 1 walk the hidden units in that same order, m(s, hi) = 32 (s >> 4) +
+// 8 ((s & 15) >> 2) + 4 hi + (s & 3). The matching A operands (weights, permuted once per workgroup)
+// sit in LDS as [s / 4][lane][s % 4], one conflict-free ds_read_b128 per 4 MFMAs. Layer 1 splits
+// the features between the two lane halves (k = hi * S1 + s, S1 = ceil(F / 2)), so each lane reads
+// a contiguous run of its row. Layer 3 (16 outputs) pads M to 32 with zero weights; the 16 -> 1
+// output is a VALU dot plus one cross-half exchange. MFMAs per 32 rows: 4 S1 + 64 + 16 (120 at
+// F = 20) at 64 cycles each per SIMD.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kFwdThreads = 256;  // 4 waves, one 32-row tile each per iteration
+constexpr int kS1Max = kMaxF / 2;
+
+__host__ __device__ constexpr int fwd_lds_floats(int S1) {
+  return S1 * 256 + 16 * 256 + 4 * 256 + H1 + H2 + 32 + 32 + 4;
+}
+
+__device__ __forceinline__ int hid_of(int s, int hi) {  // hidden index of K step s, lane half hi
+  return 32 * (s >> 4) + 8 * ((s & 15) >> 2) + 4 * hi + (s & 3);
+}
+
+__global__ __launch_bounds__(kFwdThreads) void k_mlp_forward_mfma(const float* __restrict__ X, int64_t ldx, int64_t n,
+                                                                  int F, const float* __restrict__ params,
+                                                                  float* __restrict__ prob, float* __restrict__ logit) {
+  extern __shared__ float4 smv[];
+  float* sm = reinterpret_cast<float*>(smv);
+  const int S1 = (F + 1) >> 1;
+  float* A1 = sm;
+  float* A2 = A1 + S1 * 256;
+  float* A3 = A2 + 16 * 256;
+  float* b1 = A3 + 4 * 256;
+  float* b2 = b1 + H1;
+  float* b3 = b2 + H2;  // padded to 32 (zeros)
+  float* w4 = b3 + 32;  // padded to 32 (zeros)
+  float* b4 = w4 + 32;
+  {
+    float* base = const_cast<float*>(params);
+    const Views w = views(base, F);
+    for (int e = threadIdx.x; e < S1 * 256; e += kFwdThreads) {
+      const int s = e >> 8, l = (e >> 2) & 63, t = e & 3;
+      const int k = (l >> 5) * S1 + s;
+      A1[e] = k < F ? w.W1[k * H1 + 32 * t + (l & 31)] : 0.0f;
+    }
+    for (int e = threadIdx.x; e < 16 * 256; e += kFwdThreads) {
+      const int l = (e >> 2) & 63, s = ((e >> 8) << 2) | (e & 3);
+      A2[e] = w.W2[hid_of(s, l >> 5) * H2 + (l & 31)];
+    }
+    for (int e = threadIdx.x; e < 4 * 256; e += kFwdThreads) {
+      const int l = (e >> 2) & 63, s = ((e >> 8) << 2) | (e & 3);
+      A3[e] = (l & 31) < H3 ? w.W3[hid_of(s, l >> 5) * H3 + (l & 31)] : 0.0f;
+    }
+    for (int e = threadIdx.x; e < H1; e += kFwdThreads) b1[e] = w.b1[e];
+    if (threadIdx.x < 32) {
+      b2[threadIdx.x] = w.b2[threadIdx.x];
+      b3[threadIdx.x] = threadIdx.x < H3 ? w.b3[threadIdx.x] : 0.0f;
+      w4[threadIdx.x] = threadIdx.x < H3 ? w.W4[threadIdx.x] : 0.0f;
+    }
+    if (threadIdx.x == 0) b4[0] = w.b4[0];
+  }
+  __syncthreads();
+  const float4* A1v = reinterpret_cast<const float4*>(A1);
+  const float4* A2v = reinterpret_cast<const float4*>(A2);
+  const float4* A3v = reinterpret_cast<const float4*>(A3);
+  const int lane = threadIdx.x & 63, hi = lane >> 5;
+  const int kbase = hi * S1;
+  const int nk = max(0, min(S1, F - kbase));  // features this lane half contributes
+  const float bias4 = b4[0];
+  const int64_t tiles = (n + 31) >> 5;
+  const int64_t stride = (int64_t)gridDim.x * (kFwdThreads / 64);
+  for (int64_t tile = (int64_t)blockIdx.x * (kFwdThreads / 64) + (threadIdx.x >> 6); tile < tiles; tile += stride) {
+    const int64_t row = (tile << 5) + (lane & 31);
+    const bool ok = row < n;
+    float xv[kS1Max];
+#pragma unroll
+    for (int s = 0; s < kS1Max; ++s) xv[s] = (ok && s < nk) ? X[row * ldx + kbase + s] : 0.0f;
+    // layer 1: h1T[128 x 32] = W1T . xT  (+ b1 as the accumulator's initial value)
+    f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 b = *reinterpret_cast<const float4*>(b1 + 32 * t + 8 * q + 4 * hi);
+        acc[t][4 * q + 0] = b.x;
+        acc[t][4 * q + 1] = b.y;
+        acc[t][4 * q + 2] = b.z;
+        acc[t][4 * q + 3] = b.w;
+      }
+#pragma unroll
+    for (int s = 0; s < kS1Max; ++s) {
+      if (s < S1) {
+        const float4 a = A1v[s * 64 + lane];
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, xv[s], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, xv[s], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, xv[s], acc[2], 0, 0, 0);
+        acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, xv[s], acc[3], 0, 0, 0);
+      }
+    }
+    // layer 2: h2T[32 x 32] = W2T . relu(h1T), K walked in accumulator order
+    f32x16 acc2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(b2 + 8 * q + 4 * hi);
+      acc2[4 * q + 0] = b.x;
+      acc2[4 * q + 1] = b.y;
+      acc2[4 * q + 2] = b.z;
+      acc2[4 * q + 3] = b.w;
+    }
+#pragma unroll
+    for (int sg = 0; sg < 16; ++sg) {
+      const float4 a = A2v[sg * 64 + lane];
+      const int t = sg >> 2, v = (sg & 3) * 4;
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, fmaxf(acc[t][v + 0], 0.0f), acc2, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, fmaxf(acc[t][v + 1], 0.0f), acc2, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, fmaxf(acc[t][v + 2], 0.0f), acc2, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, fmaxf(acc[t][v + 3], 0.0f), acc2, 0, 0, 0);
+    }
+    // layer 3: h3T[16 (padded 32) x 32] = W3T . relu(h2T)
+    f32x16 acc3;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(b3 + 8 * q + 4 * hi);
+      acc3[4 * q + 0] = b.x;
+      acc3[4 * q + 1] = b.y;
+      acc3[4 * q + 2] = b.z;
+      acc3[4 * q + 3] = b.w;
+    }
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) {
+      const float4 a = A3v[sg * 64 + lane];
+      acc3 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, fmaxf(acc2[4 * sg + 0], 0.0f), acc3, 0, 0, 0);
+      acc3 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, fmaxf(acc2[4 * sg + 1], 0.0f), acc3, 0, 0, 0);
+      acc3 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, fmaxf(acc2[4 * sg + 2], 0.0f), acc3, 0, 0, 0);
+      acc3 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, fmaxf(acc2[4 * sg + 3], 0.0f), acc3, 0, 0, 0);
+    }
+    // output: rows 0..15 of acc3 are v < 8; each half holds 8 of the 16 units
+    float z = 0.0f;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) z = fmaf(w4[(v & 3) + 8 * (v >> 2) + 4 * hi], fmaxf(acc3[v], 0.0f), z);
+    z += __shfl_xor(z, 32);
+    z += bias4;
+    if (hi == 0 && ok) {
+      prob[row] = 1.0f / (1.0f + expf(-z));
+      if (logit) logit[row] = z;
+    }
+  }
+}
 }  // namespace
 
 COBALT_API int cobalt_mlp_num_params(int F) { return mlp_params(F); }
@@ -385,6 +536,22 @@ COBALT_API int cobalt_mlp_forward(const float* X, int64_t ldx, int64_t n, int F,
   const int64_t tiles = (n + MB - 1) / MB;
   const int grid = (int)std::min<int64_t>(tiles, 2048);
   hipLaunchKernelGGL(k_mlp_forward, dim3(grid), dim3(NT), lds, stream, X, ldx, n, F, params, prob, logit);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_mlp_forward_mfma(const float* X, int64_t ldx, int64_t n, int F, const float* params, float* prob,
+                                       float* logit, hipStream_t stream) {
+  if (F < 1 || F > kMaxF) return -1;
+  if (n < 1) return 0;
+  const size_t lds = (size_t)fwd_lds_floats((F + 1) / 2) * sizeof(float);  // 37.4 KB at F = 20
+  if (lds > 64 * 1024)
+    CK(hipFuncSetAttribute((const void*)k_mlp_forward_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int64_t tiles = (n + 31) / 32;
+  const int64_t waves = kFwdThreads / 64;
+  const int grid = (int)std::min<int64_t>((tiles + waves - 1) / waves, 1024);  // 4 workgroups per CU
+  hipLaunchKernelGGL(k_mlp_forward_mfma, dim3(grid), dim3(kFwdThreads), lds, stream, X, ldx, n, F, params, prob,
+                     logit);
   CK_LAUNCH();
   return 0;
 }

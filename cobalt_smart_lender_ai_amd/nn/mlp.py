@@ -97,9 +97,10 @@ _native.register("cobalt_mlp_train_epoch", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
-_native.register("cobalt_mlp_forward", ctypes.c_int,
-                 [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_void_p])
+for _fwd in ("cobalt_mlp_forward", "cobalt_mlp_forward_mfma"):
+    _native.register(_fwd, ctypes.c_int,
+                     [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                      ctypes.c_void_p, ctypes.c_void_p])
 
 
 def init_params(F: int, seed: int = 0) -> np.ndarray:
@@ -199,12 +200,22 @@ class MLPModel:
 
 
 def mlp_forward_gpu(X: torch.Tensor, params: torch.Tensor, out_prob: torch.Tensor,
-                    out_logit: torch.Tensor | None = None) -> None:
-    lib = _native.lib()
+                    out_logit: torch.Tensor | None = None, kernel: str = "mfma") -> None:
+    """Sigmoid probabilities (and optionally logits) of fp32 rows ``X`` [N, F] (row stride free, unit
+    column stride). ``kernel="mfma"`` (default): every layer on fp32 MFMA with activations in
+    registers; ``"fma"``: the LDS-tiled scalar-FMA forward shared with the training kernel."""
+    if kernel not in ("mfma", "fma"):
+        raise ValueError(f"kernel must be 'mfma' or 'fma', got {kernel!r}")
     N, F = X.shape
-    rc = lib.cobalt_mlp_forward(X.data_ptr(), X.stride(0), N, F, params.data_ptr(), out_prob.data_ptr(),
-                                out_logit.data_ptr() if out_logit is not None else None, _native.stream_handle())
-    _native.check(rc, "cobalt_mlp_forward")
+    if X.dtype != torch.float32 or X.stride(1) != 1 or params.dtype != torch.float32 or not params.is_contiguous():
+        raise ValueError("mlp_forward_gpu needs fp32 X with unit column stride and contiguous fp32 params")
+    if params.numel() != num_params(F) or out_prob.numel() < N or (out_logit is not None and out_logit.numel() < N):
+        raise ValueError("mlp_forward_gpu: params / output sizes do not match X")
+    lib = _native.lib()
+    name = "cobalt_mlp_forward_mfma" if kernel == "mfma" else "cobalt_mlp_forward"
+    rc = getattr(lib, name)(X.data_ptr(), X.stride(0), N, F, params.data_ptr(), out_prob.data_ptr(),
+                            out_logit.data_ptr() if out_logit is not None else None, _native.stream_handle())
+    _native.check(rc, name)
 
 
 # ----------------------------------------------------------------------------------- training

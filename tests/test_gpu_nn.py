@@ -27,6 +27,40 @@ def test_forward_kernel_matches_torch():
     np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=2e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("kernel", ["mfma", "fma"])
+@pytest.mark.parametrize("F", [1, 7, 20, 32])
+def test_forward_kernels_all_widths_strided_biased(kernel, F):
+    """Both forward kernels vs an fp64 PyTorch reference: non-zero biases, odd widths (layer-1 K
+    padding in the MFMA kernel), a row stride wider than F, N not a multiple of the 32-row tile."""
+    rng = np.random.default_rng(F)
+    n = 70_001
+    Xw = rng.normal(0, 1, (n, F + 3)).astype(np.float32)
+    p = mlp.init_params(F, seed=F)
+    for name, (o, shape) in mlp.layout(F).items():
+        if name.startswith("b"):
+            p[o:o + int(np.prod(shape))] = rng.normal(0, 0.3, int(np.prod(shape)))
+    zref = mlp.forward_torch(torch.as_tensor(p, dtype=torch.float64), torch.as_tensor(Xw[:, :F], dtype=torch.float64), F)
+    Xd = torch.as_tensor(Xw, device="cuda")[:, :F]
+    assert Xd.stride(0) == F + 3
+    prob = torch.full((n,), -1.0, device="cuda")
+    z = torch.full((n,), -1.0, device="cuda")
+    mlp.mlp_forward_gpu(Xd, torch.as_tensor(p, device="cuda"), prob, z, kernel=kernel)
+    zr = zref.numpy()
+    np.testing.assert_allclose(z.cpu().numpy(), zr, rtol=1e-5, atol=2e-5 * max(1.0, float(np.abs(zr).max())))
+    np.testing.assert_allclose(prob.cpu().numpy(), torch.sigmoid(zref).numpy(), rtol=0, atol=1e-5)
+
+
+def test_forward_mfma_equals_fma_kernel_at_scale():
+    X, _ = _toy(1_000_003, seed=5)
+    p = torch.as_tensor(mlp.init_params(20, seed=9), device="cuda")
+    Xd = torch.as_tensor(X, device="cuda")
+    a = torch.empty(len(X), device="cuda")
+    b = torch.empty(len(X), device="cuda")
+    mlp.mlp_forward_gpu(Xd, p, a, kernel="mfma")
+    mlp.mlp_forward_gpu(Xd, p, b, kernel="fma")
+    assert float((a - b).abs().max()) < 2e-6
+
+
 def test_train_epoch_kernel_matches_torch_oracle():
     X, y = _toy(203)
     cfg = mlp.MLPConfig(epochs=1, shuffle=False)
