@@ -21,6 +21,10 @@
 //
 // Inference (k_mlp_forward): 32-row tiles per workgroup iteration with the same LDS-resident
 // forward code; writes sigmoid probabilities (and optionally logits).
+//
+// MFMA versions (default from Python): k_mlp_forward_mfma (bulk inference, 7.8G rows/s) and
+// k_mlp_train_mfma (the same epoch on 4 waves, every contraction on v_mfma_f32_32x32x2_f32,
+// 9.4 us per batch-32 step vs 29.6 us here) -- see their comments below.
 #include "common.h"
 
 namespace {
@@ -505,6 +509,473 @@ __global__ __launch_bounds__(kFwdThreads) void k_mlp_forward_mfma(const float* _
     }
   }
 }
+// ------------------------------------------------------------------------------ MFMA training
+// k_mlp_train_mfma: the same epoch semantics as k_mlp_train (bit-for-bit the same algorithm, sums in
+// a different order) with every contraction on fp32 MFMA. One workgroup = 4 waves = one model;
+// wave w owns hidden tile w (units 32w..32w+31) of layer 1 and the matching K slice of layer 2.
+//   * Forward and deltas are computed transposed (batch rows = MFMA N, lane n & 31), each layer's
+//     accumulator feeding the next MFMA directly as its B operand (K walked in accumulator-register
+//     order, rowD(s, hi)), as in k_mlp_forward_mfma.
+//   * Weight gradients contract over the batch rows (K = 32 rows), reading activations and deltas
+//     that the forward / backward phases stored row-major in LDS; their accumulators come out in the
+//     layout of the weights' registers: W1 (with b1 folded in as row F, the input carrying a
+//     constant-1 column) and W2 -- values and AdamW moments -- live in registers for the whole
+//     epoch as exactly the A operands their forward MFMAs consume. W2 is mirrored in LDS for the
+//     transposed read of the layer-1 delta; W3 / b2 / b3 / W4 / b4 and their moments live in LDS.
+//   * 3 workgroup barriers per step: layer-2 partial sums, activations/deltas stored, parameters
+//     updated (the next batch is staged into the other x buffer in between).
+constexpr int kTrThreads = 256;
+constexpr int kTrMaxF = 31;  // column F of the input is the constant 1 of the folded bias
+constexpr int XP = 33, H1P = 129, W2P = 33, W3P = 17, H2P = 33, H3P = 17;
+
+struct TrLayout {
+  int MV1, MV2, W2s, W3s, sm, sched, xb, ys, h1s, d1s, h2s, d2s, h3s, d3s, d4s, red, total;
+};
+__host__ __device__ constexpr TrLayout tr_layout() {
+  TrLayout L{};
+  int o = 0;
+  L.MV1 = o;  o += 2 * 32 * H1;  // AdamW (m, v) of W1 rows 0..F-1, b1 at row F, zero rows above
+  L.MV2 = o;  o += 2 * H1 * H2;  // AdamW (m, v) of W2
+  L.W2s = o;  o += H1 * W2P;
+  L.W3s = o;  o += H2 * W3P;
+  L.sm = o;   o += 3 * 96;       // small params b2[32] b3[32] W4[32] (padded) + b4: value / m / v
+  L.sched = o;  o += 2 * kTrThreads;  // (lr, lr_t) of the next 256 steps
+  L.xb = o;   o += 2 * MB * XP;  // double-buffered batch, column F = 1, columns > F = 0
+  L.ys = o;   o += 2 * MB;
+  L.h1s = o;  o += MB * H1P;
+  L.d1s = o;  o += MB * H1P;
+  L.h2s = o;  o += MB * H2P;
+  L.d2s = o;  o += MB * H2P;
+  L.h3s = o;  o += MB * H3P;
+  L.d3s = o;  o += MB * H3P;
+  L.d4s = o;  o += MB;
+  o = (o + 3) & ~3;
+  L.red = o;  o += 4 * 16 * 64;
+  L.total = o;
+  return L;
+}
+// small-parameter slots inside L.sm (value at +0, first moment at +96, second at +192)
+constexpr int kSmB2 = 0, kSmB3 = 32, kSmW4 = 64, kSmB4 = 95;
+
+__device__ __forceinline__ int rowD(int v, int hi) { return (v & 3) + 8 * (v >> 2) + 4 * hi; }
+
+// AdamW step with the hardware square root / reciprocal (1 ulp each; no IEEE division sequence):
+// the update differs from k_mlp_train's by rounding only.
+__device__ __forceinline__ void adam_f(float& w, float& mm, float& vv, float g, float regk, const AdamStep& s) {
+  g = fmaf(regk, w, g);  // regk = 2 * lambda on regularised kernels, 0 elsewhere
+  w -= s.lr * s.wd * w;
+  mm += (g - mm) * (1.0f - s.b1);
+  vv += (g * g - vv) * (1.0f - s.b2);
+  w -= s.lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + s.eps);
+}
+
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
+
+// NQ = F / 8 + 1: layer 1 runs 4 NQ K steps (rows 0..F, the bias row F included), a compile-time
+// count so the accumulator chain has no data-dependent control flow.
+template <int NQ>
+__global__ __launch_bounds__(kTrThreads) void k_mlp_train_mfma(const float* __restrict__ X, int64_t ldx,
+                                                               const float* __restrict__ y, int64_t n, int F,
+                                                               const int32_t* __restrict__ perm,
+                                                               float* __restrict__ params, float* __restrict__ mom1,
+                                                               float* __restrict__ mom2, int64_t* __restrict__ steps,
+                                                               MlpHyper hp, float* __restrict__ loss_out,
+                                                               uint64_t* __restrict__ prof) {
+  extern __shared__ float4 smv[];
+  float* sm = reinterpret_cast<float*>(smv);
+  constexpr TrLayout L = tr_layout();
+  // optional phase timer (lane 0 of waves 0 and 3 of model 0, s_memrealtime): prof[8 * (w == 3) + i]
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph_last = 0;
+  const bool timing = prof != nullptr && blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == 192);
+#define TR_PHASE(i)                       \
+  if (timing) {                           \
+    const uint64_t now = wall_clock64();  \
+    ph[i] += now - ph_last;               \
+    ph_last = now;                        \
+  }
+  float2* MV1 = reinterpret_cast<float2*>(sm + L.MV1);
+  float2* MV2 = reinterpret_cast<float2*>(sm + L.MV2);
+  float* W2s = sm + L.W2s;
+  float* W3s = sm + L.W3s;
+  float* SP = sm + L.sm;
+  float2* sched = reinterpret_cast<float2*>(sm + L.sched);
+  float* xbuf = sm + L.xb;
+  float* ybuf = sm + L.ys;
+  float* h1s = sm + L.h1s;
+  float* d1s = sm + L.d1s;
+  float* h2s = sm + L.h2s;
+  float* d2s = sm + L.d2s;
+  float* h3s = sm + L.h3s;
+  float* d3s = sm + L.d3s;
+  float* d4s = sm + L.d4s;
+  float* red = sm + L.red;
+
+  const int model = blockIdx.x;
+  const int P = mlp_params(F);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hi = lane >> 5, li = lane & 31;
+  const Views gp = views(params + (int64_t)model * P, F);
+  const Views gm = views(mom1 + (int64_t)model * P, F);
+  const Views gv = views(mom2 + (int64_t)model * P, F);
+
+  // ---- prologue: W1 (+ b1 as row F) and W2 tile w into registers, the rest into LDS
+  float w1r[16], w2r[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int f = rowD(v, hi), c = 32 * w + li;
+    w1r[v] = f < F ? gp.W1[f * H1 + c] : (f == F ? gp.b1[c] : 0.0f);
+    MV1[f * H1 + c] = f < F ? make_float2(gm.W1[f * H1 + c], gv.W1[f * H1 + c])
+                            : (f == F ? make_float2(gm.b1[c], gv.b1[c]) : make_float2(0.0f, 0.0f));
+    const int k = 32 * w + rowD(v, hi);
+    w2r[v] = gp.W2[k * H2 + li];
+    MV2[k * H2 + li] = make_float2(gm.W2[k * H2 + li], gv.W2[k * H2 + li]);
+  }
+  for (int e = t; e < H1 * H2; e += kTrThreads) W2s[(e / H2) * W2P + (e % H2)] = gp.W2[e];
+  for (int e = t; e < H2 * H3; e += kTrThreads) W3s[(e / H3) * W3P + (e % H3)] = gp.W3[e];
+  // W3's AdamW state: waves 1 and 3 own rows rowD(v, hi), v in [0, 8) / [8, 16), of columns li < 16
+  float w3r[8], m3r[8], v3r[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = rowD(q + (w == 3 ? 8 : 0), hi) * H3 + li;
+    const bool own = (w & 1) && li < H3;
+    w3r[q] = own ? gp.W3[e] : 0.0f;
+    m3r[q] = own ? gm.W3[e] : 0.0f;
+    v3r[q] = own ? gv.W3[e] : 0.0f;
+  }
+  if (t < 96) {
+    float pv = 0.0f, pm = 0.0f, pw = 0.0f;
+    if (t < 32) {
+      pw = gp.b2[t]; pm = gm.b2[t]; pv = gv.b2[t];
+    } else if (t < 32 + H3) {
+      pw = gp.b3[t - 32]; pm = gm.b3[t - 32]; pv = gv.b3[t - 32];
+    } else if (t >= 64 && t < 64 + H3) {
+      pw = gp.W4[t - 64]; pm = gm.W4[t - 64]; pv = gv.W4[t - 64];
+    } else if (t == kSmB4) {
+      pw = gp.b4[0]; pm = gm.b4[0]; pv = gv.b4[0];
+    }
+    SP[t] = pw;
+    SP[96 + t] = pm;
+    SP[192 + t] = pv;
+  }
+  for (int e = t; e < 2 * MB * XP; e += kTrThreads) xbuf[e] = ((e % XP) == F) ? 1.0f : 0.0f;
+
+  int64_t step = steps[model];
+  const int32_t* pm = perm + (int64_t)model * n;
+  const int B = hp.batch;
+  const int64_t nb = (n + B - 1) / B;
+  float loss_acc = 0.0f;  // lane 0 of wave 0
+  // batch prefetch, two-stage: the row ids of batch b + 2 are loaded while batch b computes and
+  // batch b + 1's features (whose ids arrived during step b - 1) are in flight, so no step waits on
+  // the dependent perm -> X round trip. Element e = t + 256 q of the B x F block (<= 4 * 256).
+  float nx[4], ny = 0.0f;
+  int32_t nid[4], nyid = 0;
+  auto fetch_ids = [&](int64_t bb) {
+    const int bsz = bb < nb ? (int)min((int64_t)B, n - bb * B) : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (t + kTrThreads * q) / F;
+      nid[q] = r < bsz ? pm[bb * B + r] : -1;
+    }
+    nyid = t < bsz ? pm[bb * B + t] : -1;
+  };
+  auto fetch = [&]() {  // features of the batch whose ids are in nid
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + kTrThreads * q, f = e - (e / F) * F;
+      nx[q] = nid[q] >= 0 ? X[(int64_t)nid[q] * ldx + f] : 0.0f;
+    }
+    ny = nyid >= 0 ? y[nyid] : 0.0f;
+  };
+  auto stage = [&](int buf) {
+    float* xb = xbuf + buf * MB * XP;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + kTrThreads * q, r = e / F, f = e - r * F;
+      if (r < MB) xb[r * XP + f] = nx[q];
+    }
+    if (t < MB) ybuf[buf * MB + t] = ny;
+  };
+  __syncthreads();  // x buffer constants before the first stage
+  if (nb > 0) {
+    fetch_ids(0);
+    fetch();
+    stage(0);
+    fetch_ids(1);
+  }
+  __syncthreads();
+
+  if (timing) ph_last = wall_clock64();
+  for (int64_t b = 0; b < nb; ++b) {
+    // The lane index is laundered once per step: every LDS address below is loop-invariant, and
+    // hoisted out of the step loop they would pin ~300 VGPRs for the whole epoch (spilling).
+    int lane_ = lane;
+    asm volatile("" : "+v"(lane_));
+    const int li = lane_ & 31, hi = lane_ >> 5;
+    int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    asm volatile("" : "+s"(w));
+    const int buf = (int)(b & 1);
+    const int bs = (int)min((int64_t)B, n - b * B);
+    const float* xb = xbuf + buf * MB * XP;
+    if (b + 1 < nb) {
+      fetch();           // batch b + 1 (ids loaded during the previous step)
+      fetch_ids(b + 2);  // ids of batch b + 2
+    }
+    if ((b & (kTrThreads - 1)) == 0) {
+      // learning-rate schedule and bias correction of the next 256 steps, one step per thread (the
+      // three powf per step would otherwise cost every wave ~450 instructions per step)
+      const float st = (float)(step + t);
+      const float e = hp.staircase ? floorf(st / (float)hp.decay_steps) : st / (float)hp.decay_steps;
+      const float lr = hp.lr0 * powf(hp.decay_rate, e);
+      const float tt = st + 1.0f;
+      sched[t] = make_float2(lr, lr * sqrtf(1.0f - powf(hp.beta2, tt)) / (1.0f - powf(hp.beta1, tt)));
+      __syncthreads();
+    }
+    TR_PHASE(0)
+    AdamStep s;
+    {
+      const float2 sc = sched[b & (kTrThreads - 1)];
+      s.lr = sc.x;
+      s.lr_t = sc.y;
+      s.wd = hp.weight_decay;
+      s.b1 = hp.beta1;
+      s.b2 = hp.beta2;
+      s.eps = hp.eps;
+      s.l2 = hp.l2;
+    }
+    // ---- F1: layer 1 tile w, layer-2 partial over this tile
+    f32x16 a1 = {};
+#pragma unroll
+    for (int s_ = 0; s_ < 4 * NQ; ++s_) a1 = MFMA32(w1r[s_], xb[li * XP + rowD(s_, hi)], a1);
+    f32x16 a2 = {};
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float h = fmaxf(a1[v], 0.0f);
+      h1s[li * H1P + 32 * w + rowD(v, hi)] = h;
+      a2 = MFMA32(w2r[v], h, a2);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      reinterpret_cast<float4*>(red)[(w * 4 + q) * 64 + lane] = make_float4(a2[4 * q], a2[4 * q + 1], a2[4 * q + 2], a2[4 * q + 3]);
+    TR_PHASE(1)
+    __syncthreads();
+    TR_PHASE(2)
+    // ---- F2 (every wave, redundantly): layer 2 sum, layer 3, output, deltas 3 / 2, delta 1 tile w
+    float h2[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float4 r = reinterpret_cast<const float4*>(red)[(ww * 4 + q) * 64 + lane];
+        acc.x += r.x;
+        acc.y += r.y;
+        acc.z += r.z;
+        acc.w += r.w;
+      }
+      h2[4 * q + 0] = fmaxf(acc.x + SP[kSmB2 + rowD(4 * q + 0, hi)], 0.0f);
+      h2[4 * q + 1] = fmaxf(acc.y + SP[kSmB2 + rowD(4 * q + 1, hi)], 0.0f);
+      h2[4 * q + 2] = fmaxf(acc.z + SP[kSmB2 + rowD(4 * q + 2, hi)], 0.0f);
+      h2[4 * q + 3] = fmaxf(acc.w + SP[kSmB2 + rowD(4 * q + 3, hi)], 0.0f);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 a3;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) a3[v] = SP[kSmB3 + rowD(v, hi)];  // zero above unit 15
+#pragma unroll
+    for (int s_ = 0; s_ < 16; ++s_) a3 = MFMA32(li < H3 ? W3s[rowD(s_, hi) * W3P + li] : 0.0f, h2[s_], a3);
+    float h3[8];
+    float z = 0.0f;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      h3[v] = fmaxf(a3[v], 0.0f);
+      z = fmaf(SP[kSmW4 + rowD(v, hi)], h3[v], z);
+    }
+    z += __shfl_xor(z, 32);
+    z += SP[kSmB4];
+    const float yy = ybuf[buf * MB + li];
+    const float pr = __builtin_amdgcn_rcpf(1.0f + __expf(-z));
+    const float d4 = li < bs ? (pr - yy) / (float)bs : 0.0f;
+    float d3[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) d3[v] = h3[v] > 0.0f ? SP[kSmW4 + rowD(v, hi)] * d4 : 0.0f;
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 a2d = {};
+#pragma unroll
+    for (int s_ = 0; s_ < 8; ++s_) a2d = MFMA32(W3s[li * W3P + rowD(s_, hi)], d3[s_], a2d);
+    float d2[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) d2[v] = h2[v] > 0.0f ? a2d[v] : 0.0f;
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 a1d = {};
+#pragma unroll
+    for (int s_ = 0; s_ < 16; ++s_) a1d = MFMA32(W2s[(32 * w + li) * W2P + rowD(s_, hi)], d2[s_], a1d);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int o = li * H1P + 32 * w + rowD(v, hi);
+      d1s[o] = h1s[o] > 0.0f ? a1d[v] : 0.0f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (w == 0) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        h2s[li * H2P + rowD(v, hi)] = h2[v];
+        d2s[li * H2P + rowD(v, hi)] = d2[v];
+      }
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        h3s[li * H3P + rowD(v, hi)] = h3[v];
+        d3s[li * H3P + rowD(v, hi)] = d3[v];
+      }
+      if (hi == 0) d4s[li] = d4;
+    }
+    TR_PHASE(3)
+    __syncthreads();
+    TR_PHASE(4)
+    // ---- G: weight gradients over the batch rows + AdamW. VALU updates are interleaved with the
+    // next gradient chain so they issue between its MFMAs: W1 with dW2, W2 with dW3 (waves 1, 3).
+    const float l2x2 = 2.0f * s.l2;
+    f32x16 g1 = {};
+#pragma unroll
+    for (int s_ = 0; s_ < 16; ++s_) {
+      const int r = 2 * s_ + hi;
+      g1 = MFMA32(xb[r * XP + li], d1s[r * H1P + 32 * w + li], g1);
+    }
+    f32x16 g2 = {};
+#pragma unroll
+    for (int s_ = 0; s_ < 16; ++s_) {
+      const int r = 2 * s_ + hi;
+      g2 = MFMA32(h1s[r * H1P + 32 * w + li], d2s[r * H2P + li], g2);
+      if (s_ < 4 * NQ) {  // registers above 4 NQ hold rows > F only (zero weight, gradient, moments)
+        const int f = rowD(s_, hi);  // rows F+1 .. 4 NQ stay zero the same way
+        float2 mv = MV1[f * H1 + 32 * w + li];
+        adam_f(w1r[s_], mv.x, mv.y, g1[s_], f < F ? l2x2 : 0.0f, s);
+        MV1[f * H1 + 32 * w + li] = mv;
+      }
+    }
+    auto adam_w2 = [&](int v) {
+      const int k = 32 * w + rowD(v, hi);
+      float2 mv = MV2[k * H2 + li];
+      adam_f(w2r[v], mv.x, mv.y, g2[v], l2x2, s);
+      MV2[k * H2 + li] = mv;
+      W2s[k * W2P + li] = w2r[v];
+    };
+    if (w & 1) {  // W3 (columns j = li < 16): waves 1 and 3 both form the gradient, each updates half
+      f32x16 g3 = {};
+#pragma unroll
+      for (int s_ = 0; s_ < 16; ++s_) {
+        const int r = 2 * s_ + hi;
+        g3 = MFMA32(h2s[r * H2P + li], li < H3 ? d3s[r * H3P + li] : 0.0f, g3);
+        adam_w2(s_);
+      }
+      if (li < H3) {
+        if (w == 1) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            adam_f(w3r[q], m3r[q], v3r[q], g3[q], l2x2, s);
+            W3s[rowD(q, hi) * W3P + li] = w3r[q];
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            adam_f(w3r[q], m3r[q], v3r[q], g3[8 + q], l2x2, s);
+            W3s[rowD(8 + q, hi) * W3P + li] = w3r[q];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) adam_w2(v);
+      if (w == 0) {  // batch loss (reported only): mean BCE from the logit over the bs real rows
+        float l = (hi == 0 && li < bs) ? fmaxf(z, 0.0f) - z * yy + __logf(1.0f + __expf(-fabsf(z))) : 0.0f;
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) l += __shfl_xor(l, o);
+        if (lane == 0) loss_acc += l / (float)bs;
+      } else {  // wave 2: b2 (lanes 0..31), b3 (32..47), W4 (48..63), b4 (lane 48 too)
+        float gg = 0.0f;
+        int slot;
+        if (lane < 32) {
+          slot = kSmB2 + lane;
+#pragma unroll
+          for (int r = 0; r < MB; ++r) gg += d2s[r * H2P + lane];
+        } else if (lane < 48) {
+          slot = kSmB3 + lane - 32;
+#pragma unroll
+          for (int r = 0; r < MB; ++r) gg += d3s[r * H3P + lane - 32];
+        } else {
+          slot = kSmW4 + lane - 48;
+          float g4 = 0.0f;
+#pragma unroll
+          for (int r = 0; r < MB; ++r) {
+            const float d = d4s[r];
+            gg = fmaf(h3s[r * H3P + lane - 48], d, gg);
+            g4 += d;
+          }
+          if (lane == 48) adam_f(SP[kSmB4], SP[96 + kSmB4], SP[192 + kSmB4], g4, 0.0f, s);
+        }
+        adam_f(SP[slot], SP[96 + slot], SP[192 + slot], gg, 0.0f, s);
+      }
+    }
+    if (b + 1 < nb) stage(buf ^ 1);
+    ++step;
+    TR_PHASE(5)
+    __syncthreads();
+    TR_PHASE(6)
+  }
+#undef TR_PHASE
+  if (timing)
+    for (int i = 0; i < 7; ++i) prof[8 * (threadIdx.x == 192) + i] += ph[i];
+  // ---- epilogue: parameters and moments back to the flat layout
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int f = rowD(v, hi), c = 32 * w + li;
+    const float2 mv1 = MV1[f * H1 + c];
+    if (f < F) {
+      gp.W1[f * H1 + c] = w1r[v];
+      gm.W1[f * H1 + c] = mv1.x;
+      gv.W1[f * H1 + c] = mv1.y;
+    } else if (f == F) {
+      gp.b1[c] = w1r[v];
+      gm.b1[c] = mv1.x;
+      gv.b1[c] = mv1.y;
+    }
+    const int k = 32 * w + rowD(v, hi);
+    const float2 mv2 = MV2[k * H2 + li];
+    gp.W2[k * H2 + li] = w2r[v];
+    gm.W2[k * H2 + li] = mv2.x;
+    gv.W2[k * H2 + li] = mv2.y;
+  }
+  if ((w & 1) && li < H3) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = rowD(q + (w == 3 ? 8 : 0), hi) * H3 + li;
+      gp.W3[e] = w3r[q];
+      gm.W3[e] = m3r[q];
+      gv.W3[e] = v3r[q];
+    }
+  }
+  if (t < 96) {
+    float* dst[3] = {nullptr, nullptr, nullptr};
+    if (t < 32) {
+      dst[0] = gp.b2 + t; dst[1] = gm.b2 + t; dst[2] = gv.b2 + t;
+    } else if (t < 32 + H3) {
+      dst[0] = gp.b3 + t - 32; dst[1] = gm.b3 + t - 32; dst[2] = gv.b3 + t - 32;
+    } else if (t >= 64 && t < 64 + H3) {
+      dst[0] = gp.W4 + t - 64; dst[1] = gm.W4 + t - 64; dst[2] = gv.W4 + t - 64;
+    } else if (t == kSmB4) {
+      dst[0] = gp.b4; dst[1] = gm.b4; dst[2] = gv.b4;
+    }
+    if (dst[0]) {
+      *dst[0] = SP[t];
+      *dst[1] = SP[96 + t];
+      *dst[2] = SP[192 + t];
+    }
+  }
+  if (t == 0) {
+    steps[model] = step;
+    loss_out[model] = loss_acc;
+  }
+}
+#undef MFMA32
 }  // namespace
 
 COBALT_API int cobalt_mlp_num_params(int F) { return mlp_params(F); }
@@ -522,6 +993,31 @@ COBALT_API int cobalt_mlp_train_epoch(const float* X, int64_t ldx, const float* 
   CK(hipFuncSetAttribute((const void*)k_mlp_train, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_mlp_train, dim3(n_models), dim3(NT), lds, stream, X, ldx, y, n, F, perm, params, m, v, steps,
                      hp, loss_out, prof);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_mlp_train_epoch_mfma(const float* X, int64_t ldx, const float* y, int64_t n, int F,
+                                           const int32_t* perm, float* params, float* m, float* v, int64_t* steps,
+                                           const void* hyper, int n_models, float* loss_out, uint64_t* prof,
+                                           hipStream_t stream) {
+  if (F < 1 || F > kTrMaxF) return -1;
+  if (n < 1 || n_models < 1) return 0;
+  MlpHyper hp = *static_cast<const MlpHyper*>(hyper);
+  if (hp.batch < 1 || hp.batch > MB || hp.decay_steps < 1) return -2;
+  const size_t lds = (size_t)tr_layout().total * sizeof(float);  // 157 KB
+  static_assert(tr_layout().total * sizeof(float) <= 160 * 1024, "trainer LDS image exceeds 160 KB");
+  const void* fn = nullptr;
+  switch (F / 8 + 1) {
+    case 1: fn = (const void*)k_mlp_train_mfma<1>; break;
+    case 2: fn = (const void*)k_mlp_train_mfma<2>; break;
+    case 3: fn = (const void*)k_mlp_train_mfma<3>; break;
+    default: fn = (const void*)k_mlp_train_mfma<4>; break;
+  }
+  CK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* args[] = {(void*)&X, (void*)&ldx, (void*)&y, (void*)&n, (void*)&F, (void*)&perm, (void*)&params, (void*)&m,
+                  (void*)&v, (void*)&steps, (void*)&hp, (void*)&loss_out, (void*)&prof};
+  CK(hipLaunchKernel(fn, dim3(n_models), dim3(kTrThreads), args, lds, stream));
   CK_LAUNCH();
   return 0;
 }

@@ -6,9 +6,12 @@ staircase decays of ``int(len(X_train)/32)`` steps, 50 epochs, batch 32, Keras A
 (weight_decay 0.004, beta 0.9/0.999, eps 1e-7), Glorot-uniform kernels / zero biases,
 EarlyStopping(monitor="val_precision", mode="max", patience=5, restore_best_weights=True).
 
-Execution: on the GPU every epoch is ONE launch of the fused LDS-resident trainer
-(``csrc/mlp.hip``: weights, AdamW moments and activations stay on one CU for all steps); ``fit_many``
-trains several models (seeds / learning rates) in the same launch, one per CU. On CPU the same
+Execution: on the GPU every epoch is ONE launch of a fused trainer that keeps weights, AdamW
+moments and activations on one CU for all steps (``csrc/mlp.hip``). The default is the fp32-MFMA
+trainer (``k_mlp_train_mfma``, F <= 31: 4 waves per model, W1/W2 in registers as the MFMA operands
+they are, 9.4 us per batch-32 step); ``kernel="fma"`` selects the 1024-thread scalar-FMA trainer
+(29.6 us per step). ``fit_many`` trains several models (seeds / learning rates) in the same launch,
+one per CU. Bulk inference runs on fp32 MFMA as well (``k_mlp_forward_mfma``). On CPU the same
 algorithm runs in plain PyTorch (:func:`train_epoch_torch`), which is also the numerics oracle of
 the kernel. History keys follow Keras 3 naming (``loss``, ``val_loss``, ``val_accuracy``,
 ``val_Precision``, ``val_Recall``, ``val_AUC``): the reference's monitor ``"val_precision"`` is not
@@ -33,6 +36,7 @@ log = logging.getLogger(__name__)
 
 H1, H2, H3 = 128, 32, 16
 MAX_F = 32
+MAX_F_MFMA = 31  # the MFMA trainer folds b1 into W1 through a constant-1 input column
 
 
 def num_params(F: int) -> int:
@@ -94,6 +98,10 @@ assert ctypes.sizeof(_Hyper) == 48
 
 _native.register("cobalt_mlp_num_params", ctypes.c_int, [ctypes.c_int])
 _native.register("cobalt_mlp_train_epoch", ctypes.c_int,
+                 [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
+_native.register("cobalt_mlp_train_epoch_mfma", ctypes.c_int,
                  [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p])
@@ -237,16 +245,21 @@ def _val_metrics(y: np.ndarray, p: np.ndarray) -> dict[str, float]:
 
 
 def fit_many(X_train, y_train, X_val=None, y_val=None, cfg: MLPConfig | None = None, seeds=(0,),
-             device=None, feature_names=None) -> tuple[list[MLPModel], list[dict]]:
+             device=None, feature_names=None, kernel: str | None = None) -> tuple[list[MLPModel], list[dict]]:
     """Train ``len(seeds)`` independent models (same data, different init/shuffle seeds).
 
-    On the GPU all models train in the same launch (one workgroup each)."""
+    On the GPU all models train in the same launch (one workgroup each). ``kernel``: ``"mfma"``
+    (default for F <= 31: 4 waves per model, every contraction on fp32 MFMA) or ``"fma"`` (1024
+    threads per model, scalar FMA through LDS)."""
     cfg = cfg or MLPConfig()
     X = np.ascontiguousarray(np.asarray(X_train, dtype=np.float32))
     y = np.asarray(y_train, dtype=np.float32).reshape(-1)
     N, F = X.shape
     if F > MAX_F:
         raise ValueError(f"at most {MAX_F} input features")
+    kernel = kernel or ("mfma" if F <= MAX_F_MFMA else "fma")
+    if kernel not in ("mfma", "fma") or (kernel == "mfma" and F > MAX_F_MFMA):
+        raise ValueError(f"kernel must be 'fma' or 'mfma' (F <= {MAX_F_MFMA}), got {kernel!r} at F={F}")
     G = len(seeds)
     dev = torch.device(device) if device is not None else (
         torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
@@ -287,10 +300,16 @@ def fit_many(X_train, y_train, X_val=None, y_val=None, cfg: MLPConfig | None = N
         perms = np.stack([r.permutation(N) if cfg.shuffle else np.arange(N) for r in rngs]).astype(np.int32)
         if dev.type == "cuda":
             permd = torch.as_tensor(perms, device=dev)
-            rc = lib.cobalt_mlp_train_epoch(Xd.data_ptr(), F, yd.data_ptr(), N, F, permd.data_ptr(), pd_.data_ptr(),
-                                            md.data_ptr(), vd.data_ptr(), steps.data_ptr(), ctypes.byref(hp), G,
-                                            loss.data_ptr(), None, _native.stream_handle())
-            _native.check(rc, "cobalt_mlp_train_epoch")
+            if kernel == "mfma":
+                rc = lib.cobalt_mlp_train_epoch_mfma(Xd.data_ptr(), F, yd.data_ptr(), N, F, permd.data_ptr(),
+                                                     pd_.data_ptr(), md.data_ptr(), vd.data_ptr(), steps.data_ptr(),
+                                                     ctypes.byref(hp), G, loss.data_ptr(), None,
+                                                     _native.stream_handle())
+            else:
+                rc = lib.cobalt_mlp_train_epoch(Xd.data_ptr(), F, yd.data_ptr(), N, F, permd.data_ptr(),
+                                                pd_.data_ptr(), md.data_ptr(), vd.data_ptr(), steps.data_ptr(),
+                                                ctypes.byref(hp), G, loss.data_ptr(), None, _native.stream_handle())
+            _native.check(rc, f"mlp train epoch ({kernel})")
             losses = (loss / nb).cpu().numpy()
             cur = pd_.cpu().numpy()
         else:
