@@ -117,7 +117,8 @@ def main() -> None:
             "scaling": a.scaling,
             "vs_baseline": None if BASELINE_ROWS_PER_S is None else value / BASELINE_ROWS_PER_S,
             "dtype": "fp32",
-            "precision": "fp32 features, fp64 gradients, exact int64 fixed-point histogram sums",
+            "precision": "fp32 features; fp64 gradient math quantised to 17-bit dithered (unbiased) fixed point; "
+                         "exact int64 histogram sums; fp64 split gains",
             "data": "synthetic LendingClub-shaped (20 deployed features, 12.9% positives), generated on device",
             "config": {
                 "model": f"GBDT binary:logistic, {a.trees} trees depth {a.depth} eta 0.05 gamma 5 lambda 1 max_bin 256 "
