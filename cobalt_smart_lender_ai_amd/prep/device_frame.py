@@ -39,7 +39,8 @@ class DCol:
     data: torch.Tensor        # [N] on the frame's device
     dtype: str                # pandas dtype on export: "float64" | "int64" | "bool" | "object"
     vocab: list | None = None  # "c": code -> value
-    src: object = None        # "h": the host Arrow column (ORIGINAL rows; decoded lazily through rowid)
+    src: object = None        # "h": the ORIGINAL rows' text (host Arrow column, or csv_gpu.DeviceStrings in
+                              # HBM), decoded lazily through rowid
 
     def null_mask(self) -> torch.Tensor:
         if self.kind == "f":
@@ -107,6 +108,8 @@ class DeviceFrame:
 
         c = self.cols[name]
         rid = self.rowid if rows is None else self.rowid[rows]
+        if hasattr(c.src, "arrow"):  # GPU-ingested text (csv_gpu.DeviceStrings, in HBM): only these rows move
+            return c.src.take(rid)
         return pc.take(c.src, rid.cpu().numpy())
 
     def as_categorical(self, name: str) -> DCol:
@@ -166,13 +169,29 @@ class DeviceFrame:
         return cls(cols, n, dev)
 
     @classmethod
-    def read_csv(cls, path_or_bytes, device, threads: bool = True) -> "DeviceFrame":
-        """Parse a (optionally gzipped) CSV with pyarrow's multithreaded C++ reader, pandas' missing
-        values, then upload every column."""
+    def read_csv(cls, path_or_bytes, device, threads: bool = True, engine: str = "auto",
+                 timings: dict | None = None) -> "DeviceFrame":
+        """Parse a (optionally gzipped) CSV with pandas' missing values into device columns.
+
+        ``engine="gpu"`` (the default on a GPU device, ``"auto"``): the bytes go to HBM and the
+        tokenizer / parser / dictionary encoder of ``csrc/csv.hip`` run there (prep/csv_gpu.py); a file
+        it cannot lay out as a rectangle falls back to ``"arrow"``: pyarrow's multithreaded C++ reader
+        on the host, then every column is uploaded."""
         import io
 
         import pyarrow as pa
         import pyarrow.csv as pcsv
+
+        if engine not in ("auto", "gpu", "arrow"):
+            raise ValueError(f"engine must be auto, gpu or arrow, got {engine!r}")
+        if engine in ("auto", "gpu") and torch.device(device).type == "cuda":
+            from .csv_gpu import CsvLayoutError, read_csv_gpu
+
+            try:
+                return read_csv_gpu(path_or_bytes, device, timings=timings)
+            except CsvLayoutError:
+                if engine == "gpu":
+                    raise
 
         src = path_or_bytes
         if isinstance(src, (bytes, bytearray)):

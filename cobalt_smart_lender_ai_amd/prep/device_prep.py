@@ -254,14 +254,19 @@ def tree_training_matrix(tree: DeviceFrame, drop: list[str] = (), label: str = "
     return t.matrix(names), t[label].data.to(torch.float32), names
 
 
-def run_device_prep(src, device="cuda", reference_date=None, preset: str = "script") -> dict:
-    """Raw CSV (path or bytes) -> cleaned -> stage 2 -> (tree, nn) DeviceFrames, with stage timings."""
+def run_device_prep(src, device="cuda", reference_date=None, preset: str = "script", engine: str = "auto") -> dict:
+    """Raw CSV (path or bytes) -> cleaned -> stage 2 -> (tree, nn) DeviceFrames, with stage timings.
+    ``engine``: the CSV reader (DeviceFrame.read_csv: "auto" = on the GPU when there is one)."""
     dev = torch.device(device)
     t = {}
+    ing: dict = {}
     t0 = time.perf_counter()
-    raw = DeviceFrame.read_csv(src, dev)
+    raw = DeviceFrame.read_csv(src, dev, engine=engine, timings=ing)
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
     t["ingest"] = time.perf_counter() - t0
+    for k in ("read", "tokenize", "parse", "columns"):
+        if k in ing:
+            t["ingest_" + k] = ing[k]
     t1 = time.perf_counter()
     c1 = device_clean_data_flow(raw, preset=preset)
     t["stage1"] = time.perf_counter() - t1

@@ -70,12 +70,21 @@ def main() -> None:
     t_bins = time.perf_counter() - tb
     dtimes = {k: round(v, 3) for k, v in res["timings"].items()}
     log(f"device path {t_dev:.2f} s {dtimes} + matrix/binning {t_bins:.2f} s; tree {res['tree'].shape}")
+    arrow_ingest = None
+    if dev.type == "cuda":  # the host-parsed ingest it replaces (pyarrow C++ reader + uploads), for reference
+        del res["clean"], res["stage2"]
+        ta = time.perf_counter()
+        from cobalt_smart_lender_ai_amd.prep.device_frame import DeviceFrame
+        DeviceFrame.read_csv(a.csv, dev, engine="arrow")
+        torch.cuda.synchronize(dev)
+        arrow_ingest = round(time.perf_counter() - ta, 3)
+        log(f"pyarrow ingest (previous engine) {arrow_ingest:.2f} s")
 
     out = {"metric": "preprocessing wall time, raw CSV -> tree/NN datasets (+ GBDT bins on device)",
            "raw_rows": shape[0], "raw_cols": shape[1], "csv_gb": round(size_gb, 3),
            "tree_shape": list(res["tree"].shape), "nn_shape": list(res["nn"].shape),
            "device_s": round(t_dev, 3), "device_stages_s": dtimes, "device_matrix_and_bins_s": round(t_bins, 3),
-           "gbdt_features": len(names), "device": str(dev)}
+           "gbdt_features": len(names), "device": str(dev), "arrow_engine_ingest_s": arrow_ingest}
     if not a.skip_pandas:
         t0 = time.perf_counter()
         df = pd.read_csv(a.csv, low_memory=False, float_precision="round_trip")

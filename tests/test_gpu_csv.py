@@ -1,0 +1,108 @@
+"""GPU CSV reader (csrc/csv.hip, prep/csv_gpu.py) vs the pyarrow reader it replaces (run with -m gpu)."""
+import numpy as np
+import pytest
+import torch
+
+from cobalt_smart_lender_ai_amd.prep.device_frame import DeviceFrame
+
+pytestmark = pytest.mark.gpu
+
+
+def _decoded(frame, name):
+    c = frame[name]
+    if c.kind == "c":
+        codes = c.data.cpu().numpy()
+        return [c.vocab[k] if k >= 0 else None for k in codes]
+    return frame.host_strings(name).to_pylist()
+
+
+def assert_frames_identical(a: DeviceFrame, b: DeviceFrame):
+    assert a.columns == b.columns
+    assert a.n == b.n
+    for name in a.columns:
+        ca, cb = a[name], b[name]
+        assert (ca.kind in "ch") == (cb.kind in "ch"), name
+        assert ca.dtype == cb.dtype, (name, ca.dtype, cb.dtype)
+        if ca.kind in "ch":
+            assert ca.kind == cb.kind, name
+            assert _decoded(a, name) == _decoded(b, name), name
+        elif ca.kind == "f":
+            x, y = ca.data.cpu().numpy(), cb.data.cpu().numpy()
+            nx, ny = np.isnan(x), np.isnan(y)
+            assert np.array_equal(nx, ny), name
+            assert np.array_equal(x[~nx].view(np.int64), y[~ny].view(np.int64)), name  # bitwise, incl. -0.0
+        else:
+            assert ca.kind == cb.kind and torch.equal(ca.data, cb.data), name
+
+
+def _tricky_csv(n: int, seed: int, crlf: bool) -> bytes:
+    rng = np.random.default_rng(seed)
+    nl = "\r\n" if crlf else "\n"
+    words = ["alpha", "beta", "Gamma, Inc.", 'say "hi"', "multi\nline", "ünïcødé", "NA", "", "x"]
+    rows = ['id,name,amount,flag,flag_null,note,empty,mixed,intnull,big,expo,neg0,plus,uniq,"quoted, header"']
+    for i in range(n):
+        def q(s):
+            return '"' + s.replace('"', '""') + '"' if any(ch in s for ch in ',"\n') or rng.random() < 0.1 else s
+        amount = rng.choice([f"{rng.normal() * 1e4:.4f}", "", "NaN", "-0.0", f"{rng.integers(-99, 99)}", "1.5e-3"])
+        rows.append(",".join([
+            str(i),
+            q(str(rng.choice(words))),
+            amount,
+            str(rng.choice(["True", "False", "true", "FALSE"])),
+            str(rng.choice(["True", "False", ""])),
+            q(f"note {rng.integers(0, 50)}, {rng.choice(words)}"),
+            "",
+            str(rng.choice(["12", "abc", "3.5", ""])),
+            str(rng.choice(["7", "", "-0", "123"])),
+            str(rng.choice(["123456789012345678901234", "5", "9007199254740993"])),
+            str(rng.choice(["1e3", "2.5E+2", "-7e-2", "0.1"])),
+            "-0",
+            str(rng.choice(["+5", "6"])),
+            q(f"user-{rng.integers(0, 1 << 40):x}, {i}"),
+            str(rng.choice(["12.5", "7"])),
+        ]))
+    return (nl.join(rows) + nl).encode("utf-8")
+
+
+@pytest.mark.parametrize("crlf", [False, True])
+def test_tricky_csv_matches_pyarrow(crlf):
+    data = _tricky_csv(3001, 3 + crlf, crlf)
+    t = {}
+    g = DeviceFrame.read_csv(data, "cuda", engine="gpu", timings=t)
+    a = DeviceFrame.read_csv(data, "cuda", engine="arrow")
+    assert t["rows"] == 3001 and t["cols"] == 15
+    assert_frames_identical(g, a)
+    assert g["uniq"].kind == "h" and g["name"].kind == "c"
+    assert g["neg0"].dtype == "int64" and g["plus"].dtype == "float64" and g["big"].dtype == "float64"
+    assert g["flag"].kind == "b" and g["flag_null"].dtype == "float64"
+
+
+def test_no_trailing_newline_and_small_frame():
+    data = b'a,b,c\n1,"x,y",2.5\n2,,3'
+    g = DeviceFrame.read_csv(data, "cuda", engine="gpu")
+    a = DeviceFrame.read_csv(data, "cuda", engine="arrow")
+    assert_frames_identical(g, a)
+    assert g.n == 2 and g["b"].kind == "c"
+
+
+def test_ragged_file_falls_back():
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import CsvLayoutError
+
+    data = b"a,b\n1,2\n3\n4,5\n"
+    with pytest.raises(CsvLayoutError):
+        DeviceFrame.read_csv(data, "cuda", engine="gpu")
+    auto = DeviceFrame.read_csv(b"a,b\n1,2\n\n3,4\n", "cuda")  # blank line: pyarrow fallback
+    assert auto.n == 2
+
+
+def test_synthetic_raw_lendingclub_matches_pyarrow(tmp_path):
+    from cobalt_smart_lender_ai_amd.dataio.synth_raw import make_raw_lendingclub
+
+    df = make_raw_lendingclub(200_000, seed=5, n_cols=143)
+    path = tmp_path / "raw.csv"
+    df.to_csv(path, index=False)
+    t = {}
+    g = DeviceFrame.read_csv(str(path), "cuda", engine="gpu", timings=t)
+    a = DeviceFrame.read_csv(str(path), "cuda", engine="arrow")
+    assert t["cols"] == 143
+    assert_frames_identical(g, a)
