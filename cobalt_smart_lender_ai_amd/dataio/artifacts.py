@@ -103,7 +103,8 @@ class S3Store(ArtifactStore):
         return self.client.get_object(Bucket=self.bucket, Key=key)["Body"].read()
 
     def put_bytes(self, key: str, data: bytes) -> None:  # pragma: no cover
-        self.client.put_object(Bucket=self.bucket, Key=key, Body=data)
+        self.client.put_object(Bucket=self.bucket, Key=key,
+                               Body=data if isinstance(data, (bytes, bytearray)) else bytes(data))
 
     def exists(self, key: str) -> bool:  # pragma: no cover
         try:

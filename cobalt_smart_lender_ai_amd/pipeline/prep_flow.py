@@ -38,7 +38,15 @@ def _engine(engine: str | None, device) -> str:
 
 
 def _write_frame(store: ArtifactStore, dfr, key: str) -> None:
-    store.write_csv(dfr.to_pandas(), key)
+    """The artifact CSV of a device frame: formatted on the GPU (byte-identical to pandas.to_csv,
+    prep/csv_gpu.frame_to_csv_bytes), pandas off the GPU."""
+    from ..prep.csv_gpu import frame_to_csv_bytes
+
+    data = frame_to_csv_bytes(dfr)
+    if data is None:
+        store.write_csv(dfr.to_pandas(), key)
+    else:
+        store.put_bytes(key, data)
 
 
 def run_clean(store: ArtifactStore, use_sample: bool = True, device=None, preset: str = "script",

@@ -350,3 +350,149 @@ def _string_columns(lib, stream, buf, fend, N, C, str_cols: list[int], dev, shar
                          dev, as_device=True)
             out[c] = DCol("h", H[j], "object", src=txt)
     return out
+
+
+# ------------------------------------------------------------------------------------------ writer
+_native.register("cobalt_csv_wcol_size", ctypes.c_int, [])
+_native.register("cobalt_csv_write_len", ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P])
+_native.register("cobalt_csv_write_bytes", ctypes.c_int, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P])
+
+W_FLOAT, W_INT, W_BOOL, W_BOOLINT, W_VOCAB, W_TEXT = range(6)
+
+
+class _WCol(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("pad", ctypes.c_int32), ("data", ctypes.c_void_p), ("off", ctypes.c_void_p),
+                ("text", ctypes.c_void_p), ("valid", ctypes.c_void_p), ("quoted", ctypes.c_void_p),
+                ("rowid", ctypes.c_void_p), ("pad2", ctypes.c_int64)]
+
+
+assert ctypes.sizeof(_WCol) == 64
+
+
+def csv_escape(s: str) -> str:
+    """The csv module's QUOTE_MINIMAL (pandas.to_csv's default) for one field."""
+    if any(ch in s for ch in ',"\n\r'):
+        return '"' + s.replace('"', '""') + '"'
+    return s
+
+
+def _text_buffers(src, dev):
+    """(bytes, int64 offsets, uint8 valid, uint8 quoted | None) on the device for a string column source."""
+    if hasattr(src, "arrow"):  # DeviceStrings
+        return src.data, src.off, src.valid.to(torch.uint8), src.quoted.to(torch.uint8)
+    import pyarrow as pa
+
+    arr = src.combine_chunks() if hasattr(src, "combine_chunks") else src
+    arr = arr.cast(pa.large_string())
+    valid = np.asarray(arr.is_valid().to_numpy(zero_copy_only=False), dtype=np.uint8)
+    bufs = arr.buffers()
+    off = np.frombuffer(bufs[1], dtype=np.int64, count=len(arr) + 1, offset=arr.offset * 8).copy()
+    data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None else np.zeros(0, np.uint8)
+    data = data[off[0]:off[-1]].copy() if len(data) else np.zeros(1, np.uint8)
+    off -= off[0]
+    return (torch.from_numpy(data).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(valid).to(dev), None)
+
+
+def frame_to_csv_bytes(frame, timings: dict | None = None) -> memoryview | bytes | None:
+    """``frame.to_pandas().to_csv(index=False)`` as UTF-8 bytes, formatted on the GPU (``csrc/csv.hip``
+    writer), as a bytes-like buffer. The rare float the device cannot certify (subnormal, beyond
+    1e290, a decimal tie within the double-double error bound) is formatted by Python's repr and spliced
+    in. None off the GPU. Cumulative phase times go to ``timings`` when given."""
+    dev = frame.device
+    if dev.type != "cuda":
+        return None
+    lib = _native.lib()
+    stream = _native.stream_handle()
+    t0 = time.perf_counter()
+    names = frame.columns
+    C, N = len(names), frame.n
+    header = (",".join(csv_escape(str(n)) for n in names) + "\n").encode("utf-8")
+    if C == 0:
+        return header
+    descs = (_WCol * C)()
+    keep = []
+    fdata: dict[int, torch.Tensor] = {}
+    for j, name in enumerate(names):
+        c = frame[name]
+        d = descs[j]
+        if c.kind == "f":
+            v = c.data.to(torch.float64).contiguous()
+            keep.append(v)
+            fdata[j] = v
+            d.data = v.data_ptr()
+            d.kind = W_INT if (c.dtype == "int64" and not bool(torch.isnan(v).any())) else W_FLOAT
+        elif c.kind == "b":
+            v = c.data.to(torch.uint8).contiguous()
+            keep.append(v)
+            d.data = v.data_ptr()
+            d.kind = W_BOOL if c.dtype == "bool" else W_BOOLINT
+        elif c.kind == "c":
+            codes = c.data.to(torch.int32).contiguous()
+            txt = [csv_escape(str(x)).encode("utf-8") for x in c.vocab]
+            offs = np.zeros(len(txt) + 1, dtype=np.int64)
+            np.cumsum([len(t) for t in txt], out=offs[1:])
+            vt = torch.from_numpy(np.frombuffer(b"".join(txt) or b"\0", dtype=np.uint8).copy()).to(dev)
+            vo = torch.from_numpy(offs).to(dev)
+            keep += [codes, vt, vo]
+            d.kind, d.data, d.off, d.text = W_VOCAB, codes.data_ptr(), vo.data_ptr(), vt.data_ptr()
+        else:  # "h": text of the ingest rows, indexed through rowid
+            data, off, valid, quoted = _text_buffers(c.src, dev)
+            rid = frame.rowid.to(torch.int64).contiguous()
+            keep += [data, off, valid, rid] + ([quoted] if quoted is not None else [])
+            d.kind, d.off, d.text, d.valid = W_TEXT, off.data_ptr(), data.data_ptr(), valid.data_ptr()
+            d.quoted = quoted.data_ptr() if quoted is not None else None
+            d.rowid = rid.data_ptr()
+    dbuf = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+    tm = {"columns": time.perf_counter() - t0}
+    lens = torch.empty((C, N), dtype=torch.int32, device=dev)
+    dig = torch.empty((C, N), dtype=torch.int64, device=dev)     # float digits, cached between the passes
+    dpk = torch.full((C, N), -2, dtype=torch.int32, device=dev)  # p | (k + 512) << 8; -1 = host text
+    _chk(lib.cobalt_csv_write_len(dbuf.data_ptr(), C, N, lens.data_ptr(), dig.data_ptr(), dpk.data_ptr(), stream),
+         "cobalt_csv_write_len")
+    host_fix = None
+    if N and bool((lens < 0).any()):  # host-formatted fields: their text lengths go into the layout
+        ci, ri = torch.nonzero(lens < 0, as_tuple=True)
+        ch, rh = ci.cpu().numpy(), ri.cpu().numpy()
+        texts = []
+        for cc in np.unique(ch):
+            sel = ch == cc
+            v = fdata[int(cc)][ri[torch.as_tensor(sel, device=dev)]].cpu().numpy()
+            if descs[int(cc)].kind == W_INT:
+                texts += [str(x) for x in v.astype(np.int64)]
+            else:
+                texts += ["" if np.isnan(x) else repr(float(x)) for x in v]
+        order = np.concatenate([np.nonzero(ch == cc)[0] for cc in np.unique(ch)])
+        tb = [t.encode("utf-8") for t in texts]
+        L = torch.tensor([len(t) for t in tb], dtype=torch.int32, device=dev)
+        ci_o, ri_o = ci[torch.as_tensor(order, device=dev)], ri[torch.as_tensor(order, device=dev)]
+        lens[ci_o, ri_o] = L
+        host_fix = (ci_o, ri_o, L, b"".join(tb))
+    torch.cuda.synchronize(dev)
+    tm["lengths"] = time.perf_counter() - t0
+    pos = torch.cumsum(lens + 1, dim=0, dtype=torch.int64)  # inclusive over columns (field + separator)
+    row_len = pos[-1].clone()
+    pos -= (lens + 1)
+    row_off = torch.cumsum(row_len, 0) - row_len + len(header)
+    pos += row_off
+    total = len(header) + int(row_len.sum())
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    out[: len(header)] = torch.frombuffer(bytearray(header), dtype=torch.uint8).to(dev)
+    _chk(lib.cobalt_csv_write_bytes(dbuf.data_ptr(), C, N, pos.data_ptr(), lens.data_ptr(), dig.data_ptr(),
+                                    dpk.data_ptr(), out.data_ptr(), stream), "cobalt_csv_write_bytes")
+    if host_fix is not None and host_fix[3]:
+        ci_o, ri_o, L, blob = host_fix
+        L64 = L.to(torch.int64)
+        start = pos[ci_o, ri_o]
+        excl = torch.cumsum(L64, 0) - L64
+        nb = len(blob)
+        idx = torch.repeat_interleave(start - excl, L64, output_size=nb) + torch.arange(nb, device=dev)
+        out[idx] = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    torch.cuda.synchronize(dev)
+    tm["format"] = time.perf_counter() - t0
+    data = memoryview(out.cpu().numpy())  # bytes-like, no further host copy
+    del keep
+    if timings is not None:
+        tm["to_host"] = time.perf_counter() - t0
+        timings.update({k + "_s": v for k, v in tm.items()})
+        timings["bytes"] = total
+    return data

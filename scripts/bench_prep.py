@@ -70,6 +70,23 @@ def main() -> None:
     t_bins = time.perf_counter() - tb
     dtimes = {k: round(v, 3) for k, v in res["timings"].items()}
     log(f"device path {t_dev:.2f} s {dtimes} + matrix/binning {t_bins:.2f} s; tree {res['tree'].shape}")
+    write = None
+    if dev.type == "cuda":  # the artifact CSVs of the prep stages (clean_data.py / feature_engineering.py saves)
+        from cobalt_smart_lender_ai_amd.prep.csv_gpu import frame_to_csv_bytes
+        write = {}
+        for key in ("clean", "tree", "nn"):
+            tw = time.perf_counter()
+            wt = {}
+            blob = frame_to_csv_bytes(res[key], timings=wt)
+            write[key + "_s"] = round(time.perf_counter() - tw, 3)
+            write[key + "_mb"] = round(len(blob) / 1e6, 1)
+            write[key + "_phases"] = {k: round(v, 3) for k, v in wt.items() if k.endswith("_s")}
+        sub = res["tree"].take(torch.arange(res["tree"].n, device=dev) < res["tree"].n // 10)
+        tw = time.perf_counter()
+        pd_blob = sub.to_pandas().to_csv(index=False).encode()
+        write["pandas_tree_10pct_s"] = round(time.perf_counter() - tw, 3)
+        write["pandas_tree_10pct_equal"] = pd_blob == bytes(frame_to_csv_bytes(sub))
+        log(f"GPU CSV write {write}")
     arrow_ingest = None
     if dev.type == "cuda":  # the host-parsed ingest it replaces (pyarrow C++ reader + uploads), for reference
         del res["clean"], res["stage2"]
@@ -84,7 +101,8 @@ def main() -> None:
            "raw_rows": shape[0], "raw_cols": shape[1], "csv_gb": round(size_gb, 3),
            "tree_shape": list(res["tree"].shape), "nn_shape": list(res["nn"].shape),
            "device_s": round(t_dev, 3), "device_stages_s": dtimes, "device_matrix_and_bins_s": round(t_bins, 3),
-           "gbdt_features": len(names), "device": str(dev), "arrow_engine_ingest_s": arrow_ingest}
+           "gbdt_features": len(names), "device": str(dev), "arrow_engine_ingest_s": arrow_ingest,
+           "artifact_csv_write": write}
     if not a.skip_pandas:
         t0 = time.perf_counter()
         df = pd.read_csv(a.csv, low_memory=False, float_precision="round_trip")

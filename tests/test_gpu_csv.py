@@ -106,3 +106,69 @@ def test_synthetic_raw_lendingclub_matches_pyarrow(tmp_path):
     a = DeviceFrame.read_csv(str(path), "cuda", engine="arrow")
     assert t["cols"] == 143
     assert_frames_identical(g, a)
+
+
+# ------------------------------------------------------------------------------------------ writer
+def _pandas_bytes(frame) -> bytes:
+    return frame.to_pandas().to_csv(index=False).encode("utf-8")
+
+
+def test_writer_floats_all_magnitudes_match_pandas():
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import frame_to_csv_bytes
+    from cobalt_smart_lender_ai_amd.prep.device_frame import DCol
+
+    rng = np.random.default_rng(11)
+    n = 200_000
+    mags = rng.normal(size=n) * 10.0 ** rng.uniform(-30, 30, n)
+    sc = 10.0 ** rng.integers(0, 6, n)
+    short = np.round(rng.normal(size=n) * 1000 * sc) / sc  # "nice" decimals
+    ints = rng.integers(-10**15, 10**15, n).astype(np.float64)
+    special = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e16, 1e15, 0.0001, 1e-05, 9999999999999998.0,
+                        1.7976931348623157e308, 2.2250738585072014e-288, 0.1, 1 / 3, 123456789.123, 5e-5] * (n // 16))
+    mk = lambda a, dt="float64": DCol("f", torch.as_tensor(a, device="cuda"), dt)  # noqa: E731
+    fr = DeviceFrame({"mags": mk(mags), "short": mk(short), "ints": mk(ints, "int64"), "special": mk(special),
+                      "intnan": mk(np.where(rng.random(n) < 0.1, np.nan, ints), "int64")}, n, "cuda")
+    t = {}
+    got = frame_to_csv_bytes(fr, timings=t)
+    assert got is not None
+    got = bytes(got)
+    want = _pandas_bytes(fr)
+    if got != want:  # locate the first differing line for the failure message
+        g, w = got.split(b"\n"), want.split(b"\n")
+        i = next(i for i in range(min(len(g), len(w))) if g[i] != w[i])
+        raise AssertionError(f"line {i}: gpu {g[i]!r} pandas {w[i]!r}")
+
+
+def test_writer_strings_codes_flags_and_row_filter_match_pandas():
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import frame_to_csv_bytes
+
+    data = _tricky_csv(4001, 9, crlf=True)
+    fr = DeviceFrame.read_csv(data, "cuda", engine="gpu")
+    assert bytes(frame_to_csv_bytes(fr)) == _pandas_bytes(fr)
+    keep = torch.as_tensor(np.random.default_rng(2).random(fr.n) < 0.6, device="cuda")
+    sub = fr.take(keep)
+    assert bytes(frame_to_csv_bytes(sub)) == _pandas_bytes(sub)
+    arrow_fr = DeviceFrame.read_csv(data, "cuda", engine="arrow")  # text kept as Arrow columns
+    assert bytes(frame_to_csv_bytes(arrow_fr.take(keep))) == _pandas_bytes(arrow_fr.take(keep))
+
+
+def test_writer_prep_outputs_match_pandas(tmp_path):
+    from cobalt_smart_lender_ai_amd.dataio.synth_raw import make_raw_lendingclub
+    from cobalt_smart_lender_ai_amd.prep import device_prep as dp
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import frame_to_csv_bytes
+
+    path = tmp_path / "raw.csv"
+    make_raw_lendingclub(60_000, seed=3, n_cols=143).to_csv(path, index=False)
+    res = dp.run_device_prep(str(path), device="cuda", reference_date="2025-07-04")
+    for key in ("clean", "tree", "nn"):
+        assert bytes(frame_to_csv_bytes(res[key])) == _pandas_bytes(res[key]), key
+
+
+def test_writer_splices_host_formatted_values():
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import frame_to_csv_bytes
+    from cobalt_smart_lender_ai_amd.prep.device_frame import DCol
+
+    x = [1.0, 5e-324, -2.5e-310, 1.7976931348623157e308, -1e300, 0.1, float("nan"), 4.9e-321]
+    fr = DeviceFrame({"x": DCol("f", torch.tensor(x, dtype=torch.float64, device="cuda"), "float64"),
+                      "y": DCol("f", torch.arange(8, dtype=torch.float64, device="cuda"), "int64")}, 8, "cuda")
+    assert bytes(frame_to_csv_bytes(fr)) == _pandas_bytes(fr)
