@@ -70,7 +70,9 @@ def cmd_train(args) -> int:
     nw = resolve_workers(cfg.fits_in_parallel)
     pool = GpuTaskPool(nw) if nw > 1 else None
     try:
-        df = st.read_csv(cfg.input_key)
+        from .pipeline.prep_flow import read_table
+
+        df = read_table(st, cfg.input_key, args.device)
         m = run_training(df, cfg, store=st, local_dir=args.local_dir, device=args.device, pool=pool)
     finally:
         if pool is not None:
@@ -86,7 +88,10 @@ def cmd_train_nn(args) -> int:
 
     st = _store(args)
     cfg = NNTrainConfig(reproduce_reference=not args.use_smote, mlp=MLPConfig(epochs=args.epochs))
-    m = run_nn_training(st.read_csv(CLEAN_DATA_KEY_NN), cfg, store=st, local_dir=args.local_dir, device=args.device)
+    from .pipeline.prep_flow import read_table
+
+    m = run_nn_training(read_table(st, CLEAN_DATA_KEY_NN, args.device), cfg, store=st, local_dir=args.local_dir,
+                        device=args.device)
     print(json.dumps({k: m[k] for k in ("auc", "auc_thresholded", "selected_features", "train_seconds")}, indent=2))
     return 0
 

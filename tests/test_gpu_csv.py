@@ -172,3 +172,26 @@ def test_writer_splices_host_formatted_values():
     fr = DeviceFrame({"x": DCol("f", torch.tensor(x, dtype=torch.float64, device="cuda"), "float64"),
                       "y": DCol("f", torch.arange(8, dtype=torch.float64, device="cuda"), "int64")}, 8, "cuda")
     assert bytes(frame_to_csv_bytes(fr)) == _pandas_bytes(fr)
+
+
+def test_read_table_equals_pandas_round_trip(tmp_path):
+    """The train / train-nn CLI input read on the GPU equals pandas' correctly rounded reader."""
+    import io
+
+    import pandas as pd
+
+    from cobalt_smart_lender_ai_amd.dataio.artifacts import LocalStore
+    from cobalt_smart_lender_ai_amd.dataio.synth_raw import make_raw_lendingclub
+    from cobalt_smart_lender_ai_amd.pipeline.prep_flow import read_table
+    from cobalt_smart_lender_ai_amd.prep import device_prep as dp
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import frame_to_csv_bytes
+
+    path = tmp_path / "raw.csv"
+    make_raw_lendingclub(30_000, seed=8, n_cols=143).to_csv(path, index=False)
+    res = dp.run_device_prep(str(path), device="cuda", reference_date="2025-07-04")
+    st = LocalStore(tmp_path / "lake")
+    for key in ("tree", "nn"):
+        st.put_bytes(f"{key}.csv", frame_to_csv_bytes(res[key]))
+        got = read_table(st, f"{key}.csv", "cuda")
+        want = pd.read_csv(io.BytesIO(st.get_bytes(f"{key}.csv")), low_memory=False, float_precision="round_trip")
+        pd.testing.assert_frame_equal(got, want, check_exact=True)
