@@ -33,11 +33,18 @@ def main() -> None:
     from cobalt_smart_lender_ai_amd.prep.clean import clean_data_flow
     from cobalt_smart_lender_ai_amd.prep.features import clean_lending_data, feature_engineer_lending_data
 
-    t0 = time.perf_counter()
     raw = make_raw_lendingclub(a.raw_rows, seed=0)
-    df = clean_data_flow(raw, device=a.device)
-    df = clean_lending_data(df, reference_date="2025-07-04", device=a.device)
-    tree, _ = feature_engineer_lending_data(df, device=a.device)
+    if a.device.startswith("cuda"):  # the CLI's default: raw CSV -> GPU reader -> device-resident stages
+        from cobalt_smart_lender_ai_amd.prep.device_prep import run_device_prep
+
+        data = raw.to_csv(index=False).encode()
+        t0 = time.perf_counter()
+        tree = run_device_prep(data, device=a.device, reference_date="2025-07-04")["tree"].to_pandas()
+    else:
+        t0 = time.perf_counter()
+        df = clean_data_flow(raw, device=a.device)
+        df = clean_lending_data(df, reference_date="2025-07-04", device=a.device)
+        tree, _ = feature_engineer_lending_data(df, device=a.device)
     t_prep = time.perf_counter() - t0
     n_feat = len([c for c in tree.columns if c != "loan_default" and c not in LEAKAGE_COLUMNS])
     rng = np.random.default_rng(7)
