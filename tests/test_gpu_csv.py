@@ -195,3 +195,36 @@ def test_read_table_equals_pandas_round_trip(tmp_path):
         got = read_table(st, f"{key}.csv", "cuda")
         want = pd.read_csv(io.BytesIO(st.get_bytes(f"{key}.csv")), low_memory=False, float_precision="round_trip")
         pd.testing.assert_frame_equal(got, want, check_exact=True)
+
+
+def test_prep_flow_gpu_engine_writes_the_pandas_artifacts(tmp_path):
+    """Both CLI prep stages on the GPU (GPU CSV reader -> device stages -> GPU CSV writer) save the
+    same artifacts as the pandas engine (values equal up to pandas' own parser rounding)."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).parent))
+    from test_device_prep import REF_DATE, assert_frames_equal
+
+    from cobalt_smart_lender_ai_amd.config import CLEAN_DATA_KEY_FULL, CLEAN_DATA_KEY_NN, CLEAN_DATA_KEY_TREE, \
+        RAW_DATA_KEY_FULL
+    from cobalt_smart_lender_ai_amd.dataio.artifacts import LocalStore
+    from cobalt_smart_lender_ai_amd.dataio.synth_raw import make_raw_lendingclub
+    from cobalt_smart_lender_ai_amd.pipeline.prep_flow import run_clean, run_features
+
+    raw = make_raw_lendingclub(20_000, seed=21, n_cols=143)
+    outs = {}
+    for tag, engine, dev in (("pandas", "pandas", "cpu"), ("device_cpu", "device", "cpu"), ("gpu", "device", "cuda")):
+        st = LocalStore(tmp_path / tag)
+        st.write_csv(raw, RAW_DATA_KEY_FULL)
+        run_clean(st, use_sample=False, device=dev, engine=engine)
+        run_features(st, device=dev, reference_date=REF_DATE, engine=engine)
+        outs[tag] = [st.read_csv(k, float_precision="round_trip")
+                     for k in (CLEAN_DATA_KEY_FULL, CLEAN_DATA_KEY_TREE, CLEAN_DATA_KEY_NN)]
+    # the GPU engine (GPU reader + kernels + GPU writer) vs the same stages on CPU tensors (pyarrow
+    # reader, pandas writer): equal up to the last ulp of device vs host log1p
+    for a, b in zip(outs["gpu"], outs["device_cpu"]):
+        assert_frames_equal(a, b, rtol=1e-15)
+    # vs the pandas engine: pandas' default float parser reads some raw values a few dozen ulp off
+    for a, b in zip(outs["gpu"], outs["pandas"]):
+        assert_frames_equal(a, b, rtol=1e-13)
