@@ -28,7 +28,8 @@ constexpr int kMaxBins = 256;          // row stride of the cut table (255 usabl
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ int wave_id() { return threadIdx.x / kWave; }
 
-// Inclusive prefix sum over the 64 lanes of a wavefront.
+// Inclusive prefix sum over the 64 lanes of a wavefront (generic shuffle form; int / int64 use the
+// DPP overloads below).
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
   const int lane = lane_id();
@@ -37,6 +38,54 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
     T t = __shfl_up(v, o, kWave);
     if (lane >= o) v += t;
   }
+  return v;
+}
+
+// ---- DPP cross-lane moves (GFX9 / CDNA data-parallel primitives: row_shr within 16-lane rows,
+// row_bcast across rows). A lane without a source (shifted in, or in a disabled row / bank) gets
+// `old`. They run at VALU latency; __shfl lowers to ds_bpermute, an LDS round trip per step.
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+
+template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
+__device__ __forceinline__ int dpp32(int v, int old) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWM, BANKM, false);
+}
+
+template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
+__device__ __forceinline__ int64_t dpp64(int64_t v, int64_t old) {
+  const int lo = dpp32<CTRL, ROWM, BANKM>((int)(uint32_t)(uint64_t)v, (int)(uint32_t)(uint64_t)old);
+  const int hi = dpp32<CTRL, ROWM, BANKM>((int)((uint64_t)v >> 32), (int)((uint64_t)old >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ int readlane32(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, lane);
+  const int hi = __builtin_amdgcn_readlane((int)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Wave64 inclusive prefix sums on DPP (Hillis-Steele within rows, then the row totals via
+// row_bcast:15 into rows 1 / 3 and row_bcast:31 into rows 2 / 3). Every lane must be active.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += dpp32<kDppRowShr1>(v, 0);
+  v += dpp32<kDppRowShr2>(v, 0);
+  v += dpp32<kDppRowShr4>(v, 0);
+  v += dpp32<kDppRowShr8>(v, 0);
+  v += dpp32<kDppRowBcast15, 0xa>(v, 0);
+  v += dpp32<kDppRowBcast31, 0xc>(v, 0);
+  return v;
+}
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v) {
+  v += dpp64<kDppRowShr1>(v, 0);
+  v += dpp64<kDppRowShr2>(v, 0);
+  v += dpp64<kDppRowShr4>(v, 0);
+  v += dpp64<kDppRowShr8>(v, 0);
+  v += dpp64<kDppRowBcast15, 0xa>(v, 0);
+  v += dpp64<kDppRowBcast31, 0xc>(v, 0);
   return v;
 }
 

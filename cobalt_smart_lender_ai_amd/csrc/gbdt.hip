@@ -69,6 +69,37 @@ __device__ __forceinline__ bool cand_better(const Cand& a, const Cand& b) {
   return a.gain > b.gain || (a.gain == b.gain && a.key < b.key);
 }
 
+template <int CTRL, int ROWM>
+__device__ __forceinline__ void best_step(double& g, int& k) {
+  const double og = __longlong_as_double(dpp64<CTRL, ROWM>(__double_as_longlong(g), __double_as_longlong(-INFINITY)));
+  const int ok = dpp32<CTRL, ROWM>(k, 0x7fffffff);
+  if (og > g || (og == g && ok < k)) { g = og; k = ok; }
+}
+
+// The wave's best candidate (max under cand_better), returned in every lane: a DPP max-scan of
+// (gain, key) leaves the winner in lane 63, a ballot finds the lane it came from (keys are unique
+// per lane), and that lane's gl / hl / cut are read back -- the same result as a shuffle butterfly
+// over the whole Cand, at VALU instead of LDS latency per step.
+__device__ __forceinline__ void wave_best(Cand& best, float& cut) {
+  double g = best.gain;
+  int k = best.key;
+  best_step<kDppRowShr1, 0xf>(g, k);
+  best_step<kDppRowShr2, 0xf>(g, k);
+  best_step<kDppRowShr4, 0xf>(g, k);
+  best_step<kDppRowShr8, 0xf>(g, k);
+  best_step<kDppRowBcast15, 0xa>(g, k);
+  best_step<kDppRowBcast31, 0xc>(g, k);
+  const double wg = __longlong_as_double(readlane64(__double_as_longlong(g), kWave - 1));
+  const int wk = readlane32(k, kWave - 1);
+  const uint64_t m = __ballot(best.key == wk && best.gain == wg);
+  const int src = m ? __ffsll((unsigned long long)m) - 1 : 0;
+  best.gain = wg;
+  best.key = wk;
+  best.gl = readlane64(best.gl, src);
+  best.hl = readlane64(best.hl, src);
+  cut = __int_as_float(readlane32(__float_as_int(cut), src));
+}
+
 __device__ __forceinline__ Cand cand_shfl_xor(const Cand& c, int o) {
   Cand r;
   r.gain = __shfl_xor(c.gain, o, kWave);
@@ -576,7 +607,7 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
         s_out[2] = b;
         s_out[3] = min(en.start + en.count, b + chunk);
       }
-      carry = __shfl(incl, kWave - 1, kWave);
+      carry = readlane32(incl, kWave - 1);
     }
     if (lane == 0) s_out[4] = carry;
   }
@@ -1307,7 +1338,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     for (int k = 1; k < 4; ++k) { cg[k] = cg[k - 1] + e.g[k]; ch[k] = ch[k - 1] + e.h[k]; }
     const int64_t ig = wave_incl_scan(cg[3]), ih = wave_incl_scan(ch[3]);
     const int64_t eg = ig - cg[3], eh = ih - ch[3];
-    const int64_t sg = __shfl(ig, kWave - 1, kWave), sh = __shfl(ih, kWave - 1, kWave);
+    const int64_t sg = readlane64(ig, kWave - 1), sh = readlane64(ih, kWave - 1);
     const int64_t mg = G - sg, mh = H - sh;  // missing-value statistics
     const bool has_missing = (mg != 0) || (mh != 0);
 #pragma unroll
@@ -1346,12 +1377,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   }
   }
   stamp_.probe(2);
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    Cand other = cand_shfl_xor(best, o);
-    const float ocut = __shfl_xor(best_cut, o, kWave);
-    if (cand_better(other, best)) { best = other; best_cut = ocut; }
-  }
+  wave_best(best, best_cut);
   if (lane == 0) { s_best[wave_id()] = best; s_cut[wave_id()] = best_cut; }
   __syncthreads();
   stamp_.probe(3);
@@ -1398,12 +1424,7 @@ __global__ __launch_bounds__(64) void k_eval_finish(GbdtDev d, int level, int pa
     best.hl = c.hl;
     best_cut = c.cut;
   }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    Cand other = cand_shfl_xor(best, o);
-    const float ocut = __shfl_xor(best_cut, o, kWave);
-    if (cand_better(other, best)) { best = other; best_cut = ocut; }
-  }
+  wave_best(best, best_cut);
   if (lane == 0) eval_finalize(d, level, n, G, H, best, best_cut);
 }
 
@@ -1583,12 +1604,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
       }
     }
   }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    Cand other = cand_shfl_xor(best, o);
-    const float ocut = __shfl_xor(best_cut, o, kWave);
-    if (cand_better(other, best)) { best = other; best_cut = ocut; }
-  }
+  wave_best(best, best_cut);
   if (lane == 0) { s_best[wv] = best; s_cut[wv] = best_cut; }
   __syncthreads();
   stamp_.probe(3);
@@ -2310,4 +2326,33 @@ COBALT_API int cobalt_bin_matrix(const float* X, int64_t n, int F, int64_t ldx, 
                                  const int32_t* nbins, uint8_t* bins, int stride, uint8_t* binsT,
                                  hipStream_t stream) {
   return cobalt_bin_matrix_ld(X, n, F, ldx, cuts, nbins, bins, stride, binsT, n, stream);
+}
+
+// Self-test of the DPP wave primitives (tests/test_gpu_gbdt.py): one wave, inclusive scans of the
+// int64 inputs (and of their low 32 bits), and the wave_best arg-max of (gain = in, key = lane).
+namespace {
+__global__ __launch_bounds__(64) void k_dpp_selftest(const int64_t* __restrict__ in, int64_t* __restrict__ o64,
+                                                     int* __restrict__ o32, int64_t* __restrict__ obest) {
+  const int lane = threadIdx.x;
+  const int64_t v = in[lane];
+  o64[lane] = wave_incl_scan(v);
+  o32[lane] = wave_incl_scan((int)v);
+  Cand c;
+  c.gain = (double)(v % 1000);
+  c.key = lane;
+  c.gl = v;
+  c.hl = -v;
+  float cut = (float)lane;
+  wave_best(c, cut);
+  obest[4 * lane + 0] = c.key;
+  obest[4 * lane + 1] = c.gl;
+  obest[4 * lane + 2] = c.hl;
+  obest[4 * lane + 3] = (int64_t)cut;
+}
+}  // namespace
+
+COBALT_API int cobalt_dpp_selftest(const int64_t* in, int64_t* o64, int* o32, int64_t* obest, hipStream_t s) {
+  hipLaunchKernelGGL(k_dpp_selftest, dim3(1), dim3(64), 0, s, in, o64, o32, obest);
+  CK_LAUNCH();
+  return 0;
 }

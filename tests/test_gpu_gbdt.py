@@ -331,3 +331,29 @@ def test_gpu_quantised_1000_trees_match_fp64_reference():
     af = roc_auc(yte, bf.predict_proba(Xte.numpy(), device="cpu"))
     print(f"[quant-1000] gpu auc {ag:.5f} fp64 auc {af:.5f}")
     assert abs(ag - af) <= 0.002
+
+
+def test_dpp_wave_primitives():
+    """DPP scans (int64 / int32) and the DPP arg-max used by split evaluation, vs NumPy."""
+    import ctypes
+
+    from cobalt_smart_lender_ai_amd import _native
+
+    _native.register("cobalt_dpp_selftest", ctypes.c_int, [ctypes.c_void_p] * 5)
+    rng = np.random.default_rng(0)
+    for trial in range(5):
+        v = rng.integers(-(1 << 40), 1 << 40, 64, dtype=np.int64) if trial else np.arange(64, dtype=np.int64)
+        vi = torch.as_tensor(v, device="cuda")
+        o64 = torch.empty(64, dtype=torch.int64, device="cuda")
+        o32 = torch.empty(64, dtype=torch.int32, device="cuda")
+        ob = torch.empty(256, dtype=torch.int64, device="cuda")
+        assert _native.lib().cobalt_dpp_selftest(vi.data_ptr(), o64.data_ptr(), o32.data_ptr(), ob.data_ptr(),
+                                                 _native.stream_handle()) == 0
+        assert np.array_equal(o64.cpu().numpy(), np.cumsum(v))
+        lo = v.astype(np.int64).astype(np.uint32).view(np.int32)
+        assert np.array_equal(o32.cpu().numpy(), np.cumsum(lo.astype(np.int64)).astype(np.uint32).view(np.int32))
+        gains = np.fmod(v, 1000).astype(np.float64)
+        win = max(range(64), key=lambda i: (gains[i], -i))
+        best = ob.cpu().numpy().reshape(64, 4)
+        assert (best[:, 0] == win).all() and (best[:, 1] == v[win]).all() and (best[:, 2] == -v[win]).all()
+        assert (best[:, 3] == win).all()
