@@ -96,6 +96,10 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// int / int64 totals in every lane: the DPP scan's last lane, read back as a scalar (all lanes active).
+__device__ __forceinline__ int wave_sum(int v) { return readlane32(wave_incl_scan(v), kWave - 1); }
+__device__ __forceinline__ int64_t wave_sum(int64_t v) { return readlane64(wave_incl_scan(v), kWave - 1); }
+
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
 #pragma unroll

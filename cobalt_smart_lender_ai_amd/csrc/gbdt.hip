@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ pa
       const int leader = __ffsll((unsigned long long)km) - 1;
       unsigned long long b0 = 0;
       if (lane == leader) b0 = atomicAdd(counter, (unsigned long long)__popcll(km));
-      b0 = __shfl(b0, leader, kWave);
+      b0 = (unsigned long long)readlane64((int64_t)b0, leader);
       if (keep) {
         const int64_t slot = (int64_t)b0 + mask_rank(km);
         if (slot < cap) {
@@ -1381,9 +1381,12 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   if (lane == 0) { s_best[wave_id()] = best; s_cut[wave_id()] = best_cut; }
   __syncthreads();
   stamp_.probe(3);
-  if (threadIdx.x != 0) return;
-  for (int k = 1; k < nw; ++k)
-    if (cand_better(s_best[k], best)) { best = s_best[k]; best_cut = s_cut[k]; }
+  if (wave_id() != 0) return;
+  // the waves' winners, one per lane of wave 0, reduced by the same DPP arg-max
+  if (lane < nw) { best = s_best[lane]; best_cut = s_cut[lane]; }
+  else { best.gain = -INFINITY; best.key = 0x7fffffff; best.gl = 0; best.hl = 0; best_cut = -FLT_MAX; }
+  wave_best(best, best_cut);
+  if (lane != 0) return;
   if (kGroups) {
     CandRec& o = d.cand[(int64_t)pos * gridDim.y + blockIdx.y];
     o.gain = best.gain;
@@ -1608,9 +1611,11 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
   if (lane == 0) { s_best[wv] = best; s_cut[wv] = best_cut; }
   __syncthreads();
   stamp_.probe(3);
+  if (wv != 0) return;
+  if (lane < kEvalThreads / kWave) { best = s_best[lane]; best_cut = s_cut[lane]; }
+  else { best.gain = -INFINITY; best.key = 0x7fffffff; best.gl = 0; best.hl = 0; best_cut = -FLT_MAX; }
+  wave_best(best, best_cut);
   if (t != 0) return;
-  for (int k = 1; k < kEvalThreads / kWave; ++k)
-    if (cand_better(s_best[k], best)) { best = s_best[k]; best_cut = s_cut[k]; }
   const int wf = best.key != 0x7fffffff ? (best.key >> 10) : 0;
   eval_finalize(d, level, n, G, H, best, best_cut, s_nb[wf]);
   stamp_.probe(4);
