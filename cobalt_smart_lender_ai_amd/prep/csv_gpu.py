@@ -32,7 +32,7 @@ from .. import _native
 
 ST_INT, ST_NULL, ST_TRUE, ST_FALSE, ST_STR, ST_HOST, ST_FRAC = range(7)
 
-_P, _I64, _I32, _U64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
+_P, _I64, _I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
 _native.register("cobalt_csv_chunk", ctypes.c_int, [])
 _native.register("cobalt_csv_quotes", ctypes.c_int, [_P, _I64, _P, _P])
 _native.register("cobalt_csv_delims", ctypes.c_int, [_P, _I64, _P, _P, _P])
@@ -452,7 +452,7 @@ def frame_to_csv_bytes(frame, timings: dict | None = None) -> memoryview | bytes
     host_fix = None
     if N and bool((lens < 0).any()):  # host-formatted fields: their text lengths go into the layout
         ci, ri = torch.nonzero(lens < 0, as_tuple=True)
-        ch, rh = ci.cpu().numpy(), ri.cpu().numpy()
+        ch = ci.cpu().numpy()
         texts = []
         for cc in np.unique(ch):
             sel = ch == cc
