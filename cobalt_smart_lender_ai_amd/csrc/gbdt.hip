@@ -158,6 +158,7 @@ struct GbdtDev {
   int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
+  int32_t* pair_first;    // [pairs_max + 1] first work item of each pair of the level (k_hist item 0)
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
                           // 4 plan only (k_hist); 11-13 partition (see k_partition)
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
@@ -587,8 +588,10 @@ struct PlanOut {
   int node, slot, begin, end, total;
 };
 
+// `first_out` (one block of the pass, or nullptr): entry e's first work item, [n_ent] = the total --
+// the fused-reduce evaluation reads its pair's item range from it.
 template <class EntryFn>
-__device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int* s_out) {
+__device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int* s_out, int* first_out = nullptr) {
   if (wave_id() == 0) {
     const int lane = lane_id();
     if (lane == 0) s_out[0] = -1;
@@ -600,6 +603,7 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
       const int nch = (en.node >= 0 && en.count > 0) ? (en.count + chunk - 1) / chunk : 0;
       const int incl = wave_incl_scan(nch) + carry;
       const int excl = incl - nch;
+      if (first_out && e < n_ent) first_out[e] = excl;
       if (nch > 0 && item >= excl && item < incl) {
         const int b = en.start + (item - excl) * chunk;
         s_out[0] = en.node;
@@ -610,6 +614,7 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
       carry = readlane32(incl, kWave - 1);
     }
     if (lane == 0) s_out[4] = carry;
+    if (first_out && lane == 0) first_out[n_ent] = carry;
   }
   __syncthreads();
   return PlanOut{s_out[0], s_out[1], s_out[2], s_out[3], s_out[4]};
@@ -932,7 +937,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   flush_meta_store(fmeta, ft, s_fo, s_fs);
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
-                                s_plan);
+                                s_plan, (item == 0 && blockIdx.y == 0) ? d.pair_first : nullptr);
   stamp_.probe(1);
   if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total, d.by_hess != 0);
   if (pl.node < 0) return;
@@ -1050,40 +1055,52 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
 // global atomic per non-zero cell per (run, slot) -- coalesced, 30-100x fewer than per-block flushes.
 constexpr int kRedItems = 16;
 
-__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int publish) {
+__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int publish, int n_grid) {
   BlockStamp stamp_(d);
   // fused partition path: block (0, 0) publishes the level's node ranges from the finished claims
   if (publish > 0 && blockIdx.x == 0 && blockIdx.y == 0) publish_level(d, publish, -1, true);
-  const int n_items = d.counters[0];
-  stamp_.probe(1);
   const int i0 = blockIdx.x * kRedItems;
-  if (i0 >= n_items) return;
-  const int cnt = min(n_items - i0, kRedItems);
   const int ncell = d.ncells;
   const int cell = blockIdx.y * blockDim.x + threadIdx.x;
   if (cell > ncell) return;
   const bool tot = cell == ncell;
-  // Issue every load of the run before the first add: the item slots (uniform, scalar loads) and
-  // the kRedItems slab cells are independent, so the run costs one memory round trip instead of
-  // one per item (the sequential loop measured ~13 us per level at 10M rows).
+  // Issue every load of the run before the first add, in ONE round trip together with the item
+  // count: the item indices are clamped to the launched work-item range (n_grid <= items_cap), not
+  // to the count, so no load waits on it (items past the count are stale and masked below), and the
+  // node-total cell's branch sits outside the unrolled loads (a per-element branch made hipcc wait
+  // for every load in turn: 16 x 3 dependent round trips, ~7 us of the kernel's ~12). The count is
+  // loaded after them in program order: its uniform use (readfirstlane + wait) must not come first.
   int slot[kRedItems];
   int64_t g[kRedItems], h[kRedItems];
+  if (tot) {
 #pragma unroll
-  for (int k = 0; k < kRedItems; ++k) {  // clamped, branch-free loads; the tail is masked below
-    const int it = i0 + min(k, cnt - 1);
-    slot[k] = d.items_h[it].slot;
-    if (tot) {
+    for (int k = 0; k < kRedItems; ++k) {
+      const int it = min(i0 + k, n_grid - 1);
+      slot[k] = d.items_h[it].slot;
       g[k] = d.slab_tot[2 * it];
       h[k] = d.slab_tot[2 * it + 1];
-    } else {
-      const uint64_t v = d.slab[(int64_t)it * ncell + cell];
-      g[k] = (int64_t)(int32_t)(uint32_t)(v >> 32);
-      h[k] = (int64_t)(uint32_t)v;
+    }
+  } else {
+    uint64_t v[kRedItems];
+#pragma unroll
+    for (int k = 0; k < kRedItems; ++k) {
+      const int it = min(i0 + k, n_grid - 1);
+      slot[k] = d.items_h[it].slot;
+      v[k] = d.slab[(int64_t)it * ncell + cell];
+    }
+#pragma unroll
+    for (int k = 0; k < kRedItems; ++k) {
+      g[k] = (int64_t)(int32_t)(uint32_t)(v[k] >> 32);
+      h[k] = (int64_t)(uint32_t)v[k];
     }
   }
+  const int n_items = d.counters[0];
+  stamp_.probe(1);
+  if (i0 >= n_items) return;
+  const int cnt = min(n_items - i0, kRedItems);
 #pragma unroll
-  for (int k = 0; k < kRedItems; ++k)
-    if (k >= cnt) { g[k] = 0; h[k] = 0; slot[k] = slot[cnt - 1]; }
+  for (int k = 0; k < kRedItems; ++k)  // stale tail items: no slot (flushes nothing)
+    if (k >= cnt) { g[k] = 0; h[k] = 0; slot[k] = -2; }
   // items of one slot are consecutive: flush one atomic pair per (run, slot)
   stamp_.probe(2);
   int cur = slot[0];
@@ -1237,8 +1254,14 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
 // kGroups: the node's features are split over gridDim.y blocks of `fg` features each (one CU per
 // group instead of one per node: the fp64 gain scan of a wide node -- 106 features in the RFE stage --
 // is issue-bound on a single CU); each group writes its best candidate and k_eval_finish reduces them.
-template <bool kGroups>
+//
+// `fused` (one GPU, deep levels with few work items per pair): k_hist_reduce was not launched; the
+// block sums its pair's per-item slabs itself (items [pair_first[pair], pair_first[pair + 1]), the
+// same exact int64 sums in another order) and the built child's block stores the result in hist_b,
+// where the next level reads it as the parent histogram. Saves the reduce launch (~13 us per level).
+template <bool kGroups, bool kFused>
 __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg) {
+  constexpr bool fused = kFused;
   BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   const int fbeg = kGroups ? blockIdx.y * fg : 0;
@@ -1247,7 +1270,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   Node* nodes = d.nodes;
   const int pair = level == 0 ? 0 : (pos >> 1);
   const int64_t SE = d.slot_elems;
-  const int64_t* hb = d.hist_b[parity] + pair * SE;
+  int64_t* hb = d.hist_b[parity] + pair * SE;
   int64_t* hs = d.hist_s[parity] + pair * SE;
   const int lane = lane_id();
   const int nw = (int)(blockDim.x / kWave);
@@ -1282,6 +1305,11 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     G = hb[(int64_t)d.ncells * 2];
     H = hb[(int64_t)d.ncells * 2 + 1];
   }
+  int it0 = 0, it1 = 0;
+  if constexpr (fused) {
+    it0 = d.pair_first[pair];
+    it1 = d.pair_first[pair + 1];
+  }
   if (status != kActive) return;
   stamp_.probe(1);
   __shared__ Cand s_best[16];
@@ -1303,6 +1331,59 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   for (int fbase = fbeg + wave_id(); fbase < fend; fbase += 2 * nw) {  // one pass for F <= 32
   if (fbase != fbeg + wave_id()) load_meta(fbase);
   // round trip 2: the histogram bins (and the parent's, for the subtraction)
+  if constexpr (fused) {
+    // the pair's per-item slabs, summed here (the parent's bins go out first, they are independent)
+    int64_t ag[2][4], ah[2][4], pg[2][4], ph[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool in = ef[s].on && lane * 4 + k < ef[s].nb;
+        pg[s][k] = (in && !built) ? parent[fbase_off[s] + 2 * k] : 0;
+        ph[s][k] = (in && !built) ? parent[fbase_off[s] + 2 * k + 1] : 0;
+        ag[s][k] = 0;
+        ah[s][k] = 0;
+      }
+    // unconditional loads (cells clamped into the slab row), masked adds: a guarded load per cell
+    // would make hipcc wait for each one in turn
+    const int ncell = d.ncells;
+    int cidx[2][4];
+    bool cin[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        cidx[s][k] = min((int)(fbase_off[s] / 2) + k, ncell - 1);
+        cin[s][k] = ef[s].on && lane * 4 + k < ef[s].nb;
+      }
+#pragma unroll 2
+    for (int it = it0; it < it1; ++it) {
+      const uint64_t* row = d.slab + (int64_t)it * ncell;
+      uint64_t v[2][4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[s][k] = row[cidx[s][k]];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint64_t w = cin[s][k] ? v[s][k] : 0ull;
+          ag[s][k] += (int64_t)(int32_t)(uint32_t)(w >> 32);
+          ah[s][k] += (int64_t)(uint32_t)w;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      EvalFeat& e = ef[s];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        e.g[k] = built ? ag[s][k] : pg[s][k] - ag[s][k];
+        e.h[k] = built ? ah[s][k] : ph[s][k] - ah[s][k];
+      }
+      if (lane == 0) e.cutm1 = -FLT_MAX;
+    }
+  } else {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     EvalFeat& e = ef[s];
@@ -1318,18 +1399,20 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     }
     if (lane == 0) e.cutm1 = -FLT_MAX;
   }
+  }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const EvalFeat& e = ef[s];
     if (!e.on) continue;
     const int f = e.f, nb = e.nb;
-    if (!built) {  // materialise the sibling histogram for the next level
+    if (!built || fused) {  // materialise the sibling (or, fused, the built child's) histogram for the next level
+      int64_t* dst = built ? hb : hs;
       const int64_t base = ((int64_t)d.hoff[f] + lane * 4) * 2;
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (lane * 4 + k < nb) {
-          hs[base + 2 * k] = e.g[k];
-          hs[base + 2 * k + 1] = e.h[k];
+          dst[base + 2 * k] = e.g[k];
+          dst[base + 2 * k + 1] = e.h[k];
         }
     }
     int64_t cg[4], ch[4];
@@ -2051,6 +2134,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   }
   if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.pair_first, ((size_t)c->pairs_max + 1) * sizeof(int32_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.hoff, (F + 1) * sizeof(int32_t)))) return rc;
@@ -2155,6 +2239,15 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // measures slower than the separate passes (COBALT_FUSED_PART=1)
   const bool env_fuse_part = getenv("COBALT_FUSED_PART") != nullptr && atoi(getenv("COBALT_FUSED_PART")) != 0;
   const bool fuse_part = fuse_root && env_fuse_part;
+  // reduce fused into k_eval<false> (one GPU) at levels with at most `fused_max` work items per pair
+  // (upper bound: ub / pairs); COBALT_FUSED_REDUCE overrides (0 = off)
+  static const int env_fused = getenv("COBALT_FUSED_REDUCE") ? atoi(getenv("COBALT_FUSED_REDUCE")) : -1;
+  const int fused_max = env_fused >= 0 ? env_fused : 0;
+  auto fused_level = [&](int lv) {
+    if (dp || fuse_part || eval_fg > 0 || eval_compact || lv < 1 || lv >= D || fused_max <= 0) return false;
+    const int ub_lv = ceil_div(d.n, chunk_hist(d, lv)) + (1 << lv);
+    return ceil_div(ub_lv, 1 << (lv - 1)) <= fused_max;
+  };
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
   static const int env_root = getenv("COBALT_ROOT_CHUNK") ? atoi(getenv("COBALT_ROOT_CHUNK")) : 0;
@@ -2199,8 +2292,10 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           GLAUNCH("k_hist", k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level,
                   chh);
       }
-      GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
-              dim3(256), 0, stream, d, parity, fuse_part ? level : 0);
+      const bool fused = fused_level(level);
+      if (!fused)
+        GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
+                dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap));
       CK_LAUNCH();
       if (dp) {
         // row-count choice: ranks built their locally smaller child -> turn it into the local LEFT
@@ -2216,18 +2311,22 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       }
       if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
         const int ng = ceil_div(d.F, eval_fg);
-        GLAUNCH("k_eval", k_eval<true>, dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d, level,
-                parity, t, eval_fg);
+        GLAUNCH("k_eval", (k_eval<true, false>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d,
+                level, parity, t, eval_fg);
         GLAUNCH("k_eval_finish", k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
       } else if (eval_compact) {
         GLAUNCH("k_eval", k_eval_compact, dim3(1 << level), dim3(kEvalThreads), 0, stream, d, level, parity, t);
       } else {
-        GLAUNCH("k_eval", k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
+        if (fused)
+          GLAUNCH("k_eval", (k_eval<false, true>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
+        else
+          GLAUNCH("k_eval", (k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
       }
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
-        const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;
+        // a fused next level stores its histograms instead of accumulating them: nothing to zero
+        const int64_t zero_next = fused_level(level + 1) ? 0 : (int64_t)(1 << level) * d.slot_elems;
         if (part_wide(d))
           GLAUNCH("k_partition", k_partition<16>, dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next, level, chp);
         else
