@@ -628,10 +628,20 @@ __device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, int
   if (level == 0) return PlanEntry{0, 0, 0, (int)d.n};
   const int q = (1 << (level - 1)) - 1 + p;
   const Node& par = d.nodes[q];
-  if (par.status != kSplit) return PlanEntry{-1, p, 0, 0};
-  const int lc = d.cursors[2 * q];
-  const bool left_small = d.by_hess ? d.nodes[2 * q + 1].build != 0 : lc <= d.cursors[2 * q + 1];
-  return left_small ? PlanEntry{2 * q + 1, p, par.start, lc} : PlanEntry{2 * q + 2, p, par.start + lc, par.count - lc};
+  // every load first, selected after: one round trip (a load behind the status test would wait)
+  const int st = par.status, pstart = par.start, pcount = par.count;
+  const int2 cc = *reinterpret_cast<const int2*>(d.cursors + 2 * q);  // one 8-byte load: both counts
+  const int lc = cc.x, rc = cc.y;
+  const int lbuild = d.nodes[2 * q + 1].build;
+  // selects, not an early return: hipcc sinks loads into the branch that uses them
+  const bool ok = st == kSplit;
+  const bool left_small = d.by_hess ? lbuild != 0 : lc <= rc;
+  PlanEntry en;
+  en.node = ok ? (left_small ? 2 * q + 1 : 2 * q + 2) : -1;
+  en.slot = p;
+  en.start = ok ? (left_small ? pstart : pstart + lc) : 0;
+  en.count = ok ? (left_small ? lc : pcount - lc) : 0;
+  return en;
 }
 
 // Block (0, 0) of the histogram pass publishes the level's node ranges / build flags for the
@@ -691,8 +701,11 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   const bool in = lane < ft;
   const int f = f0 + (in ? lane : 0);
   HistLaneRaw r;
-  r.on = in && d.fmask[(int64_t)tree * d.F + f] != 0;
-  const int ly = in ? d.layout[f].y : 0;
+  // unconditional loads (f is clamped), masked after: both in one round trip
+  const uint8_t fmv = d.fmask[(int64_t)tree * d.F + f];
+  const int ly0 = d.layout[f].y;
+  r.on = in && fmv != 0;
+  const int ly = in ? ly0 : 0;
   r.sh = ly & 7;
   r.full = (ly & 8) != 0;
   return r;
@@ -758,8 +771,13 @@ struct FlushMeta {
 __device__ __forceinline__ FlushMeta flush_meta_load(const GbdtDev& d, int tree, int f0, int ft) {
   FlushMeta m{0, -1};
   const int t = threadIdx.x;
-  if (t <= ft) m.fo = d.hoff[f0 + t];
-  if (t < ft) m.fs = d.fmask[(int64_t)tree * d.F + f0 + t] != 0 ? (d.layout[f0 + t].y & 7) : -1;
+  // unconditional loads at clamped indices, selected after (one round trip, no chained waits)
+  const int tc = min(t, ft), tf = min(t, ft - 1);
+  const int fo = d.hoff[f0 + tc];
+  const uint8_t fmv = d.fmask[(int64_t)tree * d.F + f0 + tf];
+  const int ly = d.layout[f0 + tf].y;
+  if (t <= ft) m.fo = fo;
+  if (t < ft) m.fs = fmv != 0 ? (ly & 7) : -1;
   return m;
 }
 
@@ -935,9 +953,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   const FlushMeta fmeta = flush_meta_load(d, tree, f0, ft);
   const int entries = ft * kMaxBins + kWave;  // tile_entries[y] == ft * 256, + per-lane trash cells
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
-  flush_meta_store(fmeta, ft, s_fo, s_fs);
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
                                 s_plan, (item == 0 && blockIdx.y == 0) ? d.pair_first : nullptr);
+  // after the plan (storing first would wait for the metadata before the plan's loads go out); the
+  // barrier after the row loop publishes it to the flush
+  flush_meta_store(fmeta, ft, s_fo, s_fs);
   stamp_.probe(1);
   if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total, d.by_hess != 0);
   if (pl.node < 0) return;
@@ -1286,8 +1306,10 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       e.f = fbase + s * nw;
       const int fc = min(e.f, d.F - 1);
       const bool valid = e.f < fend;
-      e.on = valid && fm[fc] != 0;
-      e.nb = valid ? d.nbins[fc] : 0;
+      const uint8_t fmv = fm[fc];  // unconditional loads, masked after (no per-load branch)
+      const int nbv = d.nbins[fc];
+      e.on = valid && fmv != 0;
+      e.nb = valid ? nbv : 0;
       fbase_off[s] = ((int64_t)d.hoff[fc] + lane * 4) * 2;
 #pragma unroll
       for (int k = 0; k < 4; ++k) e.cut[k] = d.cuts[fc * kMaxBins + lane * 4 + k];
@@ -1298,13 +1320,12 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   // round trip 1 (uniform scalar loads)
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
-  int64_t G = nodes[n].G, H = nodes[n].H;
-  int pbuild = 1;
-  if (level > 0) pbuild = nodes[(1 << (level - 1)) - 1 + (pos >> 1)].build;
-  if (level == 0) {
-    G = hb[(int64_t)d.ncells * 2];
-    H = hb[(int64_t)d.ncells * 2 + 1];
-  }
+  // unconditional (in-bounds) loads selected after: one round trip, no per-load branch
+  const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
+  const int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
+  const int64_t ng = nodes[n].G, nh = nodes[n].H;
+  const int64_t G = level == 0 ? rg : ng, H = level == 0 ? rh : nh;
+  const int pbuild = level > 0 ? pbuild_raw : 1;
   int it0 = 0, it1 = 0;
   if constexpr (fused) {
     it0 = d.pair_first[pair];
@@ -1553,13 +1574,12 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
   const Node* nodes = d.nodes;
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
-  int64_t G = nodes[n].G, H = nodes[n].H;
-  int pbuild = 1;
-  if (level > 0) pbuild = nodes[(1 << (level - 1)) - 1 + (pos >> 1)].build;
-  if (level == 0) {
-    G = hb[(int64_t)d.ncells * 2];
-    H = hb[(int64_t)d.ncells * 2 + 1];
-  }
+  // unconditional (in-bounds) loads selected after: one round trip, no per-load branch
+  const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
+  const int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
+  const int64_t ng = nodes[n].G, nh = nodes[n].H;
+  const int64_t G = level == 0 ? rg : ng, H = level == 0 ? rh : nh;
+  const int pbuild = level > 0 ? pbuild_raw : 1;
   if (status != kActive) return;  // uniform across the block
   __syncthreads();
   stamp_.probe(1);
@@ -1721,11 +1741,6 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
 // 256-thread blocks with 8192-row items, which keep more independent blocks in flight per CU.
 constexpr int kPartSteps = 32;  // 64-row steps per wave
 
-__device__ __forceinline__ bool goes_left(const uint8_t* col, int r, int j, bool dl) {
-  const int b = col[r];
-  return (b == kMissingBin) ? dl : (b <= j);
-}
-
 template <int kPartWaves>
 __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int parity, int64_t zero_next, int level,
                                                                int chunk) {
@@ -1743,7 +1758,8 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   const int first = (1 << level) - 1;
   const PlanOut pl = block_plan(1 << level, chunk, item, [&](int e) {
     const Node& n = d.nodes[first + e];
-    return (n.status == kSplit && n.count > 0) ? PlanEntry{first + e, 0, n.start, n.count} : PlanEntry{-1, 0, 0, 0};
+    const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
+    return (st == kSplit && cnt > 0) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
   }, s_plan);
   stamp_.probe(1);
   if (pl.node < 0) return;
@@ -1772,10 +1788,16 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
     const int i = wb + k * kWave + lane;
     r[k] = i < we ? (identity ? i : cur[i]) : -1;
   }
+  // the split feature's bins: unconditional loads (padding rows read row 0), so all kPartSteps are in
+  // flight at once -- a load guarded per step made hipcc wait for each in turn (32 round trips)
+  uint8_t bv[kPartSteps];
+#pragma unroll
+  for (int k = 0; k < kPartSteps; ++k) bv[k] = col[max(r[k], 0)];
 #pragma unroll
   for (int k = 0; k < kPartSteps; ++k) {
     const bool valid = r[k] >= 0;
-    const bool left = valid && (d.ablate == 11 ? ((r[k] & 1) != 0) : goes_left(col, r[k], j, dl));
+    const bool gl = bv[k] == kMissingBin ? dl : ((int)bv[k] <= j);
+    const bool left = valid && (d.ablate == 11 ? ((r[k] & 1) != 0) : gl);
     lbits |= (uint32_t)left << k;
     vbits |= (uint32_t)valid << k;
     const uint64_t lm = __ballot(left), vm = __ballot(valid);
@@ -1849,7 +1871,8 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
   const int first = (1 << level) - 1;
   const PlanOut pl = block_plan(1 << level, chunk, item, [&](int e) {
     const Node& n = d.nodes[first + e];
-    return (n.status == kSplit && n.count > 0) ? PlanEntry{first + e, 0, n.start, n.count} : PlanEntry{-1, 0, 0, 0};
+    const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
+    return (st == kSplit && cnt > 0) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
   }, s_plan);
   if (item == 0 && threadIdx.x == 0) d.counters[0] = pl.total;  // work items of the next level's reduce
   if (pl.node < 0) return;
@@ -1890,10 +1913,13 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
     const int i = wb + k * kWave + lane;
     r[k] = i < we ? (identity ? i : cur[i]) : -1;
   }
+  uint8_t bv[kPS];  // unconditional loads: all in flight at once (see k_partition)
+#pragma unroll
+  for (int k = 0; k < kPS; ++k) bv[k] = col[max(r[k], 0)];
 #pragma unroll
   for (int k = 0; k < kPS; ++k) {
     const bool valid = r[k] >= 0;
-    const bool left = valid && goes_left(col, r[k], j, dl);
+    const bool left = valid && (bv[k] == kMissingBin ? dl : ((int)bv[k] <= j));
     lbits |= (uint32_t)left << k;
     vbits |= (uint32_t)valid << k;
     const uint64_t lm = __ballot(left), vm = __ballot(valid);
@@ -2251,8 +2277,10 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
   static const int env_root = getenv("COBALT_ROOT_CHUNK") ? atoi(getenv("COBALT_ROOT_CHUNK")) : 0;
-  const int root_chunk = env_root > 0 ? std::min(16384, std::max(1024, env_root / 64 * 64))
-                                      : std::min(chunk_hist(d, 0), 8192);
+  // (never more root items than the work-item buffers hold)
+  const int root_min = (int)((ceil_div(d.n, (int64_t)c->items_cap - 8) + 63) / 64 * 64);
+  const int root_chunk = std::max(root_min, env_root > 0 ? std::min(16384, std::max(1024, env_root / 64 * 64))
+                                                         : std::min(chunk_hist(d, 0), 8192));
   // Per tree: grad (+ root histogram, node-table init, archive/apply of the previous tree), then per
   // level: [fused: partition of the previous level + this level's histogram | unfused: hist] ->
   // reduce -> [RCCL histogram all-reduce] -> eval [-> unfused: partition]; the last split level's
