@@ -46,6 +46,7 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
 // `old`. They run at VALU latency; __shfl lowers to ds_bpermute, an LDS round trip per step.
 constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
 constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+constexpr int kDppWaveShr1 = 0x138;  // whole-wave shift by one lane (lane i <- lane i - 1; lane 0 <- old)
 
 template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
 __device__ __forceinline__ int dpp32(int v, int old) {

@@ -158,7 +158,6 @@ struct GbdtDev {
   int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
-  int32_t* pair_first;    // [pairs_max + 1] first work item of each pair of the level (k_hist item 0)
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
                           // 4 plan only (k_hist); 11-13 partition (see k_partition)
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
@@ -588,10 +587,8 @@ struct PlanOut {
   int node, slot, begin, end, total;
 };
 
-// `first_out` (one block of the pass, or nullptr): entry e's first work item, [n_ent] = the total --
-// the fused-reduce evaluation reads its pair's item range from it.
 template <class EntryFn>
-__device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int* s_out, int* first_out = nullptr) {
+__device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int* s_out) {
   if (wave_id() == 0) {
     const int lane = lane_id();
     if (lane == 0) s_out[0] = -1;
@@ -603,7 +600,6 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
       const int nch = (en.node >= 0 && en.count > 0) ? (en.count + chunk - 1) / chunk : 0;
       const int incl = wave_incl_scan(nch) + carry;
       const int excl = incl - nch;
-      if (first_out && e < n_ent) first_out[e] = excl;
       if (nch > 0 && item >= excl && item < incl) {
         const int b = en.start + (item - excl) * chunk;
         s_out[0] = en.node;
@@ -614,7 +610,6 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
       carry = readlane32(incl, kWave - 1);
     }
     if (lane == 0) s_out[4] = carry;
-    if (first_out && lane == 0) first_out[n_ent] = carry;
   }
   __syncthreads();
   return PlanOut{s_out[0], s_out[1], s_out[2], s_out[3], s_out[4]};
@@ -954,7 +949,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   const int entries = ft * kMaxBins + kWave;  // tile_entries[y] == ft * 256, + per-lane trash cells
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
-                                s_plan, (item == 0 && blockIdx.y == 0) ? d.pair_first : nullptr);
+                                s_plan);
   // after the plan (storing first would wait for the metadata before the plan's loads go out); the
   // barrier after the row loop publishes it to the flush
   flush_meta_store(fmeta, ft, s_fo, s_fs);
@@ -1210,10 +1205,10 @@ __device__ __forceinline__ double calc_weight(double g, double h, double lambda_
 // subtraction, masks, bin counts, cut values) before computing, so a level costs ~2 dependent memory
 // round trips; the winning candidate carries its cut value (no load after the reduction).
 struct EvalFeat {
-  int f, nb;
+  int f, nb, off;  // feature, bin count, compact cell offset
   bool on;
-  int64_t g[4], h[4];
-  float cut[4], cutm1;  // cut of bins lane*4+k, and of bin lane*4-1 (missing-left splits at b-1)
+  int64_t g[4], h[4];   // bin 64 c + lane of chunk c
+  float cut[4];  // cut of bin 64 c + lane (the bin before it, for missing-left splits, comes by DPP)
 };
 
 // Node decision from its best candidate (split or leaf; children of the last split level become leaves).
@@ -1275,13 +1270,14 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
 // group instead of one per node: the fp64 gain scan of a wide node -- 106 features in the RFE stage --
 // is issue-bound on a single CU); each group writes its best candidate and k_eval_finish reduces them.
 //
-// `fused` (one GPU, deep levels with few work items per pair): k_hist_reduce was not launched; the
-// block sums its pair's per-item slabs itself (items [pair_first[pair], pair_first[pair + 1]), the
-// same exact int64 sums in another order) and the built child's block stores the result in hist_b,
-// where the next level reads it as the parent histogram. Saves the reduce launch (~13 us per level).
-template <bool kGroups, bool kFused>
+// Wave w takes features w and w + nw per pass. A feature's bins are laid out LANE-major in chunks of
+// 64 (bin = 64 c + lane): a feature costs ceil(nb / 64) chunk steps of fp64 gain work -- one for a
+// binary feature, four for a 256-bin one (the former bin-major layout, 4 consecutive bins per lane,
+// cost every feature four) -- and each chunk is one coalesced 16-byte (g, h) load per lane. A chunk's
+// left sums are a DPP int64 wave scan plus the carry of the chunks before it. Candidates, keys and
+// tie-breaks are unchanged, so the trees are bit-identical.
+template <bool kGroups>
 __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg) {
-  constexpr bool fused = kFused;
   BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   const int fbeg = kGroups ? blockIdx.y * fg : 0;
@@ -1290,7 +1286,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   Node* nodes = d.nodes;
   const int pair = level == 0 ? 0 : (pos >> 1);
   const int64_t SE = d.slot_elems;
-  int64_t* hb = d.hist_b[parity] + pair * SE;
+  const int64_t* hb = d.hist_b[parity] + pair * SE;
   int64_t* hs = d.hist_s[parity] + pair * SE;
   const int lane = lane_id();
   const int nw = (int)(blockDim.x / kWave);
@@ -1298,7 +1294,6 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   // Per-feature metadata (mask, bin count, compact offset, cut values) does not depend on the node:
   // it is loaded in the same round trip as the node record (unconditional, in-bounds loads).
   EvalFeat ef[2];
-  int64_t fbase_off[2];
   auto load_meta = [&](int fbase) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1310,177 +1305,165 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       const int nbv = d.nbins[fc];
       e.on = valid && fmv != 0;
       e.nb = valid ? nbv : 0;
-      fbase_off[s] = ((int64_t)d.hoff[fc] + lane * 4) * 2;
+      e.off = d.hoff[fc];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) e.cut[k] = d.cuts[fc * kMaxBins + lane * 4 + k];
-      e.cutm1 = d.cuts[fc * kMaxBins + max(lane * 4 - 1, 0)];
+      for (int c = 0; c < 4; ++c) e.cut[c] = d.cuts[fc * kMaxBins + c * kWave + lane];
     }
   };
   load_meta(fbeg + wave_id());
-  // round trip 1 (uniform scalar loads)
+  // round trip 1 (uniform scalar loads); unconditional (in-bounds) loads selected after
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
-  // unconditional (in-bounds) loads selected after: one round trip, no per-load branch
   const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
   const int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
   const int64_t ng = nodes[n].G, nh = nodes[n].H;
-  const int64_t G = level == 0 ? rg : ng, H = level == 0 ? rh : nh;
+  // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
+  const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
   const int pbuild = level > 0 ? pbuild_raw : 1;
-  int it0 = 0, it1 = 0;
-  if constexpr (fused) {
-    it0 = d.pair_first[pair];
-    it1 = d.pair_first[pair + 1];
-  }
-  if (status != kActive) return;
+  // No early return for an inactive node: a branch here let hipcc sink the feature metadata loads
+  // below it (a third dependent round trip). Its block computes on valid buffers and stores nothing.
+  const bool active = status == kActive;
   stamp_.probe(1);
   __shared__ Cand s_best[16];
   __shared__ float s_cut[16];
   const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
-  const int64_t* parent = nullptr;
+  const int64_t* parent = hb;  // the sibling's parent histogram (unused when this child was built)
   if (!built) {
     const int ppos = pos >> 1;
     const int ppair = level == 1 ? 0 : (ppos >> 1);
     parent = (pbuild ? d.hist_b[parity ^ 1] : d.hist_s[parity ^ 1]) + ppair * SE;
   }
-  const double parent_gain = calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw);
+  // wave-uniform: kept in SGPRs (as a VALU result it held a VGPR pair the candidate loop spilled)
+  const double parent_gain = __longlong_as_double(
+      readlane64(__double_as_longlong(calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw)), 0));
   Cand best;
   best.gain = -INFINITY;
   best.key = 0x7fffffff;
   best.gl = 0;
   best.hl = 0;
   float best_cut = -FLT_MAX;
-  for (int fbase = fbeg + wave_id(); fbase < fend; fbase += 2 * nw) {  // one pass for F <= 32
-  if (fbase != fbeg + wave_id()) load_meta(fbase);
-  // round trip 2: the histogram bins (and the parent's, for the subtraction)
-  if constexpr (fused) {
-    // the pair's per-item slabs, summed here (the parent's bins go out first, they are independent)
-    int64_t ag[2][4], ah[2][4], pg[2][4], ph[2][4];
+  const longlong2* hb2 = reinterpret_cast<const longlong2*>(hb);
+  const longlong2* pa2 = reinterpret_cast<const longlong2*>(readlane64((int64_t)parent, 0));  // uniform base
+  // one pass: a block covers at most 2 features per wave (the host keeps F <= 32 per block)
+  {
+  // round trip 2: the histogram bins (and the parent's, for the subtraction) of both features, all
+  // issued before the first use (clamped cells: the loads need no per-load guard)
+  // (32-bit byte offsets from the uniform bases: the loads take the SGPR-base + VGPR-offset form
+  // instead of a 64-bit VGPR address pair each -- 32 VGPRs the kernel otherwise spilled)
+  longlong2 v[2][4], pv[2][4];
+  uint32_t cofs[2][4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      cofs[s][c] = (uint32_t)(ef[s].off + min(c * kWave + lane, max(ef[s].nb - 1, 0))) * (uint32_t)sizeof(longlong2);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      v[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c]);
+  if (!built) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool in = ef[s].on && lane * 4 + k < ef[s].nb;
-        pg[s][k] = (in && !built) ? parent[fbase_off[s] + 2 * k] : 0;
-        ph[s][k] = (in && !built) ? parent[fbase_off[s] + 2 * k + 1] : 0;
-        ag[s][k] = 0;
-        ah[s][k] = 0;
-      }
-    // unconditional loads (cells clamped into the slab row), masked adds: a guarded load per cell
-    // would make hipcc wait for each one in turn
-    const int ncell = d.ncells;
-    int cidx[2][4];
-    bool cin[2][4];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        cidx[s][k] = min((int)(fbase_off[s] / 2) + k, ncell - 1);
-        cin[s][k] = ef[s].on && lane * 4 + k < ef[s].nb;
-      }
-#pragma unroll 2
-    for (int it = it0; it < it1; ++it) {
-      const uint64_t* row = d.slab + (int64_t)it * ncell;
-      uint64_t v[2][4];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[s][k] = row[cidx[s][k]];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint64_t w = cin[s][k] ? v[s][k] : 0ull;
-          ag[s][k] += (int64_t)(int32_t)(uint32_t)(w >> 32);
-          ah[s][k] += (int64_t)(uint32_t)w;
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      EvalFeat& e = ef[s];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        e.g[k] = built ? ag[s][k] : pg[s][k] - ag[s][k];
-        e.h[k] = built ? ah[s][k] : ph[s][k] - ah[s][k];
-      }
-      if (lane == 0) e.cutm1 = -FLT_MAX;
-    }
-  } else {
+      for (int c = 0; c < 4; ++c)
+        pv[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(pa2) + cofs[s][c]);
+  }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     EvalFeat& e = ef[s];
-    const int64_t base = fbase_off[s];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool in = e.on && lane * 4 + k < e.nb;
-      const int64_t bg = in ? hb[base + 2 * k] : 0, bh = in ? hb[base + 2 * k + 1] : 0;
-      const int64_t pg = (in && !built) ? parent[base + 2 * k] : 0;
-      const int64_t ph = (in && !built) ? parent[base + 2 * k + 1] : 0;
-      e.g[k] = built ? bg : pg - bg;
-      e.h[k] = built ? bh : ph - bh;
+    for (int c = 0; c < 4; ++c) {
+      const bool in = e.on && c * kWave + lane < e.nb;
+      const int64_t g = built ? v[s][c].x : pv[s][c].x - v[s][c].x;
+      const int64_t h = built ? v[s][c].y : pv[s][c].y - v[s][c].y;
+      e.g[c] = in ? g : 0;
+      e.h[c] = in ? h : 0;
     }
-    if (lane == 0) e.cutm1 = -FLT_MAX;
-  }
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const EvalFeat& e = ef[s];
     if (!e.on) continue;
     const int f = e.f, nb = e.nb;
-    if (!built || fused) {  // materialise the sibling (or, fused, the built child's) histogram for the next level
-      int64_t* dst = built ? hb : hs;
-      const int64_t base = ((int64_t)d.hoff[f] + lane * 4) * 2;
+    const int nch = (nb + kWave - 1) / kWave;  // wave-uniform
+    if (!built && active) {  // materialise the sibling histogram for the next level
+      longlong2* hs2 = reinterpret_cast<longlong2*>(hs);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (lane * 4 + k < nb) {
-          dst[base + 2 * k] = e.g[k];
-          dst[base + 2 * k + 1] = e.h[k];
-        }
+      for (int c = 0; c < 4; ++c)
+        if (c < nch && c * kWave + lane < nb) hs2[e.off + c * kWave + lane] = make_longlong2(e.g[c], e.h[c]);
     }
-    int64_t cg[4], ch[4];
-    cg[0] = e.g[0]; ch[0] = e.h[0];
+    // inclusive left sums of every bin: per-chunk wave scans + the carry of the previous chunks
+    int64_t ig[4], ih[4];
+    int64_t cg = 0, ch = 0;
 #pragma unroll
-    for (int k = 1; k < 4; ++k) { cg[k] = cg[k - 1] + e.g[k]; ch[k] = ch[k - 1] + e.h[k]; }
-    const int64_t ig = wave_incl_scan(cg[3]), ih = wave_incl_scan(ch[3]);
-    const int64_t eg = ig - cg[3], eh = ih - ch[3];
-    const int64_t sg = readlane64(ig, kWave - 1), sh = readlane64(ih, kWave - 1);
-    const int64_t mg = G - sg, mh = H - sh;  // missing-value statistics
+    for (int c = 0; c < 4; ++c) {
+      if (c < nch) {
+        const int64_t sg = wave_incl_scan(e.g[c]), sh = wave_incl_scan(e.h[c]);
+        ig[c] = sg + cg;
+        ih[c] = sh + ch;
+        cg += readlane64(sg, kWave - 1);
+        ch += readlane64(sh, kWave - 1);
+      } else {
+        ig[c] = 0;
+        ih[c] = 0;
+      }
+    }
+    const int64_t mg = G - cg, mh = H - ch;  // missing-value statistics
     const bool has_missing = (mg != 0) || (mh != 0);
+    // Candidates, one chunk per iteration of a rolled loop: the chunk's values are rotated down the
+    // register arrays (constant indices), so only one chunk's fp64 temporaries are live at a time
+    // (the unrolled form spilled at the 128-VGPR limit of a 1024-thread block).
+    int64_t rg[4], rh[4], rig[4], rih[4];
+    float rcut[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int b = lane * 4 + k;
-      if (b >= nb) continue;
-      // direction 0: missing -> right, left = bins <= b
-      {
-        const int64_t GL = eg + cg[k], HL = eh + ch[k];
-        const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
-        const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
-        if (hl >= d.mcw && hr >= d.mcw) {
-          Cand c;
-          c.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
-          c.key = f * 1024 + b;
-          c.gl = GL;
-          c.hl = HL;
-          if (cand_better(c, best)) { best = c; best_cut = e.cut[k]; }
+    for (int c = 0; c < 4; ++c) { rg[c] = e.g[c]; rh[c] = e.h[c]; rig[c] = ig[c]; rih[c] = ih[c]; rcut[c] = e.cut[c]; }
+    float carry_cut = -FLT_MAX;  // cut of the previous chunk's last bin
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      // cut of bin b - 1: the previous lane's (DPP wave shift), lane 0 takes lane 63 of chunk c - 1
+      const float cutp = __int_as_float(dpp32<kDppWaveShr1>(__float_as_int(rcut[0]), __float_as_int(carry_cut)));
+      carry_cut = __int_as_float(readlane32(__float_as_int(rcut[0]), kWave - 1));
+      const int b = c * kWave + lane;
+      if (b < nb) {
+        // direction 0: missing -> right, left = bins <= b
+        {
+          const int64_t GL = rig[0], HL = rih[0];
+          const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
+          const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
+          if (hl >= d.mcw && hr >= d.mcw) {
+            Cand cd;
+            cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+            cd.key = f * 1024 + b;
+            cd.gl = GL;
+            cd.hl = HL;
+            if (cand_better(cd, best)) { best = cd; best_cut = rcut[0]; }
+          }
+        }
+        // direction 1: missing -> left, left = bins <= b-1 (+ missing)
+        if (has_missing) {
+          const int64_t GL = rig[0] - rg[0] + mg, HL = rih[0] - rh[0] + mh;
+          const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
+          const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
+          if (hl >= d.mcw && hr >= d.mcw) {
+            Cand cd;
+            cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+            cd.key = f * 1024 + 512 + (nb - 1 - b);
+            cd.gl = GL;
+            cd.hl = HL;
+            if (cand_better(cd, best)) { best = cd; best_cut = b == 0 ? -FLT_MAX : cutp; }
+          }
         }
       }
-      // direction 1: missing -> left, left = bins <= b-1 (+ missing)
-      if (has_missing && b <= nb - 1) {
-        const int64_t GL = eg + cg[k] - e.g[k] + mg, HL = eh + ch[k] - e.h[k] + mh;
-        const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
-        const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
-        if (hl >= d.mcw && hr >= d.mcw) {
-          Cand c;
-          c.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
-          c.key = f * 1024 + 512 + (nb - 1 - b);
-          c.gl = GL;
-          c.hl = HL;
-          if (cand_better(c, best)) { best = c; best_cut = b == 0 ? -FLT_MAX : (k == 0 ? e.cutm1 : e.cut[k - 1]); }
-        }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        rg[k] = rg[k + 1]; rh[k] = rh[k + 1]; rig[k] = rig[k + 1]; rih[k] = rih[k + 1]; rcut[k] = rcut[k + 1];
       }
     }
   }
   }
   stamp_.probe(2);
+  if (!active) return;  // block-uniform
   wave_best(best, best_cut);
   if (lane == 0) { s_best[wave_id()] = best; s_cut[wave_id()] = best_cut; }
   __syncthreads();
@@ -1739,11 +1722,14 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
 // are many and small (measured: removing the claims took a 10M-row level from 58 to 24 us). Small
 // row counts therefore use 1024-thread blocks (fewer, bigger items: ~150 at 1.25M rows); large ones
 // 256-thread blocks with 8192-row items, which keep more independent blocks in flight per CU.
-constexpr int kPartSteps = 32;  // 64-row steps per wave
+constexpr int kPartSteps = 32;  // 64-row steps per wave (maximum; see k_partition's kSteps)
 
-template <int kPartWaves>
+// kSteps: 64-row steps per wave, sized by the host to the item (chunk <= kPartWaves * kSteps * 64):
+// steps past the item would still issue their (unconditional) bin loads and ballots.
+template <int kPartWaves, int kSteps>
 __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int parity, int64_t zero_next, int level,
                                                                int chunk) {
+  constexpr int kPartSteps = kSteps;
   BlockStamp stamp_(d);
   __shared__ int32_t s_cnt[2][kPartWaves];
   __shared__ int32_t s_base[2];
@@ -2071,7 +2057,9 @@ static int chunk_hist(const GbdtDev& d, int level) {
   static const int env1 = getenv("COBALT_HIST_CHUNK") ? atoi(getenv("COBALT_HIST_CHUNK")) : 0;
   if (level == 0) return env0 > 0 ? std::min(16384, std::max(512, env0)) : d.chunk;
   if (env1 > 0) return std::min(16384, std::max(512, env1));
-  return pow2_clamp((d.n / 2 + 383) / 384, 1024, 8192);
+  // <= 4096 rows: with the reduce at ~3 us per level, more, smaller items balance the CUs better
+  // (10M rows: 295.7 vs 304.8 ms per fit with 8192; 2048 is slower again: 311.8)
+  return pow2_clamp((d.n / 2 + 383) / 384, 1024, 4096);
 }
 // Partition item size and block shape (see k_partition); COBALT_PART_CHUNK overrides the size.
 static bool part_wide(const GbdtDev& d) { return d.n < 4000000; }
@@ -2079,7 +2067,9 @@ static int chunk_part(const GbdtDev& d) {
   static const int env = getenv("COBALT_PART_CHUNK") ? atoi(getenv("COBALT_PART_CHUNK")) : 0;
   const int cap = (part_wide(d) ? 16 : 4) * kPartSteps * kWave;
   if (env > 0) return std::min(cap, std::max(1024, env / 1024 * 1024));
-  return 8192;
+  // wide (16-wave) blocks: 4096-row items spread the level over ~2x the CUs (1M rows: 104.7 vs
+  // 106.8 ms per fit); narrow blocks keep 8192 (10M rows: 4096 measured 318.6 vs 304.8 ms)
+  return part_wide(d) ? 4096 : 8192;
 }
 
 static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
@@ -2160,7 +2150,6 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   }
   if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&d.pair_first, ((size_t)c->pairs_max + 1) * sizeof(int32_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.hoff, (F + 1) * sizeof(int32_t)))) return rc;
@@ -2252,6 +2241,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
   static const int env_fg = getenv("COBALT_EVAL_FG") ? atoi(getenv("COBALT_EVAL_FG")) : -1;
   int eval_fg = env_fg >= 0 ? env_fg : (d.F > 32 ? 8 : 0);
+  if (eval_fg == 0 && d.F > 32) eval_fg = 8;  // one k_eval block evaluates at most 32 features
   if (eval_fg > 0) eval_fg = std::min(32, std::max(eval_fg, ceil_div(d.F, 64)));
   // compact-cell evaluation for narrow data (COBALT_EVAL_COMPACT=1; default: the F x 256-slot k_eval)
   // Opt-in: measured 14.2 vs 13.5 us per node-level at 1M rows and 106 vs 109 us per tree at 10M
@@ -2265,15 +2255,6 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // measures slower than the separate passes (COBALT_FUSED_PART=1)
   const bool env_fuse_part = getenv("COBALT_FUSED_PART") != nullptr && atoi(getenv("COBALT_FUSED_PART")) != 0;
   const bool fuse_part = fuse_root && env_fuse_part;
-  // reduce fused into k_eval<false> (one GPU) at levels with at most `fused_max` work items per pair
-  // (upper bound: ub / pairs); COBALT_FUSED_REDUCE overrides (0 = off)
-  static const int env_fused = getenv("COBALT_FUSED_REDUCE") ? atoi(getenv("COBALT_FUSED_REDUCE")) : -1;
-  const int fused_max = env_fused >= 0 ? env_fused : 0;
-  auto fused_level = [&](int lv) {
-    if (dp || fuse_part || eval_fg > 0 || eval_compact || lv < 1 || lv >= D || fused_max <= 0) return false;
-    const int ub_lv = ceil_div(d.n, chunk_hist(d, lv)) + (1 << lv);
-    return ceil_div(ub_lv, 1 << (lv - 1)) <= fused_max;
-  };
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
   static const int env_root = getenv("COBALT_ROOT_CHUNK") ? atoi(getenv("COBALT_ROOT_CHUNK")) : 0;
@@ -2320,10 +2301,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           GLAUNCH("k_hist", k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level,
                   chh);
       }
-      const bool fused = fused_level(level);
-      if (!fused)
-        GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
-                dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap));
+      GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
+              dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap));
       CK_LAUNCH();
       if (dp) {
         // row-count choice: ranks built their locally smaller child -> turn it into the local LEFT
@@ -2339,26 +2318,32 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       }
       if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
         const int ng = ceil_div(d.F, eval_fg);
-        GLAUNCH("k_eval", (k_eval<true, false>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d,
-                level, parity, t, eval_fg);
+        GLAUNCH("k_eval", k_eval<true>, dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d, level,
+                parity, t, eval_fg);
         GLAUNCH("k_eval_finish", k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
       } else if (eval_compact) {
         GLAUNCH("k_eval", k_eval_compact, dim3(1 << level), dim3(kEvalThreads), 0, stream, d, level, parity, t);
       } else {
-        if (fused)
-          GLAUNCH("k_eval", (k_eval<false, true>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
-        else
-          GLAUNCH("k_eval", (k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
+        GLAUNCH("k_eval", k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
       }
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
-        // a fused next level stores its histograms instead of accumulating them: nothing to zero
-        const int64_t zero_next = fused_level(level + 1) ? 0 : (int64_t)(1 << level) * d.slot_elems;
-        if (part_wide(d))
-          GLAUNCH("k_partition", k_partition<16>, dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next, level, chp);
+        const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;
+        const int pw = part_wide(d) ? 16 : 4;
+        const int steps = ceil_div(chp, pw * kWave);  // <= kPartSteps (chunk_part's cap)
+        if (pw == 16 && steps <= 4)
+          GLAUNCH("k_partition", (k_partition<16, 4>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
+                  level, chp);
+        else if (pw == 16 && steps <= 8)
+          GLAUNCH("k_partition", (k_partition<16, 8>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
+                  level, chp);
+        else if (pw == 16)
+          GLAUNCH("k_partition", (k_partition<16, kPartSteps>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity,
+                  zero_next, level, chp);
         else
-          GLAUNCH("k_partition", k_partition<4>, dim3(ubp), dim3(4 * kWave), 0, stream, d, parity, zero_next, level, chp);
+          GLAUNCH("k_partition", (k_partition<4, kPartSteps>), dim3(ubp), dim3(4 * kWave), 0, stream, d, parity,
+                  zero_next, level, chp);
       }
       CK_LAUNCH();
     }
