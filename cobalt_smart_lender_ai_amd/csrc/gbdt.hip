@@ -677,8 +677,12 @@ struct HistLanes {
   uint64_t fbits;                 // colsample mask of the tile's features
   uint64_t fullbits;              // 256-bin features (no missing values): code 255 is a real bin
   uint32_t sh0, sh1, sh2, sh3;    // 3-bit copy shifts per feature, 8 features per word (SGPRs)
-  uint32_t trash;                 // per-lane trash cell (missing values, disabled features)
+  uint32_t trash;                 // per-lane trash cell (generic path: missing values, disabled features)
   uint32_t lane;
+  // 32-byte record path (hist_add_rec32): per feature fl of the tile, fm = nbins | (copy shift + 3) << 16
+  // (uniform -> SGPRs) and lb8 = this lane's byte offset of its copy of the feature's bin 0 (VGPRs)
+  uint32_t fm[24];
+  uint32_t lb8[24];
 };
 
 // Per-tile feature state for the LDS histogram lanes. Lane k loads feature f0 + k's colsample bit and
@@ -688,7 +692,7 @@ struct HistLanes {
 // them together with its other independent loads (work plan, flush offsets): one round trip for all.
 struct HistLaneRaw {
   bool on, full;
-  int sh;
+  int sh, nb;
 };
 
 __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tree, int f0, int ft) {
@@ -699,10 +703,12 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   // unconditional loads (f is clamped), masked after: both in one round trip
   const uint8_t fmv = d.fmask[(int64_t)tree * d.F + f];
   const int ly0 = d.layout[f].y;
+  const int nb0 = d.nbins[f];
   r.on = in && fmv != 0;
   const int ly = in ? ly0 : 0;
   r.sh = ly & 7;
   r.full = (ly & 8) != 0;
+  r.nb = in ? min(max(nb0, 1), kMaxBins) : 1;
   return r;
 }
 
@@ -722,6 +728,16 @@ __device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, i
     switch (fl >> 3) { case 0: hl.sh0 |= v; break; case 1: hl.sh1 |= v; break; case 2: hl.sh2 |= v; break; default: hl.sh3 |= v; }
   }
   hl.trash = (uint32_t)(ft * kMaxBins) + hl.lane;
+  // features past the tile or masked out by colsample: nbins 0 -> every row adds into this lane's trash
+  // cell (the row loop then has no per-feature branch)
+  const uint32_t mv = on ? ((uint32_t)raw.nb | ((uint32_t)(sh + 3) << 16)) : (3u << 16);
+#pragma unroll
+  for (int fl = 0; fl < 24; ++fl) {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mv, fl);
+    hl.fm[fl] = m;
+    hl.lb8[fl] = (m & 0xffffu) ? ((uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << ((m >> 16) - 3)) - 1u))) * 8u
+                               : hl.trash * 8u;
+  }
   return hl;
 }
 
@@ -730,22 +746,25 @@ __device__ __forceinline__ HistLanes hist_lanes(const GbdtDev& d, int tree, int 
 }
 
 // Add one 32-byte record (bins in a.xyzw / b.xy, packed (g, h) in b.wz) to the LDS histogram.
-__device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes& hl, int ft, const uint4& a,
+// Per feature: byte extract, clamp, shift-add, ds_add_u64 (3 VALU ops per atomic). The missing code
+// 255 clamps to cell nbins, which the layout keeps inside the feature's 256 cells and the flush never
+// reads (a 256-bin feature has no missing values: its code 255 is a real bin); features masked out by
+// colsample, and the tile's padding up to FT4 (= features rounded up to 4), add into a trash cell.
+template <int FT4>
+__device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes& hl, const uint4& a,
                                                const uint4& b) {
+  static_assert(FT4 % 4 == 0 && FT4 > 0 && FT4 <= 24, "32-byte records hold <= 24 bins");
   const uint64_t gp = ((uint64_t)b.w << 32) | b.z;
+  char* base = reinterpret_cast<char*>(s_hist);
 #pragma unroll
-  for (int fl = 0; fl < 24; ++fl) {
-    if (fl < ft) {
-      const bool fen = (hl.fbits >> fl) & 1ull;
-      const uint32_t shw = fl < 8 ? hl.sh0 : (fl < 16 ? hl.sh1 : hl.sh2);
-      const uint32_t sh = (shw >> (3 * (fl & 7))) & 7u;
-      const uint32_t cbase = (uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << sh) - 1u));
+  for (int fl = 0; fl < FT4; ++fl) {
+    {
+      const uint32_t m = hl.fm[fl];
       const int q = fl >> 2;
       const uint32_t word = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : b.y;
       const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
-      const bool real = bb != kMissingBin || ((hl.fullbits >> fl) & 1ull);
-      const uint32_t cell = (real && fen) ? cbase + (bb << sh) : hl.trash;
-      atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp);
+      const uint32_t off = hl.lb8[fl] + (min(bb, m & 0xffffu) << (m >> 16));
+      atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
     }
   }
 }
@@ -824,7 +843,7 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // holding the freshly quantised (g, h) and the bins -- the separate root histogram pass (a full
 // 32 B/row re-read) disappears. Block b = root work item b: rows [b*chunk, (b+1)*chunk).
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
-template <int U>
+template <int U, int FT4>
 __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_dyn[];
@@ -921,7 +940,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
       reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
       tg += gq;
       th += hq;
-      hist_add_rec32(s_hist, hl, ft, ra[u], rb[u]);
+      hist_add_rec32<FT4>(s_hist, hl, ra[u], rb[u]);
     }
   }
   __syncthreads();
@@ -931,6 +950,8 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
 
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 
+// FT4 > 0: 32-byte records with one tile of <= FT4 features (FT4 = F rounded up to 4); 0: generic rows.
+template <int FT4>
 __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk) {
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_hist[];
@@ -976,15 +997,19 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   const int B = blockDim.x;
   constexpr int U = 4;  // rows in flight per thread
   const uint32_t trash = hl.trash;
-  if (d.stride == 32 && ft == d.F && ft <= 24) {
+  if constexpr (FT4 > 0) {
     // 32-byte records (bins | pad | (g,h)): one pair of 16-byte loads per row
     // software pipeline: the row ids of iteration k+1 are loaded while iteration k's records are in
     // flight, so each iteration waits on one memory round trip instead of two (ridx -> record)
+    // row-id loads are unconditional at a clamped index and masked after (a load guarded per row
+    // sits in its own exec branch, and the waits around it cover every load in flight)
+    const int ilast = max(w.end - 1, w.begin);
     int rn[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = w.begin + threadIdx.x + u * B;
-      rn[u] = i < w.end ? (identity ? i : rix[i]) : -1;
+      const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
+      rn[u] = i < w.end ? rv : -1;
     }
     for (int i0 = w.begin + threadIdx.x; i0 < w.end; i0 += U * B) {
       int r[U];
@@ -996,11 +1021,13 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
         const uint4* rec = reinterpret_cast<const uint4*>(d.bins + (int64_t)(r[u] >= 0 ? r[u] : r[0]) * 32);
         a[u] = rec[0];
         b2[u] = rec[1];
+        asm volatile("" : "+v"(b2[u].y));  // keep two 16-byte loads per row when bins 20-23 are unused
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + U * B + u * B;
-        rn[u] = i < w.end ? (identity ? i : rix[i]) : -1;
+        const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
+        rn[u] = i < w.end ? rv : -1;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1009,7 +1036,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
         th += (int64_t)b2[u].z;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) hist_add_rec32(s_hist, hl, ft, a[u], b2[u]);
+      for (int u = 0; u < U; ++u) hist_add_rec32<FT4>(s_hist, hl, a[u], b2[u]);
     }
   } else {
   const int nchunks = (ft + 7) >> 3;
@@ -1769,10 +1796,13 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   static_assert(kPartSteps <= 32, "step bit masks are 32-bit");
   uint32_t lbits = 0, vbits = 0;
   int nl = 0, nr = 0;
+  // row ids: unconditional loads at a clamped index (w.end - 1 is a row of this item), masked after
 #pragma unroll
   for (int k = 0; k < kPartSteps; ++k) {
     const int i = wb + k * kWave + lane;
-    r[k] = i < we ? (identity ? i : cur[i]) : -1;
+    const int ic = min(i, w.end - 1);
+    const int rv = identity ? ic : cur[ic];
+    r[k] = i < we ? rv : -1;
   }
   // the split feature's bins: unconditional loads (padding rows read row 0), so all kPartSteps are in
   // flight at once -- a load guarded per step made hipcc wait for each in turn (32 round trips)
@@ -1942,7 +1972,7 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
       if ((want >> (k0 + u)) & 1u) {
         tg += (int64_t)(int32_t)b[u].w;
         th += (int64_t)b[u].z;
-        hist_add_rec32(s_hist, hl, F, a[u], b[u]);
+        hist_add_rec32<24>(s_hist, hl, a[u], b[u]);
       }
     }
   }
@@ -2072,6 +2102,36 @@ static int chunk_part(const GbdtDev& d) {
   return part_wide(d) ? 4096 : 8192;
 }
 
+// Histogram kernels by record shape: FT4 = F rounded up to 4 for 32-byte records with one feature tile
+// (<= 24 features), 0 otherwise (generic rows / several tiles; the fused root pass is not used then).
+typedef void (*HistKernel)(GbdtDev, int, int, int, int);
+typedef void (*GradHistKernel)(GbdtDev, int, int, int);
+static int hist_ft4(const GbdtDev& d) {
+  return (d.stride == 32 && d.F <= 24 && d.feat_tile >= d.F) ? (d.F + 3) / 4 * 4 : 0;
+}
+static HistKernel hist_kernel(int ft4) {
+  switch (ft4) {
+    case 4: return k_hist<4>;
+    case 8: return k_hist<8>;
+    case 12: return k_hist<12>;
+    case 16: return k_hist<16>;
+    case 20: return k_hist<20>;
+    case 24: return k_hist<24>;
+    default: return k_hist<0>;
+  }
+}
+static GradHistKernel grad_hist_kernel(int ft4) {
+  switch (ft4) {
+    case 4: return k_grad_hist<2, 4>;
+    case 8: return k_grad_hist<2, 8>;
+    case 12: return k_grad_hist<2, 12>;
+    case 16: return k_grad_hist<2, 16>;
+    case 20: return k_grad_hist<2, 20>;
+    case 24: return k_grad_hist<2, 24>;
+    default: return nullptr;
+  }
+}
+
 static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
   CK(hipMalloc(p, bytes < 16 ? 16 : bytes));
   c->allocs.push_back(*p);
@@ -2189,8 +2249,10 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
     int off = 0;
     for (int f = t * ft; f < std::min(F, (t + 1) * ft); ++f) {
       const int b = std::max(1, std::min(256, nb[f]));
+      // copies = 2^sh with (nb + 1) * copies <= 256: the clamped missing code (cell nb, see
+      // hist_add_rec32) stays inside the feature's cells; a 256-bin feature has one copy
       int sh = 0;
-      while (sh < 6 && (b << (sh + 1)) <= kMaxBins) ++sh;  // copies = 2^sh, nb * copies <= 256
+      while (sh < 6 && ((b + 1) << (sh + 1)) <= kMaxBins) ++sh;
       // bit 3: a 256-bin feature (no missing values; code 255 is its real bin 255)
       lay[f] = make_int2((f - t * ft) * kMaxBins, sh | (b >= 256 ? 8 : 0));
       off += kMaxBins;
@@ -2207,15 +2269,15 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   CK(hipMemcpy(c->d.tile_entries, ent.data(), ntiles * sizeof(int32_t), hipMemcpyHostToDevice));
   c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t);
   if (c->lds_hist > 64 * 1024) {
-    CK(hipFuncSetAttribute((const void*)k_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
+    CK(hipFuncSetAttribute((const void*)hist_kernel(hist_ft4(c->d)), hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)c->lds_hist));
     CK(hipFuncSetAttribute((const void*)k_part_hist<kPartHistWaves, kPartHistSteps>,
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
   const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
-  if (grad_hist_lds > 64 * 1024) {
-    CK(hipFuncSetAttribute((const void*)k_grad_hist<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
-    CK(hipFuncSetAttribute((const void*)k_grad_hist<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
-  }
+  if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d)))
+    CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d)), hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)grad_hist_lds));
   return 0;
 }
 
@@ -2235,7 +2297,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const bool dp = c->cfg.comm != nullptr;
   d.dp = dp ? 1 : 0;
   // gradients + root histogram in one pass (32-byte records, one feature tile)
-  const bool fuse_root = !sampled && d.stride == 32 && d.F <= 24 && ftiles == 1 && d.ablate == 0 &&
+  const int ft4 = hist_ft4(d);
+  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && d.ablate == 0 &&
                          getenv("COBALT_NO_FUSED_ROOT") == nullptr;
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
@@ -2249,8 +2312,6 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const int env_compact = getenv("COBALT_EVAL_COMPACT") ? atoi(getenv("COBALT_EVAL_COMPACT")) : 0;
   const bool eval_compact = eval_fg == 0 && env_compact != 0 && d.F <= kEvalMaxF &&
                             d.ncells <= kEvalThreads * kEvalCPT;
-  // rows in flight per thread in the gradient + root histogram pass (COBALT_GRAD_U=4: +1%, within noise)
-  static const int grad_u = getenv("COBALT_GRAD_U") ? atoi(getenv("COBALT_GRAD_U")) : 2;
   // partition fused with the next level's histogram (same record-layout conditions); opt-in while it
   // measures slower than the separate passes (COBALT_FUSED_PART=1)
   const bool env_fuse_part = getenv("COBALT_FUSED_PART") != nullptr && atoi(getenv("COBALT_FUSED_PART")) != 0;
@@ -2275,12 +2336,9 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     if (sampled)
       GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
               stream, d);
-    else if (fuse_root && grad_u == 4)
-      GLAUNCH("k_grad_hist", k_grad_hist<4>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
-              d, t, apply, root_chunk);
     else if (fuse_root)
-      GLAUNCH("k_grad_hist", k_grad_hist<2>, dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds, stream,
-              d, t, apply, root_chunk);
+      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
+              stream, d, t, apply, root_chunk);
     else
       GLAUNCH("k_grad", k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
     if (apply >= 0 && !sampled) c->applied = t;
@@ -2298,8 +2356,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
         ub = ceil_div(d.n, chh) + (1 << level);
         if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-          GLAUNCH("k_hist", k_hist, dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t, level,
-                  chh);
+          GLAUNCH("k_hist", hist_kernel(ft4), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t,
+                  level, chh);
       }
       GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
               dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap));
