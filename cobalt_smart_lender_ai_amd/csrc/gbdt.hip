@@ -6,7 +6,7 @@
 //
 // Design (MI355X-first, not a translation of XGBoost's CPU/CUDA code):
 //  * Features are pre-quantised to uint8 bins (<= 255 real bins + code 255 = missing; 256 real bins
-//    for a feature without missing values, see HistLanes.fullbits), stored twice:
+//    for a feature without missing values, see hist_add_rec32), stored twice:
 //    row-major [N][stride] for histogram gathers (one row = a few dwords) and feature-major
 //    [F][N] for the partition step (one byte per row, coalesced within a node).
 //  * Gradients are quantised to fixed point and packed into one u64 per row
@@ -675,9 +675,7 @@ __device__ void publish_level(const GbdtDev& d, int level, int total, bool keep_
 // LDS histogram helpers shared by k_hist and k_grad_hist (32-byte record fast path).
 struct HistLanes {
   uint64_t fbits;                 // colsample mask of the tile's features
-  uint64_t fullbits;              // 256-bin features (no missing values): code 255 is a real bin
-  uint32_t sh0, sh1, sh2, sh3;    // 3-bit copy shifts per feature, 8 features per word (SGPRs)
-  uint32_t trash;                 // per-lane trash cell (generic path: missing values, disabled features)
+  uint32_t trash;                 // per-lane trash cell (masked / padding features of the 32-byte path)
   uint32_t lane;
   // 32-byte record path (hist_add_rec32): per feature fl of the tile, fm = nbins | (copy shift + 3) << 16
   // (uniform -> SGPRs) and lb8 = this lane's byte offset of its copy of the feature's bin 0 (VGPRs)
@@ -691,7 +689,7 @@ struct HistLanes {
 // The loads are split from the ballots (hist_lanes_load / hist_lanes_finish) so a kernel can issue
 // them together with its other independent loads (work plan, flush offsets): one round trip for all.
 struct HistLaneRaw {
-  bool on, full;
+  bool on;
   int sh, nb;
 };
 
@@ -707,33 +705,37 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   r.on = in && fmv != 0;
   const int ly = in ? ly0 : 0;
   r.sh = ly & 7;
-  r.full = (ly & 8) != 0;
   r.nb = in ? min(max(nb0, 1), kMaxBins) : 1;
   return r;
 }
 
-__device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, int ft) {
+// Per-feature histogram metadata of lane fl's feature: nbins | (copy shift + 3) << 16; a feature past
+// the tile or masked out by colsample gets nbins 0 (the 32-byte path adds it into a trash cell).
+__device__ __forceinline__ uint32_t hist_meta(const HistLaneRaw& raw) {
+  return raw.on ? ((uint32_t)raw.nb | ((uint32_t)(raw.sh + 3) << 16)) : (3u << 16);
+}
+
+// Stage the metadata of the tile's features in LDS (s_fm[64], lane fl = feature fl) from ONE wave: the
+// row loops read it back with a uniform LDS load + readfirstlane, which is correct under any exec
+// mask (a readlane of a lane that is inactive where the compiler places it would read a stale VGPR).
+// A caller's later barrier publishes it. Using the block's last wave keeps wave 0 -- the work planner
+// -- from waiting on the metadata loads before it issues the plan's.
+__device__ __forceinline__ void hist_meta_store(const HistLaneRaw& raw, uint32_t* s_fm) {
+  if (wave_id() == (int)(blockDim.x / kWave) - 1) s_fm[lane_id()] = hist_meta(raw);
+}
+
+__device__ __forceinline__ uint32_t hist_meta_of(const uint32_t* s_fm, int fl) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fm[fl]);
+}
+
+__device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, int ft, const uint32_t* s_fm) {
   HistLanes hl;
   hl.lane = lane_id();
-  const bool in = (int)hl.lane < ft;
-  const bool on = raw.on;
-  const int sh = raw.sh;
-  hl.fbits = __ballot(on);
-  hl.fullbits = __ballot(raw.full);
-  const uint64_t b0 = __ballot(in && (sh & 1)), b1 = __ballot(in && (sh & 2)), b2 = __ballot(in && (sh & 4));
-  hl.sh0 = hl.sh1 = hl.sh2 = hl.sh3 = 0;
-  for (int fl = 0; fl < ft; ++fl) {
-    const uint32_t v = (uint32_t)(((b0 >> fl) & 1ull) | (((b1 >> fl) & 1ull) << 1) | (((b2 >> fl) & 1ull) << 2))
-                       << (3 * (fl & 7));
-    switch (fl >> 3) { case 0: hl.sh0 |= v; break; case 1: hl.sh1 |= v; break; case 2: hl.sh2 |= v; break; default: hl.sh3 |= v; }
-  }
+  hl.fbits = __ballot(raw.on);
   hl.trash = (uint32_t)(ft * kMaxBins) + hl.lane;
-  // features past the tile or masked out by colsample: nbins 0 -> every row adds into this lane's trash
-  // cell (the row loop then has no per-feature branch)
-  const uint32_t mv = on ? ((uint32_t)raw.nb | ((uint32_t)(sh + 3) << 16)) : (3u << 16);
 #pragma unroll
   for (int fl = 0; fl < 24; ++fl) {
-    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)mv, fl);
+    const uint32_t m = hist_meta_of(s_fm, fl);
     hl.fm[fl] = m;
     hl.lb8[fl] = (m & 0xffffu) ? ((uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << ((m >> 16) - 3)) - 1u))) * 8u
                                : hl.trash * 8u;
@@ -741,9 +743,6 @@ __device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, i
   return hl;
 }
 
-__device__ __forceinline__ HistLanes hist_lanes(const GbdtDev& d, int tree, int f0, int ft) {
-  return hist_lanes_finish(hist_lanes_load(d, tree, f0, ft), ft);
-}
 
 // Add one 32-byte record (bins in a.xyzw / b.xy, packed (g, h) in b.wz) to the LDS histogram.
 // Per feature: byte extract, clamp, shift-add, ds_add_u64 (3 VALU ops per atomic). The missing code
@@ -844,11 +843,13 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // 32 B/row re-read) disappears. Block b = root work item b: rows [b*chunk, (b+1)*chunk).
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
 template <int U, int FT4>
+// (no waves-per-EU bound: capping it at 80 VGPRs spills, 276.5 vs 269.7 ms per 10M fit)
 __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_dyn[];
   __shared__ int64_t s_tot[2][16];
   __shared__ int s_fo[kMaxFeatTile + 1], s_fs[kMaxFeatTile];
+  __shared__ uint32_t s_fm[kWave];
   const int ft = d.F;
   const int entries = ft * kMaxBins + kWave;  // one tile: tile_entries[0] == F * 256
   // independent metadata loads first (they share the round trip of the previous tree's node table)
@@ -876,6 +877,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   }
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
   flush_meta_store(fmeta, ft, s_fo, s_fs);
+  hist_meta_store(lraw, s_fm);
   __syncthreads();
   stamp_.probe(1);
   const int item = blockIdx.x;
@@ -885,7 +887,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
     w.node = 0; w.slot = 0; w.begin = (int32_t)begin; w.end = (int32_t)end;
     d.items_h[item] = w;
   }
-  const HistLanes hl = hist_lanes_finish(lraw, ft);
+  const HistLanes hl = hist_lanes_finish(lraw, ft, s_fm);
   const uint64_t tree_key = tree_key_of(d.seed, tree);
   const uint64_t dkey = splitmix64(tree_key ^ kDitherSalt);
   int64_t tg = 0, th = 0;
@@ -951,8 +953,10 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 
 // FT4 > 0: 32-byte records with one tile of <= FT4 features (FT4 = F rounded up to 4); 0: generic rows.
+// (6 waves per SIMD = the 3 blocks per CU that the LDS tile allows: keeps the kernel within 80 VGPRs)
 template <int FT4>
-__global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, int tree, int level, int chunk) {
+__global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_hist(
+    GbdtDev d, int parity, int tree, int level, int chunk) {
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_hist[];
   __shared__ int64_t s_tot[2][16];
@@ -969,6 +973,8 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   const FlushMeta fmeta = flush_meta_load(d, tree, f0, ft);
   const int entries = ft * kMaxBins + kWave;  // tile_entries[y] == ft * 256, + per-lane trash cells
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
+  __shared__ uint32_t s_fm[kWave];
+  hist_meta_store(lraw, s_fm);  // (last wave; block_plan's barrier publishes it)
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
                                 s_plan);
   // after the plan (storing first would wait for the metadata before the plan's loads go out); the
@@ -984,9 +990,8 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   w.end = pl.end;
   if (blockIdx.y == 0 && threadIdx.x == 0) d.items_h[item] = w;
   if (d.ablate == 4) return;  // timing-only: plan + publish only
-  const HistLanes hl = hist_lanes_finish(lraw, ft);
+  const HistLanes hl = hist_lanes_finish(lraw, ft, s_fm);
   const uint64_t fbits = hl.fbits;
-  const uint32_t sh0 = hl.sh0, sh1 = hl.sh1, sh2 = hl.sh2, sh3 = hl.sh3;
   stamp_.probe(2);
 
   const int32_t* rix = d.ridx[parity];
@@ -996,7 +1001,6 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
   constexpr int U = 4;  // rows in flight per thread
-  const uint32_t trash = hl.trash;
   if constexpr (FT4 > 0) {
     // 32-byte records (bins | pad | (g,h)): one pair of 16-byte loads per row
     // software pipeline: the row ids of iteration k+1 are loaded while iteration k's records are in
@@ -1063,21 +1067,21 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(GbdtDev d, int parity, in
         lo[u] = row[0];
         hi[u] = (c * 8 + 4 < ft) ? row[1] : 0xFFFFFFFFu;
       }
-      const uint32_t shc = c == 0 ? sh0 : (c == 1 ? sh1 : (c == 2 ? sh2 : sh3));
       const uint32_t fbc = (uint32_t)(fbits >> (c * 8)) & 0xFFu;
-      const uint32_t flc = (uint32_t)(hl.fullbits >> (c * 8)) & 0xFFu;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         if ((fbc >> k) & 1u) {
-          const uint32_t sh = (shc >> (3 * k)) & 7u;
-          const uint32_t cbase = (uint32_t)((c * 8 + k) * kMaxBins) + (lane & ((1u << sh) - 1u));
+          // as hist_add_rec32: the missing code clamps to the feature's unread cell nbins
+          const uint32_t m = hist_meta_of(s_fm, c * 8 + k);
+          const uint32_t nb = m & 0xffffu, sh3 = m >> 16;
+          const uint32_t lb8 = ((uint32_t)((c * 8 + k) * kMaxBins) + (lane & ((1u << (sh3 - 3)) - 1u))) * 8u;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            // branch-free: missing values (and padded rows, gp == 0) add into a per-lane trash cell
             const uint32_t b = ((k < 4 ? lo[u] : hi[u]) >> (8 * (k & 3))) & 0xffu;
-            const uint32_t cell = (b != kMissingBin || ((flc >> k) & 1u)) ? cbase + (b << sh) : trash;
-            if (d.ablate == 1) tg += cell; else
-            atomicAdd(reinterpret_cast<unsigned long long*>(&s_hist[cell]), (unsigned long long)gp[u]);
+            const uint32_t off = lb8 + (min(b, nb) << sh3);
+            if (d.ablate == 1) tg += off; else
+            atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_hist) + off),
+                      (unsigned long long)gp[u]);
           }
         }
       }
@@ -1906,9 +1910,11 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
   const int F = d.F;
   const int entries = d.tile_entries[0] + kWave;  // + per-lane trash cells
   for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
-  const HistLanes hl = hist_lanes(d, tree, 0, F);
+  const HistLaneRaw lraw = hist_lanes_load(d, tree, 0, F);
   __shared__ int s_fo[kMaxFeatTile + 1], s_fs[kMaxFeatTile];
+  __shared__ uint32_t s_fm[kWave];
   flush_meta_store(flush_meta_load(d, tree, 0, F), F, s_fo, s_fs);  // published by the barrier below
+  hist_meta_store(lraw, s_fm);
 
   // pass 1: row ids + split-feature bins -> directions and per-wave counts (rows stay in registers)
   const bool identity = parity == 0 && q == 0;
@@ -1944,6 +1950,7 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
   }
   if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nr; }
   __syncthreads();  // (also orders the LDS histogram zeroing before the atomics below)
+  const HistLanes hl = hist_lanes_finish(lraw, F, s_fm);
   unsigned long long claim = 0;
   if (threadIdx.x == 0) {
     int tl = 0, tr = 0;
