@@ -159,7 +159,7 @@ struct GbdtDev {
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
-                          // 4 plan only (k_hist); 11-13 partition (see k_partition)
+                          // 4 plan only (k_hist); 12 partition without the cursor claims
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
   int32_t by_hess;        // build k_eval's (global) hessian choice: DP default, COBALT_BUILD_BY_HESS on one GPU
   CandRec* cand;          // [2^(max_depth-1)][64] per-group split candidates (grouped evaluation)
@@ -1792,14 +1792,15 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   const uint8_t* col = d.binsT + (int64_t)nd.feat * d.ldt;
   const int j = nd.bin;
   const bool dl = nd.default_left != 0;
-  const int wv = wave_id(), lane = lane_id();
+  // wave index as a uniform (SGPR) value: the per-step row counts and prefix masks stay scalar
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
   const int len = w.end - w.begin;
   const int per = ((len + kPartWaves - 1) / kPartWaves + kWave - 1) / kWave * kWave;
   const int wb = min(w.end, w.begin + wv * per), we = min(w.end, wb + per);
   int r[kPartSteps];
   static_assert(kPartSteps <= 32, "step bit masks are 32-bit");
-  uint32_t lbits = 0, vbits = 0;
-  int nl = 0, nr = 0;
+  uint32_t lbits = 0;
+  int nl = 0, nv = 0;
   // row ids: unconditional loads at a clamped index (w.end - 1 is a row of this item), masked after
 #pragma unroll
   for (int k = 0; k < kPartSteps; ++k) {
@@ -1813,18 +1814,25 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   uint8_t bv[kPartSteps];
 #pragma unroll
   for (int k = 0; k < kPartSteps; ++k) bv[k] = col[max(r[k], 0)];
+  // Pass 1 in integer arithmetic (boolean forms compiled to per-step branches and spilled masks): the
+  // direction bit of each row (bin <= j, or the default direction for the missing code) goes to bit k of
+  // lbits (0 for the padding lanes, r = -1). The valid rows of step k are a prefix of the lanes (rows
+  // wb + 64 k + lane < we), so the wave's valid count is we - wb.
+  const int jm1 = j + 1;  // left <=> bin - (j + 1) < 0
+  const uint32_t dlv = dl ? 1u : 0u;
+  nv = max(0, we - wb);
 #pragma unroll
   for (int k = 0; k < kPartSteps; ++k) {
-    const bool valid = r[k] >= 0;
-    const bool gl = bv[k] == kMissingBin ? dl : ((int)bv[k] <= j);
-    const bool left = valid && (d.ablate == 11 ? ((r[k] & 1) != 0) : gl);
-    lbits |= (uint32_t)left << k;
-    vbits |= (uint32_t)valid << k;
-    const uint64_t lm = __ballot(left), vm = __ballot(valid);
-    nl += __popcll(lm);
-    nr += __popcll(vm) - __popcll(lm);
+    const uint32_t b = bv[k];
+    const uint32_t lt = (uint32_t)((int)b - jm1) >> 31;  // bin <= j
+    const uint32_t ms = (b + 1u) >> 8;                    // bin == 255 (missing)
+    const uint32_t ok = ~(uint32_t)r[k] >> 31;            // a row, not padding
+    const uint32_t left = (lt | (ms & dlv)) & ok;
+    lbits |= left << k;
+    nl += __popcll(__ballot(left != 0u));
   }
-  if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nr; }
+  asm volatile("" : "+v"(lbits));  // pass 2 reads the packed bits (not 32 live per-step values)
+  if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nv - nl; }
   __syncthreads();
   stamp_.probe(2);
   if (threadIdx.x == 0) {
@@ -1843,17 +1851,22 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   stamp_.probe(3);
   int bl = s_base[0], br = s_base[1];
   for (int k = 0; k < wv; ++k) { bl += s_cnt[0][k]; br += s_cnt[1][k]; }
-  const int rend = nd.start + nd.count - 1;
+  // Pass 2: one destination per lane (left rows ascending from the node start, right rows descending
+  // from its end), one store per step under the valid-lane mask.
+  uint32_t pl_ = (uint32_t)(nd.start + bl);                 // next left slot
+  uint32_t pr_ = (uint32_t)(nd.start + nd.count - 1 - br);  // next right slot (descending)
 #pragma unroll
   for (int k = 0; k < kPartSteps; ++k) {
-    const bool valid = (vbits >> k) & 1u, left = (lbits >> k) & 1u;
-    const uint64_t lm = __ballot(valid && left), rm = __ballot(valid && !left);
-    if (valid && d.ablate != 13) {
-      if (left) nxt[nd.start + bl + mask_rank(lm)] = r[k];
-      else nxt[rend - (br + mask_rank(rm))] = r[k];
-    }
-    bl += __popcll(lm);
-    br += __popcll(rm);
+    const bool valid = r[k] >= 0;
+    const uint32_t left = (lbits >> k) & 1u;
+    const uint64_t lm = __ballot(left != 0u), vm = __ballot(valid);
+    const uint32_t rk_l = mask_rank(lm);
+    // valid lanes are a prefix: a right row's rank among the right rows is lane - rk_l
+    const uint32_t dst = rk_l + (left ? pl_ : pr_ - (uint32_t)lane);
+    if (valid) nxt[dst] = r[k];
+    const uint32_t cl = (uint32_t)__popcll(lm);
+    pl_ += cl;
+    pr_ -= (uint32_t)__popcll(vm) - cl;
   }
 }
 
