@@ -2358,7 +2358,7 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   // different LDS lane groups of a wave64 access, so the atomics stay conflict-free while the flush
   // sums half as many copies (10M: 253.4 -> 250.3 ms per fit, 1M: 87.1 -> 85.7; 16 copies measured
   // the same within noise). COBALT_MAX_COPY_SHIFT overrides the log2 (0..6).
-  static const int max_sh = getenv("COBALT_MAX_COPY_SHIFT") ? std::min(6, std::max(0, atoi(getenv("COBALT_MAX_COPY_SHIFT")))) : 5;
+  const int max_sh = getenv("COBALT_MAX_COPY_SHIFT") ? std::min(6, std::max(0, atoi(getenv("COBALT_MAX_COPY_SHIFT")))) : 5;
   int max_ent = 0;
   for (int t = 0; t < ntiles; ++t) {
     int off = 0;

@@ -65,6 +65,22 @@ def test_gpu_trees_identical_to_host_oracle(kw):
         assert np.array_equal(tg.sum_hessian, tc.sum_hessian)
 
 
+@pytest.mark.parametrize("env", [{"COBALT_HIST_PAIR": "0"}, {"COBALT_MAX_COPY_SHIFT": "6"},
+                                 {"COBALT_MAX_COPY_SHIFT": "0", "COBALT_HIST_PAIR": "0"}])
+def test_gpu_histogram_variants_identical_to_host_oracle(env, monkeypatch):
+    """The histogram variants behind switches (one lane per row instead of the default lane-pair record
+    gathers; 64 or 1 per-lane copies of a low-cardinality feature instead of 32) grow the oracle's
+    trees (the switches are read when a trainer context is created)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    X, y = _data(60_000, seed=4)
+    p = gbdt.GBDTParams(n_estimators=4, max_depth=6, learning_rate=0.3, gamma=0.5, scale_pos_weight=6.7,
+                        random_state=11)
+    bg = gbdt.train(X, y, p, device="cuda")
+    bc = gbdt.train(X, y, p, device="cpu")
+    assert bg.save_raw("ubj") == bc.save_raw("ubj")
+
+
 @pytest.mark.timeout(600)
 def test_gpu_large_n_kernel_shapes_identical_to_host_oracle():
     """Above 4M rows the trainer switches kernel shapes (k_partition<4>, 8192-row root items,
