@@ -2470,7 +2470,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
                 c->lds_hist, stream, d, pl & 1, (int64_t)(1 << pl) * d.slot_elems, pl, kPartHistRows, t);
       } else {
         const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
-        ub = ceil_div(d.n, chh) + (1 << level);
+        // with the row-count rule every pair builds its smaller child (<= half the parent's rows), so the
+        // level's items number at most ceil(n / 2 / chunk) + one partial item per pair: half the grid
+        // (and half the reduce grid) of the all-rows bound, fewer blocks that only plan and exit. The
+        // hessian rule (data parallel) may build the larger child: all-rows bound.
+        ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
+                                       : ceil_div(d.n, chh) + (1 << level);
         if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
           GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t,
                   level, chh);
