@@ -1529,6 +1529,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     }
     const int64_t mg = G - cg, mh = H - ch;  // missing-value statistics
     const bool has_missing = (mg != 0) || (mh != 0);
+    const double GD = (double)G, HD = (double)H, MGd = (double)mg, MHd = (double)mh;  // exact (< 2^53)
     // Candidates, one chunk per iteration of a rolled loop: the chunk's values are rotated down the
     // register arrays (constant indices), so only one chunk's fp64 temporaries are live at a time
     // (the unrolled form spilled at the 128-VGPR limit of a 1024-thread block).
@@ -1545,10 +1546,14 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       const int b = c * kWave + lane;
       if (b < nb) {
         // direction 0: missing -> right, left = bins <= b
+        // the int64 sums are < 2^53 in magnitude, so integer differences taken in fp64 are exact: the
+        // right side is GD - GLd instead of converting G - GL (bit-identical, two int64 -> fp64
+        // conversions fewer per direction)
+        const double GLd = (double)rig[0], HLd = (double)rih[0];
         {
           const int64_t GL = rig[0], HL = rih[0];
-          const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
-          const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
+          const double gl = GLd * d.ginv, hl = HLd * d.hinv;
+          const double gr = (GD - GLd) * d.ginv, hr = (HD - HLd) * d.hinv;
           if (hl >= d.mcw && hr >= d.mcw) {
             Cand cd;
             cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
@@ -1561,8 +1566,9 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
         // direction 1: missing -> left, left = bins <= b-1 (+ missing)
         if (has_missing) {
           const int64_t GL = rig[0] - rg[0] + mg, HL = rih[0] - rh[0] + mh;
-          const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
-          const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
+          const double GL1 = (GLd - (double)rg[0]) + MGd, HL1 = (HLd - (double)rh[0]) + MHd;  // exact
+          const double gl = GL1 * d.ginv, hl = HL1 * d.hinv;
+          const double gr = (GD - GL1) * d.ginv, hr = (HD - HL1) * d.hinv;
           if (hl >= d.mcw && hr >= d.mcw) {
             Cand cd;
             cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
