@@ -2245,6 +2245,18 @@ static GradHistKernel grad_hist_kernel(int ft4) {
   }
 }
 
+// Compute units of the current device (256 on MI355X), cached per process.
+static int device_cu_count() {
+  static int n = 0;
+  if (n <= 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      n = v;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
 static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
   CK(hipMalloc(p, bytes < 16 ? 16 : bytes));
   c->allocs.push_back(*p);
@@ -2443,8 +2455,17 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   static const int env_root = getenv("COBALT_ROOT_CHUNK") ? atoi(getenv("COBALT_ROOT_CHUNK")) : 0;
   // (never more root items than the work-item buffers hold)
   const int root_min = (int)((ceil_div(d.n, (int64_t)c->items_cap - 8) + 63) / 64 * 64);
+  // Fused root pass: whole rounds of resident blocks (2 per CU at 95 VGPRs x 512 threads) of ~8k rows;
+  // a partial last round idles CUs (10M rows: 8192-row items = 2.4 rounds, 9792-row items = 2 rounds:
+  // 167.5 -> 158.3 us per tree in the stamps)
+  int root_rule = std::min(chunk_hist(d, 0), 8192);
+  if (fuse_root) {
+    const int64_t res = 2LL * device_cu_count();
+    const int64_t rounds = std::max<int64_t>(1, (d.n + res * 4096) / (res * 8192));  // nearest to n / (res * 8192)
+    root_rule = (int)std::min<int64_t>(16384, std::max<int64_t>(1024, (ceil_div(d.n, rounds * res) + 63) / 64 * 64));
+  }
   const int root_chunk = std::max(root_min, env_root > 0 ? std::min(16384, std::max(1024, env_root / 64 * 64))
-                                                         : std::min(chunk_hist(d, 0), 8192));
+                                                         : root_rule);
   // Per tree: grad (+ root histogram, node-table init, archive/apply of the previous tree), then per
   // level: [fused: partition of the previous level + this level's histogram | unfused: hist] ->
   // reduce -> [RCCL histogram all-reduce] -> eval [-> unfused: partition]; the last split level's
