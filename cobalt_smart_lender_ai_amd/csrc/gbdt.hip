@@ -684,9 +684,10 @@ struct HistLanes {
   uint32_t lb8[24];
 };
 
-// Per-tile feature state for the LDS histogram lanes. Lane k loads feature f0 + k's colsample bit and
-// copy shift (one round trip, instead of 2 x ft dependent scalar loads per thread -- ~10 us per block
-// for a 32-feature tile), and ballots spread them to every lane. Called by every thread of a block.
+// Per-tile feature state for the LDS histogram lanes. Lane k loads feature f0 + k's colsample bit, copy
+// shift and bin count (one round trip, instead of 2 x ft dependent scalar loads per thread -- ~10 us per
+// block for a 32-feature tile); one wave stages them in LDS (hist_meta_store) and every lane reads them
+// back as uniform values (hist_lanes_finish). Called by every thread of a block.
 // The loads are split from the ballots (hist_lanes_load / hist_lanes_finish) so a kernel can issue
 // them together with its other independent loads (work plan, flush offsets): one round trip for all.
 struct HistLaneRaw {
@@ -2504,8 +2505,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
                                        : ceil_div(d.n, chh) + (1 << level);
         if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-          GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist, stream, d, parity, t,
-                  level, chh);
+          GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
+                  stream, d, parity, t, level, chh);
       }
       GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
               dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap));
