@@ -1313,6 +1313,17 @@ __device__ __forceinline__ double calc_gain(double g, double h, double lambda_, 
   return (t * t) / (h + lambda_);
 }
 
+// Both children's gains of a candidate split with ONE fp64 division: (tl^2 (hr + lambda) + tr^2 (hl +
+// lambda)) / ((hl + lambda)(hr + lambda)). Candidates are only scored when both children reach
+// min_child_weight. Same operation order as the host oracle (models/gbdt_host.py, _calc_gain_pair).
+__device__ __forceinline__ double calc_gain_pair(double gl, double hl, double gr, double hr, double lambda_,
+                                                 double alpha) {
+  const double tl = alpha == 0.0 ? gl : thresh_l1(gl, alpha);
+  const double tr = alpha == 0.0 ? gr : thresh_l1(gr, alpha);
+  const double dl = hl + lambda_, dr = hr + lambda_;
+  return (tl * tl * dr + tr * tr * dl) / (dl * dr);
+}
+
 __device__ __forceinline__ double calc_weight(double g, double h, double lambda_, double alpha, double mcw) {
   if (h < mcw || h <= 0.0) return 0.0;
   const double t = alpha == 0.0 ? g : thresh_l1(g, alpha);
@@ -1557,7 +1568,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
           const double gr = (GD - GLd) * d.ginv, hr = (HD - HLd) * d.hinv;
           if (hl >= d.mcw && hr >= d.mcw) {
             Cand cd;
-            cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+            cd.gain = calc_gain_pair(gl, hl, gr, hr, d.lambda_, d.alpha) - parent_gain;
             cd.key = f * 1024 + b;
             cd.gl = GL;
             cd.hl = HL;
@@ -1572,7 +1583,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
           const double gr = (GD - GL1) * d.ginv, hr = (HD - HL1) * d.hinv;
           if (hl >= d.mcw && hr >= d.mcw) {
             Cand cd;
-            cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+            cd.gain = calc_gain_pair(gl, hl, gr, hr, d.lambda_, d.alpha) - parent_gain;
             cd.key = f * 1024 + 512 + (nb - 1 - b);
             cd.gl = GL;
             cd.hl = HL;
@@ -1795,7 +1806,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
         const double gr = (double)(G - GLi) * d.ginv, hr = (double)(H - HLi) * d.hinv;
         if (hl >= d.mcw && hr >= d.mcw) {
           Cand cd;
-          cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+          cd.gain = calc_gain_pair(gl, hl, gr, hr, d.lambda_, d.alpha) - parent_gain;
           cd.key = f * 1024 + b;
           cd.gl = GLi;
           cd.hl = HLi;
@@ -1809,7 +1820,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
         const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
         if (hl >= d.mcw && hr >= d.mcw) {
           Cand cd;
-          cd.gain = calc_gain(gl, hl, d.lambda_, d.alpha, d.mcw) + calc_gain(gr, hr, d.lambda_, d.alpha, d.mcw) - parent_gain;
+          cd.gain = calc_gain_pair(gl, hl, gr, hr, d.lambda_, d.alpha) - parent_gain;
           cd.key = f * 1024 + 512 + (nb - 1 - b);
           cd.gl = GL;
           cd.hl = HL;

@@ -101,6 +101,17 @@ def _calc_gain(g, h, lam, alpha, mcw):
     return np.where(h < mcw, 0.0, (t * t) / (h + lam))
 
 
+def _calc_gain_pair(gl, hl, gr, hr, lam, alpha):
+    """Both children's gains with one division, in the device's operation order (csrc/gbdt.hip,
+    calc_gain_pair); only used where both children reach min_child_weight."""
+    tl = gl if alpha == 0.0 else _thresh_l1(gl, alpha)
+    tr = gr if alpha == 0.0 else _thresh_l1(gr, alpha)
+    dl = hl + lam
+    dr = hr + lam
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return (tl * tl * dr + tr * tr * dl) / (dl * dr)
+
+
 def _calc_weight(g: float, h: float, lam: float, alpha: float, mcw: float) -> float:
     if h < mcw or h <= 0.0:
         return 0.0
@@ -181,8 +192,7 @@ def _eval_node(hist, G, H, nbins, fmask, p: HostGbdtParams):
             ok = (hl >= p.min_child_weight) & (hr >= p.min_child_weight)
             if not ok.any():
                 continue
-            gain = (_calc_gain(gl, hl, p.reg_lambda, p.reg_alpha, p.min_child_weight)
-                    + _calc_gain(gr, hr, p.reg_lambda, p.reg_alpha, p.min_child_weight)) - pg
+            gain = _calc_gain_pair(gl, hl, gr, hr, p.reg_lambda, p.reg_alpha) - pg
             gain = np.where(ok, gain, -np.inf)
             mx = gain.max()
             if mx == -np.inf:
