@@ -178,3 +178,18 @@ def test_predictor_tile_packing(reference_booster):
     assert len(nodes) == tree_ptr[-1]
     small = predict_ops.pack_forest(reference_booster, tile_nodes=int(np.diff(tree_ptr).max()))[2]
     assert len(small) >= len(tiles)
+
+
+@pytest.mark.parametrize("alpha", [0.0, 0.5])
+def test_pair_gain_equals_sum_of_child_gains(alpha):
+    """The one-division split gain (device calc_gain_pair / host _calc_gain_pair) is XGBoost's
+    CalcGain(left) + CalcGain(right) up to fp64 rounding."""
+    from cobalt_smart_lender_ai_amd.models import gbdt_host as H
+
+    rng = np.random.default_rng(5)
+    gl, gr = rng.normal(0, 50, 1000), rng.normal(0, 50, 1000)
+    hl, hr = rng.uniform(1, 400, 1000), rng.uniform(1, 400, 1000)
+    lam = 1.0
+    pair = H._calc_gain_pair(gl, hl, gr, hr, lam, alpha)
+    ref = H._calc_gain(gl, hl, lam, alpha, 1.0) + H._calc_gain(gr, hr, lam, alpha, 1.0)
+    assert np.allclose(pair, ref, rtol=1e-12, atol=1e-12)
