@@ -132,6 +132,7 @@ def main() -> None:
                 "max_depth": a.depth,
             },
             "rows_global": n_global,
+            "dp_transport": ctx.transport if world > 1 else None,
             "auc": None if auc is None else round(auc, 5),
             "test_rows": a.test_rows,
             "fit_breakdown_ms": {

@@ -65,6 +65,11 @@ _SIGS: dict[str, tuple] = {
     "cobalt_comm_async_error": (c_int, [c_void_p]),
     "cobalt_comm_allreduce": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
     "cobalt_comm_allgather": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    # ipccomm.hip
+    "cobalt_ipc_handle_bytes": (c_int, []),
+    "cobalt_ipc_create": (c_int, [c_int, c_int, c_int64, c_double, ctypes.POINTER(c_void_p), c_void_p]),
+    "cobalt_ipc_connect": (c_int, [c_void_p, c_void_p]),
+    "cobalt_ipc_epoch": (ctypes.c_uint, [c_void_p]),
     # loopcomm.hip
     "cobalt_comm_loop_group": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "cobalt_comm_loop_rank": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),

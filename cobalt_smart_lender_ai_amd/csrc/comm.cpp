@@ -1,4 +1,6 @@
-// Native RCCL communicator for the GBDT hot path (per-level histogram all-reduce).
+// Native RCCL communicator for the GBDT hot path (per-level histogram all-reduce), and the dispatch
+// of the cobalt_comm_* entry points over the three communicator kinds (RCCL, in-process loopback,
+// IPC one-shot group -- see comm.h).
 //
 // torch.distributed (backend "nccl" == RCCL on ROCm) bootstraps the process group and ships the
 // 128-byte unique id; this file owns a dedicated communicator so the int64 histogram all-reduce
@@ -66,6 +68,7 @@ void comm_set_error(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg)
 
 static inline void* nccl_of(void* h) { return static_cast<CobaltComm*>(h)->nccl; }
 static inline bool is_loop(void* h) { return static_cast<CobaltComm*>(h)->kind == 1; }
+static inline bool is_ipc(void* h) { return static_cast<CobaltComm*>(h)->kind == 2; }
 
 COBALT_API int cobalt_comm_load(const char* path) {
   if (g_api.lib) return 0;
@@ -112,6 +115,8 @@ COBALT_API int cobalt_comm_destroy(void* comm, int abort) {
   Result r = 0;
   if (h->kind == 1) {
     loop_release(h);
+  } else if (h->kind == 2) {
+    ipc_release(h);
   } else if (g_api.lib) {
     r = abort ? g_api.comm_abort(static_cast<Comm>(h->nccl)) : g_api.comm_destroy(static_cast<Comm>(h->nccl));
   }
@@ -122,6 +127,7 @@ COBALT_API int cobalt_comm_destroy(void* comm, int abort) {
 // Asynchronous communicator error (a peer died, a network/transport failure): 0 = healthy. Polled by
 // the host-side collective watchdog (parallel/dist.py) while it waits on the trainer's stream.
 COBALT_API int cobalt_comm_async_error(void* comm) {
+  if (comm && is_ipc(comm)) return ipc_error(static_cast<CobaltComm*>(comm));
   if (!comm || is_loop(comm) || !g_api.async_error) return 0;
   Result st = 0;
   Result r = g_api.async_error(static_cast<Comm>(nccl_of(comm)), &st);
@@ -135,6 +141,7 @@ COBALT_API int cobalt_comm_async_error(void* comm) {
 
 COBALT_API int cobalt_comm_allreduce_sum_i64(void* comm, int64_t* buf, int64_t count, hipStream_t stream) {
   if (is_loop(comm)) return loop_allreduce(static_cast<CobaltComm*>(comm), buf, count, 0, kSum, stream);
+  if (is_ipc(comm)) return ipc_allreduce(static_cast<CobaltComm*>(comm), buf, count, 0, kSum, stream);
   Result r = g_api.all_reduce(buf, buf, (size_t)count, kInt64, kSum, static_cast<Comm>(nccl_of(comm)), stream);
   if (r) snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", g_api.error_string(r));
   return r;
@@ -145,6 +152,7 @@ COBALT_API int cobalt_comm_allreduce(void* comm, void* buf, int64_t count, int d
   const int dt = dtype_code(dtype);
   if (dt < 0 || (op != kSum && op != kMax && op != kMin)) return -3;
   if (is_loop(comm)) return loop_allreduce(static_cast<CobaltComm*>(comm), buf, count, dtype, op, stream);
+  if (is_ipc(comm)) return ipc_allreduce(static_cast<CobaltComm*>(comm), buf, count, dtype, op, stream);
   Result r = g_api.all_reduce(buf, buf, (size_t)count, dt, op, static_cast<Comm>(nccl_of(comm)), stream);
   if (r) snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", g_api.error_string(r));
   return r;
@@ -155,6 +163,7 @@ COBALT_API int cobalt_comm_allgather(void* comm, const void* send, void* recv, i
   const int dt = dtype_code(dtype);
   if (dt < 0) return -3;
   if (is_loop(comm)) return loop_allgather(static_cast<CobaltComm*>(comm), send, recv, count, dtype, stream);
+  if (is_ipc(comm)) { comm_set_error("ipc: all-gather is not provided by the IPC group"); return -3; }
   Result r = g_api.all_gather(send, recv, (size_t)count, dt, static_cast<Comm>(nccl_of(comm)), stream);
   if (r) snprintf(g_err, sizeof(g_err), "ncclAllGather: %s", g_api.error_string(r));
   return r;

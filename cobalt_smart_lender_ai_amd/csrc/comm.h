@@ -1,15 +1,18 @@
-// Communicator handle shared by comm.cpp (RCCL) and loopcomm.hip (in-process loopback group).
+// Communicator handle shared by comm.cpp (RCCL), loopcomm.hip (in-process loopback group) and
+// ipccomm.hip (one-shot all-reduce over IPC-mapped peer buffers).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 struct LoopGroup;
+struct IpcGroup;
 
 struct CobaltComm {
-  int kind;          // 0 = RCCL communicator, 1 = loopback rank of an in-process group
+  int kind;          // 0 = RCCL communicator, 1 = loopback rank of an in-process group, 2 = IPC group
   void* nccl;        // ncclComm_t (kind 0)
   LoopGroup* group;  // (kind 1)
   int rank, nranks;
+  IpcGroup* ipc;     // (kind 2)
 };
 
 // dtype: 0 int64, 1 uint8, 2 int32, 3 f32, 4 f64; op: 0 sum, 2 max, 3 min
@@ -17,3 +20,17 @@ int loop_allreduce(CobaltComm* c, void* buf, int64_t count, int dtype, int op, h
 int loop_allgather(CobaltComm* c, const void* send, void* recv, int64_t count, int dtype, hipStream_t stream);
 void loop_release(CobaltComm* c);
 void comm_set_error(const char* msg);
+
+// IPC group (ipccomm.hip)
+int ipc_allreduce(CobaltComm* c, void* buf, int64_t count, int dtype, int op, hipStream_t stream);
+int ipc_error(CobaltComm* c);
+void ipc_release(CobaltComm* c);
+// The buffer the next exchange sends (this rank's IPC-exported slot of parity epoch + 1).
+void* ipc_send_buffer(CobaltComm* c);
+int64_t ipc_capacity(CobaltComm* c);
+// Zero the first `bytes` of the next send buffer (stream-ordered; safe once this rank's previous
+// exchange has run: every peer finished reading that slot before it published its own flag).
+int ipc_zero_send(CobaltComm* c, int64_t bytes, hipStream_t stream);
+// One exchange: publish the send buffer, wait for every peer's, out = sum over ranks (rank order),
+// then zero the first `zero_bytes` of the following send buffer.
+int ipc_exchange(CobaltComm* c, void* out, int64_t count, int dtype, int op, int64_t zero_bytes, hipStream_t stream);

@@ -23,6 +23,7 @@
 //  * Data parallel: the only cross-rank traffic is one int64 SUM all-reduce of the built
 //    histogram slots per level, issued on the same stream through a native RCCL communicator.
 #include "common.h"
+#include "comm.h"
 #include <math.h>
 #include <string.h>
 #include <stdlib.h>
@@ -156,6 +157,8 @@ struct GbdtDev {
   int2* layout;           // [F] histogram LDS layout: x = cell offset within tile, y = log2(copies)
   int32_t* tile_entries;  // [n_tiles] LDS cells per feature tile
   int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
+  int64_t* hist_red;      // k_hist_reduce destination: nullptr = hist_b[parity]; the IPC group's send slot
+                          // under IPC data parallelism (the exchange then writes the global sums to hist_b)
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
@@ -1237,13 +1240,14 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
     if (k >= cnt) { g[k] = 0; h[k] = 0; slot[k] = -2; }
   // items of one slot are consecutive: flush one atomic pair per (run, slot)
   stamp_.probe(2);
+  int64_t* const red = d.hist_red ? d.hist_red : d.hist_b[parity];
   int cur = slot[0];
   int64_t sg = 0, sh = 0;
 #pragma unroll
   for (int k = 0; k < kRedItems; ++k) {
     if (slot[k] != cur) {
       if (cur >= 0 && (sg | sh)) {
-        int64_t* dst = d.hist_b[parity] + (int64_t)cur * d.slot_elems + (int64_t)cell * 2;
+        int64_t* dst = red + (int64_t)cur * d.slot_elems + (int64_t)cell * 2;
         atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)sg);
         atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)sh);
       }
@@ -1254,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
     sh += h[k];
   }
   if (cur >= 0 && (sg | sh)) {
-    int64_t* dst = d.hist_b[parity] + (int64_t)cur * d.slot_elems + (int64_t)cell * 2;
+    int64_t* dst = red + (int64_t)cur * d.slot_elems + (int64_t)cell * 2;
     atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)sg);
     atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)sh);
   }
@@ -2442,6 +2446,18 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // any native communicator turns on the data-parallel protocol (a 1-rank one exercises it on 1 GPU)
   const bool dp = c->cfg.comm != nullptr;
   d.dp = dp ? 1 : 0;
+  // IPC one-shot group (ipccomm.hip): the reduce accumulates into this rank's exported send slot and
+  // one exchange kernel per level writes the all-reduced histograms into hist_b (no RCCL call)
+  CobaltComm* const cc = static_cast<CobaltComm*>(c->cfg.comm);
+  const bool ipc = dp && cc->kind == 2;
+  d.hist_red = nullptr;
+  if (ipc) {
+    if (ipc_capacity(cc) < (int64_t)c->pairs_max * d.slot_elems * (int64_t)sizeof(int64_t)) {
+      comm_set_error("ipc: slot capacity below one level of histograms (raise COBALT_IPC_SLOT_MB)");
+      return -14;
+    }
+    if (int rc = ipc_zero_send(cc, d.slot_elems * (int64_t)sizeof(int64_t), stream)) return rc;
+  }
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const int ft4 = hist_ft4(d);
   const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && d.ablate == 0 &&
@@ -2519,6 +2535,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
                   stream, d, parity, t, level, chh);
       }
+      d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
               dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap));
       CK_LAUNCH();
@@ -2531,7 +2548,14 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
                   level, parity);
           CK_LAUNCH();
         }
-        int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
+        int rc;
+        if (ipc) {  // the exchange also zeroes the next level's send slot (next tree's root after the last)
+          const int64_t next_slots = level + 1 < D ? (1 << level) : 1;
+          rc = ipc_exchange(cc, d.hist_b[parity], (int64_t)slots * d.slot_elems, 0, 0,
+                            next_slots * d.slot_elems * (int64_t)sizeof(int64_t), stream);
+        } else {
+          rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
+        }
         if (rc) return rc;
       }
       if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
@@ -2547,7 +2571,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
-        const int64_t zero_next = (int64_t)(1 << level) * d.slot_elems;
+        // (under IPC the exchange overwrites the next level's hist_b slots whole: nothing to zero)
+        const int64_t zero_next = ipc ? 0 : (int64_t)(1 << level) * d.slot_elems;
         const int pw = part_wide(d) ? 16 : 4;
         const int steps = ceil_div(chp, pw * kWave);  // <= kPartSteps (chunk_part's cap)
         if (pw == 16 && steps <= 4)

@@ -53,7 +53,9 @@ class GBDTParams:
     scale_pos_weight: float = 1.0
     random_state: int = 0
     base_score: float | None = None
-    sketch_rows: int = 1 << 18
+    # rows of the strided global sample the quantile sketch uses; None / 0 = every row (exact weighted
+    # quantiles on one rank; per-rank device summaries merged under data parallelism)
+    sketch_rows: int | None = 1 << 18
     # quantile-sketch weights: "sample" = the sample weights (XGBoost hist semantics, the reference's
     # tree_method), "hessian" = first-round hessians (sample weight x scale_pos_weight for positives,
     # XGBoost approx semantics); sketch_mode "summary" merges per-rank QuantileSummary objects
@@ -159,11 +161,24 @@ def _allreduce_max_flags(flags: torch.Tensor, dist, dev) -> torch.Tensor:
 
 
 def _summary_cuts(samp: torch.Tensor, wsamp: torch.Tensor | None, max_bin: int, has_missing: torch.Tensor,
-                  dist, dev) -> tuple[torch.Tensor, torch.Tensor]:
+                  dist, dev, on_device: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
     """sketch_mode="summary": every rank summarises its own sample, the summaries are all-gathered
-    (a few KB per feature instead of the raw rows) and merged identically on every rank."""
-    summ = sketch.QuantileSummary.build(samp.cpu().numpy(), None if wsamp is None else wsamp.cpu().numpy())
-    off, vals, wts, _ = summ.to_arrays()
+    (a few KB per feature instead of the raw rows) and merged identically on every rank. Integer
+    weights are scaled by the GLOBAL max weight, so one unit means the same weight on every rank.
+    ``on_device``: the summary is built where the sample lives (:func:`sketch.device_summary`; the
+    full-data sketch), else by the host :class:`sketch.QuantileSummary`."""
+    w_max = None
+    if wsamp is not None:
+        w_max = float(wsamp.max()) if wsamp.numel() else 0.0
+        if dist is not None and dist.world > 1:
+            w_max = dist.allreduce_scalar(w_max, "max", dev)
+        w_max = w_max if w_max > 0 else 1.0
+    if on_device:
+        off, vals, wts = sketch.device_summary(samp, wsamp, w_max=w_max)
+    else:
+        summ = sketch.QuantileSummary.build(samp.cpu().numpy(), None if wsamp is None else wsamp.cpu().numpy(),
+                                            w_max=w_max)
+        off, vals, wts, _ = summ.to_arrays()
     if dist is not None and dist.world > 1:
         per = int(dist.allreduce_scalar(float(len(vals)), "max", dev))  # common padded length
         ent = torch.full((per, 2), float("nan"), dtype=torch.float64)
@@ -180,16 +195,21 @@ def _summary_cuts(samp: torch.Tensor, wsamp: torch.Tensor | None, max_bin: int, 
             parts.append(sketch.QuantileSummary.from_arrays(o, e[:, 0].astype(np.float32), e[:, 1].astype(np.int64),
                                                             np.zeros(F1 - 1, dtype=bool)))
         summ = sketch.QuantileSummary.merge(parts)
+    else:
+        summ = sketch.QuantileSummary.from_arrays(off, vals, wts, np.zeros(len(off) - 1, dtype=bool))
     summ.has_missing = has_missing.cpu().numpy().astype(bool)
     c, nb = summ.cuts(max_bin)
     return torch.from_numpy(c).to(dev), torch.from_numpy(nb).to(dev)
 
 
-def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int = 1 << 18, device=None, dist=None,
+def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = 1 << 18, device=None, dist=None,
                 n_rows_global: int | None = None, row_offset: int = 0, sketch_weights=None,
                 sketch_mode: str = "sample") -> BinnedData:
     """Weighted quantile sketch (K12) on a global strided sample + binning (K13).
 
+    ``sketch_rows`` None / 0: every row (XGBoost ``hist`` sketches all rows): exact weighted quantiles
+    on one rank; under data parallelism every rank summarises its whole shard on its device and the
+    summaries are merged (all-gathering 10M raw rows would move the matrix itself).
     ``sketch_weights`` ([N_local], optional): per-row sketch weights (see models/sketch.py).
     A feature gets 256 bins only if it has no missing value in the FULL data (all ranks)."""
     dev = _resolve_device(device, X)
@@ -202,13 +222,14 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int = 1 << 18, device=Non
     has_missing = torch.isnan(Xt).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
     if world > 1:
         has_missing = _allreduce_max_flags(has_missing, dist, dev)
-    stride = sketch.sample_stride(n_glob, sketch_rows)
+    full = not sketch_rows
+    stride = 1 if full else sketch.sample_stride(n_glob, sketch_rows)
     samp = sketch.local_sample(Xt, row_offset, stride)
     wsamp = None
     if sketch_weights is not None:
         wsamp = sketch.local_sample(_to_tensor(sketch_weights, dev).reshape(-1, 1), row_offset, stride)[:, 0]
-    if sketch_mode == "summary":
-        cuts, nbins = _summary_cuts(samp, wsamp, max_bin, has_missing, dist, dev)
+    if sketch_mode == "summary" or (full and world > 1):
+        cuts, nbins = _summary_cuts(samp, wsamp, max_bin, has_missing, dist, dev, on_device=full)
     else:
         if world > 1:
             samp = dist.allgather_rows(samp)

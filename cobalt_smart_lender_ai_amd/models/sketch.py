@@ -206,11 +206,19 @@ class QuantileSummary:
         return v[last], gw.astype(np.int64)
 
     @classmethod
-    def build(cls, X: np.ndarray, w: np.ndarray | None = None, size: int = 2048) -> "QuantileSummary":
+    def build(cls, X: np.ndarray, w: np.ndarray | None = None, size: int = 2048,
+              w_max: float | None = None) -> "QuantileSummary":
+        """Summary of the rows ``X`` [n, F]. ``w_max``: the weight that maps to ``2^20`` integer units.
+        Summaries that are merged must share it (the GLOBAL max weight under data parallelism --
+        one unit must mean the same weight on every rank); default: the local max."""
         X = np.asarray(X, dtype=np.float32)
         n, F = X.shape
-        wq = np.ones(n, dtype=np.int64) if w is None else np.round(
-            np.asarray(w, np.float64) * (WEIGHT_SCALE / max(float(np.max(w)), 1e-300))).astype(np.int64)
+        if w is None:
+            wq = np.ones(n, dtype=np.int64)
+        else:
+            wd = np.asarray(w, np.float64).reshape(-1)
+            scale = w_max if w_max is not None else (float(wd.max()) if wd.size else 1.0)
+            wq = np.round(wd * (WEIGHT_SCALE / max(float(scale), 1e-300))).astype(np.int64)
         vals, wts, miss = [], [], np.zeros(F, dtype=bool)
         for f in range(F):
             x = X[:, f]
@@ -271,6 +279,55 @@ class QuantileSummary:
     def from_arrays(cls, off, vals, wts, miss) -> "QuantileSummary":
         return cls([vals[off[f]:off[f + 1]] for f in range(len(off) - 1)],
                    [wts[off[f]:off[f + 1]] for f in range(len(off) - 1)], miss)
+
+
+def device_summary(X: torch.Tensor, w: torch.Tensor | None = None, size: int = 8192,
+                   w_max: float | None = None) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """:class:`QuantileSummary` arrays (offsets, values, int64 weights) of EVERY row of ``X`` [n, F],
+    computed on ``X``'s device: one batched sort per feature column (rocPRIM via ``torch.sort``), the
+    distinct values' integer weights by a segmented sum, and the same cumulative-weight prune as
+    :meth:`QuantileSummary._prune` -- so only ``<= size`` entries per feature leave the device. The
+    full-data sketch of a data-parallel fit merges these per-rank summaries (``w_max`` = the global
+    max weight, see :meth:`QuantileSummary.build`)."""
+    n, F = X.shape
+    dev = X.device
+    if w is None:
+        wq = torch.ones(n, dtype=torch.int64, device=dev)
+    else:
+        wd = w.to(device=dev, dtype=torch.float64).reshape(-1)
+        scale = w_max if w_max is not None else (float(wd.max()) if wd.numel() else 1.0)
+        wq = torch.round(wd * (WEIGHT_SCALE / max(float(scale), 1e-300))).to(torch.int64)
+    offs, vals, wts = [0], [], []
+    for f in range(F):
+        x = X[:, f].to(torch.float32)
+        ok = ~torch.isnan(x)
+        xv = x[ok]
+        if xv.numel() == 0:
+            offs.append(offs[-1])
+            continue
+        xs, order = torch.sort(xv)
+        ws = wq[ok][order]
+        new = torch.ones_like(xs, dtype=torch.bool)
+        new[1:] = xs[1:] != xs[:-1]
+        gid = torch.cumsum(new.to(torch.int64), 0) - 1
+        u = xs[new]
+        uw = torch.zeros(u.numel(), dtype=torch.int64, device=dev).scatter_add_(0, gid, ws)
+        if u.numel() > size:  # prune by cumulative weight (QuantileSummary._prune, on the device)
+            cum = torch.cumsum(uw, 0)
+            W = int(cum[-1])
+            grp = torch.clamp((cum * size - 1) // max(W, 1), max=size - 1) if W > 0 else torch.zeros_like(cum)
+            last = torch.ones_like(grp, dtype=torch.bool)
+            last[:-1] = grp[1:] != grp[:-1]
+            cl = cum[last]
+            gw = torch.diff(cl, prepend=torch.zeros(1, dtype=torch.int64, device=dev))
+            u, uw = u[last], gw
+        vals.append(u.cpu().numpy())
+        wts.append(uw.cpu().numpy())
+        offs.append(offs[-1] + int(u.numel()))
+    off = np.asarray(offs, dtype=np.int64)
+    v = np.concatenate(vals).astype(np.float32) if vals else np.zeros(0, np.float32)
+    ww = np.concatenate(wts).astype(np.int64) if wts else np.zeros(0, np.int64)
+    return off, v, ww
 
 
 def bin_matrix_host(X: np.ndarray, cuts: np.ndarray, nbins: np.ndarray) -> np.ndarray:

@@ -2,9 +2,16 @@
 
 Bootstrap and small metadata collectives go through ``torch.distributed`` (backend ``"nccl"`` is RCCL
 on ROCm; ``"gloo"`` for CPU rehearsals). The hot GBDT collective — the per-level int64 histogram
-all-reduce — runs on a dedicated native RCCL communicator (``csrc/comm.cpp``) created here from a
-unique id broadcast over the torch group, so the C++ trainer can enqueue it on its own HIP stream
-in the middle of a tree without returning to Python.
+all-reduce — runs on a dedicated native communicator created here, so the C++ trainer can enqueue it
+on its own HIP stream in the middle of a tree without returning to Python. Two transports:
+
+* ``"ipc"`` (default when every rank is on this node): the one-shot IPC group of
+  ``csrc/ipccomm.hip``. Each rank exports two send slots + a flag word; the handles are all-gathered
+  once over the torch group, and a level's all-reduce is ONE kernel that waits on the peers' epoch
+  flags and sums all ranks' slots straight over xGMI (every link at once, no ring hops, no RCCL
+  launch). It also runs with several processes sharing one GPU, which RCCL refuses.
+* ``"rccl"``: a native RCCL communicator (``csrc/comm.cpp``) from a unique id broadcast over the torch
+  group (multi-node, or ``COBALT_DP_TRANSPORT=rccl`` for A/B comparisons).
 
 The reference has no distributed layer; this module is the MI355X-native
 replacement for its ``n_jobs=-1`` process parallelism (model_tree_train_test.py:155).
@@ -28,6 +35,7 @@ class DistContext:
     local_rank: int = 0
     backend: str = "none"
     native_comm: int | None = None          # cobalt_comm handle (GPU) or None
+    transport: str = "none"                 # "ipc" | "rccl" | "loopback" | "none"
     _owns_group: bool = field(default=False, repr=False)
 
     @property
@@ -82,6 +90,10 @@ class DistContext:
         if self.native_comm:
             from .. import _native
 
+            if self.transport == "ipc" and self.world > 1:
+                # peers map this rank's slots: nobody unmaps / frees before every rank is done
+                torch.cuda.synchronize()
+                self.barrier()
             _native.lib().cobalt_comm_destroy(ctypes.c_void_p(self.native_comm), 0)
             self.native_comm = None
         if self._owns_group and tdist.is_initialized():
@@ -92,8 +104,13 @@ class DistContext:
 _CTX: DistContext | None = None
 
 
-def init_from_env(backend: str | None = None, native: bool | None = None, timeout_s: int = 600) -> DistContext:
-    """Initialise from torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (single process if absent)."""
+def init_from_env(backend: str | None = None, native: bool | None = None, timeout_s: int = 600,
+                  transport: str | None = None) -> DistContext:
+    """Initialise from torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (single process if absent).
+
+    ``native`` creates the trainer's native communicator (default: with the ``nccl`` backend);
+    ``transport`` picks it (``"ipc"`` / ``"rccl"``; default ``COBALT_DP_TRANSPORT`` or ``"auto"`` =
+    IPC when all ranks share this node, else RCCL)."""
     global _CTX
     if _CTX is not None:
         return _CTX
@@ -120,12 +137,104 @@ def init_from_env(backend: str | None = None, native: bool | None = None, timeou
     if native is None:
         native = backend == "nccl"
     if native:
-        ctx.native_comm = create_native_comm(ctx)
+        ctx.native_comm, ctx.transport = create_native_comm(ctx, transport)
     _CTX = ctx
     return ctx
 
 
-def create_native_comm(ctx: DistContext) -> int:
+def _pick_transport(ctx: DistContext, transport: str | None) -> str:
+    t = (transport or os.environ.get("COBALT_DP_TRANSPORT", "auto")).lower()
+    if t not in ("auto", "ipc", "rccl"):
+        raise ValueError(f"COBALT_DP_TRANSPORT must be auto, ipc or rccl, not {t!r}")
+    if t == "auto":
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world)))
+        t = "ipc" if local_world == ctx.world else "rccl"
+    return t
+
+
+def create_native_comm(ctx: DistContext, transport: str | None = None) -> tuple[int, str]:
+    """The trainer's native communicator and its transport name (see the module docstring). An
+    automatically chosen IPC group that fails its self-test falls back to RCCL with a warning."""
+    t = _pick_transport(ctx, transport)
+    if t == "ipc":
+        try:
+            return create_ipc_comm(ctx), "ipc"
+        except Exception as e:  # noqa: BLE001
+            if transport == "ipc" or os.environ.get("COBALT_DP_TRANSPORT", "auto").lower() == "ipc" \
+                    or ctx.backend != "nccl":
+                raise
+            import warnings
+
+            warnings.warn(f"IPC all-reduce group unavailable ({e}); using RCCL")
+    return create_rccl_comm(ctx), "rccl"
+
+
+def ipc_slot_bytes() -> int:
+    """Send-slot capacity of the IPC group (``COBALT_IPC_SLOT_MB``, default 64 MiB: one level of
+    histograms is pairs x (cells + 1) x 16 B, 0.7 MB for the 20-feature depth-7 model)."""
+    return int(float(os.environ.get("COBALT_IPC_SLOT_MB", "64")) * (1 << 20))
+
+
+def ipc_timeout_s() -> float:
+    """How long an exchange waits for a peer before the group is marked failed (``COBALT_IPC_TIMEOUT_S``)."""
+    return float(os.environ.get("COBALT_IPC_TIMEOUT_S", "120"))
+
+
+def create_ipc_comm(ctx: DistContext) -> int:
+    """IPC one-shot group over the ranks of this node: export, all-gather the handles over the torch
+    group, map every peer, then a self-test all-reduce of a known pattern on both send slots."""
+    from .. import _native
+
+    lib = _native.lib()
+    nb = int(lib.cobalt_ipc_handle_bytes())
+    mine = (ctypes.c_uint8 * nb)()
+    h = ctypes.c_void_p()
+    rc = lib.cobalt_ipc_create(ctx.rank, ctx.world, ipc_slot_bytes(), ipc_timeout_s(), ctypes.byref(h), mine)
+    if rc != 0:
+        raise RuntimeError(f"cobalt_ipc_create failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+    try:
+        if ctx.world > 1:
+            dev = ctx._coll_device("cpu")
+            t = torch.tensor(list(bytes(mine)), dtype=torch.uint8, device=dev)
+            outs = [torch.zeros_like(t) for _ in range(ctx.world)]
+            tdist.all_gather(outs, t)
+            blob = b"".join(bytes(o.cpu().tolist()) for o in outs)
+        else:  # a 1-rank group (exercises the protocol on one process)
+            blob = bytes(mine)
+        allh = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
+        rc = lib.cobalt_ipc_connect(h, allh)
+        if rc != 0:
+            raise RuntimeError(f"cobalt_ipc_connect failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+        _ipc_selftest(ctx, int(h.value))
+    except Exception:
+        lib.cobalt_comm_destroy(h, 1)
+        raise
+    return int(h.value)
+
+
+def _ipc_selftest(ctx: DistContext, comm: int) -> None:
+    from .. import _native
+
+    lib = _native.lib()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = 4099
+    idx = torch.arange(n, dtype=torch.int64, device=dev)
+    for rnd in range(2):  # both send slots
+        buf = idx * (ctx.rank + 1) + 1000 * rnd
+        rc = lib.cobalt_comm_allreduce(ctypes.c_void_p(comm), ctypes.c_void_p(buf.data_ptr()), n, 0, 0,
+                                       ctypes.c_void_p(_native.stream_handle()))
+        if rc != 0:
+            raise RuntimeError(f"IPC self-test all-reduce failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+        torch.cuda.synchronize(dev)
+        if lib.cobalt_comm_async_error(ctypes.c_void_p(comm)):
+            raise RuntimeError(f"IPC self-test: {lib.cobalt_comm_last_error().decode()}")
+        w = ctx.world
+        want = idx * (w * (w + 1) // 2) + 1000 * rnd * w
+        if not torch.equal(buf, want):
+            raise RuntimeError("IPC self-test all-reduce returned wrong sums")
+
+
+def create_rccl_comm(ctx: DistContext) -> int:
     """Create the trainer's RCCL communicator; the unique id travels over the torch group."""
     from .. import _native
 

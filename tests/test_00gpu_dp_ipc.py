@@ -1,0 +1,54 @@
+"""Data parallelism across PROCESSES on one GPU (the multi-rank configuration a 1-GPU box can run):
+2 and 3 ranks share cuda:0, bootstrap over gloo and all-reduce their per-level histograms through the
+IPC one-shot group (csrc/ipccomm.hip). The model must equal the 1-process fit byte for byte, and a
+rank that dies mid-fit must make its peer fail fast through the group's deadline + the watchdog's
+abort instead of hanging.
+
+The file sorts before every other GPU test: the ranks (and the 1-rank reference) run in spawned
+processes, and this pytest process never initialises HIP (spawning from an initialised process is
+refused on the pool)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROWS = 300_000
+
+
+def _check_clean(parent_initialised):
+    if parent_initialised:
+        pytest.skip("HIP already initialised in this process; run this file on its own")
+
+
+@pytest.mark.timeout(900)
+def test_ipc_data_parallel_processes_equal_single_process():
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    ref = dp_check.run(1, ROWS)[0]
+    assert ref["ok"], ref
+    for procs in (2, 3):
+        got = dp_check.run(procs, ROWS, timeout_s=400)
+        for g in got:
+            assert g["ok"], g
+            assert g["transport"] == "ipc"
+            # one exchange per level per tree, plus the connect self-test's two
+            assert g["ipc_epochs"] == 2 + 7 * ref["trees"]
+            assert g["model_sha256"] == ref["model_sha256"], (procs, g["rank"])
+
+
+@pytest.mark.timeout(600)
+def test_ipc_dead_peer_fails_fast():
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=12)
+    got = dp_check.run(2, 200_000, params, checkpoint_every=1, timeout_s=300,
+                       env={"COBALT_FAULT_AFTER_TREES": "3", "COBALT_FAULT_RANK": "1",
+                            "COBALT_IPC_TIMEOUT_S": "5"})
+    r0, r1 = got
+    assert r1.get("error") == "InjectedFault", r1
+    assert not r0["ok"]
+    assert r0.get("error") == "CollectiveTimeout", r0
+    assert "deadline" in r0.get("message", "") or "communicator error" in r0.get("message", ""), r0
+    assert r0["elapsed_s"] < 120, r0

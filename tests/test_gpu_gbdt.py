@@ -199,6 +199,30 @@ def test_gpu_data_parallel_protocol_with_one_rank_rccl():
     lib.cobalt_comm_destroy(h, 0)
 
 
+@pytest.mark.parametrize("depth", [3, 7])
+def test_gpu_data_parallel_protocol_with_one_rank_ipc(depth):
+    """The DP path on a 1-rank IPC one-shot group (reduce into the exported send slot, one exchange
+    kernel per level) gives exactly the single-GPU trees; one exchange per level per tree."""
+    import ctypes
+
+    from cobalt_smart_lender_ai_amd import _native
+    from cobalt_smart_lender_ai_amd.parallel.dist import DistContext, create_ipc_comm
+
+    ctx = DistContext(rank=0, world=1, local_rank=0, backend="none")
+    ctx.native_comm, ctx.transport = create_ipc_comm(ctx), "ipc"
+    lib = _native.lib()
+    e0 = lib.cobalt_ipc_epoch(ctypes.c_void_p(ctx.native_comm))
+    X, y = _data(300_000, seed=12)
+    params = dict(n_estimators=5, max_depth=depth, learning_rate=0.1, gamma=1.0, subsample=0.9, random_state=5,
+                  scale_pos_weight=6.0)
+    ref = gbdt.train(X, y, params, device="cuda")
+    dp = gbdt.train(X, y, params, device="cuda", dist=ctx)
+    assert dp.save_raw("ubj") == ref.save_raw("ubj")
+    assert lib.cobalt_ipc_epoch(ctypes.c_void_p(ctx.native_comm)) - e0 == 5 * depth
+    assert lib.cobalt_comm_async_error(ctypes.c_void_p(ctx.native_comm)) == 0
+    lib.cobalt_comm_destroy(ctypes.c_void_p(ctx.native_comm), 0)
+
+
 def _wide(n, F, seed):
     rng = np.random.default_rng(seed)
     X = rng.normal(size=(n, F)).astype(np.float32)

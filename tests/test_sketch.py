@@ -129,3 +129,87 @@ def test_quantile_summary_merge_is_rank_consistent_and_accurate():
         ranks = np.searchsorted(xs, c[f, :k].numpy(), side="left") / len(xs)
         target = np.arange(1, k + 1) / (k + 1)
         assert np.max(np.abs(ranks - target)) < 2.0 / 256
+
+
+def _rank_error_ok(X, w, c, nb, f, tol):
+    """Cuts of feature f sit within ``tol`` (fraction of the total weight) of the weighted quantiles."""
+    ok = ~np.isnan(X[:, f])
+    order = np.argsort(X[ok, f], kind="stable")
+    xs = X[ok, f][order]
+    ws = (np.ones(ok.sum()) if w is None else w[ok][order]).astype(np.float64)
+    cum = np.cumsum(ws) / ws.sum()
+    k = int(nb[f]) - 1
+    ranks = cum[np.searchsorted(xs, c[f, :k].numpy(), side="left") - 1]
+    target = np.arange(1, k + 1) / (k + 1)
+    return np.max(np.abs(ranks - target)) < tol
+
+
+def test_weighted_summary_merge_uses_the_global_weight_scale():
+    """each rank scaled its integer weights by its OWN max weight, so merged summaries mixed
+    units. With ranks whose weights differ by 50x, the merged cuts must still be the weighted
+    quantiles of the union (exact for low-cardinality features), identical on every rank; a rank with
+    an empty shard must not break the merge."""
+    from cobalt_smart_lender_ai_amd.parallel import loopback
+
+    n = 48_000
+    X = _mixed(n, 8)
+    w = np.random.default_rng(9).uniform(0.5, 1.5, n)
+    w[n // 2:] *= 50.0  # ranks 2-3 carry 50x the weight of ranks 0-1 ...
+    X[n // 2:, :2] += np.float32(3.0)  # ... and hold shifted values, so the weighting moves the cuts
+    exact = sketch.compute_cuts(torch.from_numpy(X), 256, weights=torch.from_numpy(w))
+    bounds = [(0, n // 4), (n // 4, n // 2), (n // 2, 3 * n // 4), (3 * n // 4, n), (n, n)]  # rank 4: empty
+
+    def rank_fn(ctx):
+        s, e = bounds[ctx.rank]
+        bd = gbdt.bin_dataset(X[s:e], device="cpu", sketch_rows=n, dist=ctx, n_rows_global=n, row_offset=s,
+                              sketch_mode="summary", sketch_weights=w[s:e])
+        return bd.cuts, bd.nbins
+
+    outs = loopback.run_ranks(5, rank_fn, device="cpu")
+    for c, nb in outs[1:]:
+        assert torch.equal(c, outs[0][0]) and torch.equal(nb, outs[0][1])
+    c, nb = outs[0]
+    assert torch.equal(c[2:], exact[0][2:]) and torch.equal(nb[2:], exact[1][2:])
+    for f in (0, 1):
+        assert _rank_error_ok(X, w, c, nb, f, 0.006)
+
+
+def test_device_summary_equals_host_summary():
+    X = _mixed(30_000, 10)
+    w = np.random.default_rng(11).uniform(0.2, 2.0, len(X))
+    for wt in (None, w):
+        host = sketch.QuantileSummary.build(X, wt, size=1024).to_arrays()
+        dev = sketch.device_summary(torch.from_numpy(X), None if wt is None else torch.from_numpy(wt), size=1024)
+        for a, b in zip(host[:3], dev):
+            assert np.array_equal(a, b)
+
+
+def test_full_data_sketch_single_rank_is_exact_and_ranks_agree():
+    """sketch_rows=None: every row is sketched -- exact weighted quantiles (the NumPy oracle) on one
+    rank; under data parallelism the per-rank device summaries merge to the same cuts on every rank,
+    within the summary's rank error of the exact ones."""
+    from cobalt_smart_lender_ai_amd.parallel import loopback
+    from cobalt_smart_lender_ai_amd.parallel.dist import shard_range
+
+    n = 40_000
+    X = _mixed(n, 12)
+    w = np.random.default_rng(13).uniform(0.5, 3.0, n)
+    one = gbdt.bin_dataset(X, device="cpu", sketch_rows=None, sketch_weights=w)
+    for f, maxb in ((0, 256), (1, 255)):
+        ref = sketch.weighted_quantile_cuts_np(X[:, f], w, maxb)
+        assert int(one.nbins[f]) == len(ref) + 1
+        assert np.array_equal(one.cuts[f, : len(ref)].numpy(), ref)
+
+    def rank_fn(ctx):
+        s, e = shard_range(n, ctx.rank, ctx.world)
+        bd = gbdt.bin_dataset(X[s:e], device="cpu", sketch_rows=None, dist=ctx, n_rows_global=n, row_offset=s,
+                              sketch_weights=w[s:e])
+        return bd.cuts, bd.nbins
+
+    outs = loopback.run_ranks(4, rank_fn, device="cpu")
+    for c, nb in outs[1:]:
+        assert torch.equal(c, outs[0][0]) and torch.equal(nb, outs[0][1])
+    c, nb = outs[0]
+    assert torch.equal(c[2:], one.cuts[2:]) and torch.equal(nb[2:], one.nbins[2:])
+    for f in (0, 1):
+        assert _rank_error_ok(X, w, c, nb, f, 0.004)
