@@ -177,19 +177,44 @@ def decode(data: bytes) -> Any:
 
 # ------------------------------------------------------------------------------------- encoder
 
+_FRAME_TARGET = 64 * 1024  # pickle's protocol-4 frame size target (pickle._Framer)
+
+
 class _Writer:
+    """Protocol-4 opcode writer with pickle's framing: opcodes accumulate in a frame that is emitted
+    as ``FRAME <len>`` once it reaches 64 KiB at an object boundary or at the end, and a bytes payload
+    of >= 64 KiB is written OUTSIDE any frame after the current one is flushed -- what CPython's
+    pickler (and so joblib.dump) produces, byte for byte."""
+
     def __init__(self) -> None:
-        self.b = io.BytesIO()
+        self.out = io.BytesIO()
+        self.frame = io.BytesIO()
         self.memo_n = 0
 
     def op(self, code: bytes, payload: bytes = b"") -> None:
-        self.b.write(code + payload)
+        self.frame.write(code + payload)
+
+    def commit(self, force: bool = False) -> None:
+        n = self.frame.tell()
+        if n and (force or n >= _FRAME_TARGET):
+            self.out.write(b"\x95" + struct.pack("<Q", n) + self.frame.getvalue())  # FRAME
+            self.frame = io.BytesIO()
+
+    def large(self, header: bytes, payload: bytes) -> None:
+        self.commit(force=True)
+        self.out.write(header)
+        self.out.write(payload)
+
+    def getvalue(self) -> bytes:
+        self.commit(force=True)
+        return self.out.getvalue()
 
     def memoize(self) -> None:
         self.op(b"\x94")  # MEMOIZE
         self.memo_n += 1
 
     def str(self, s: str) -> None:
+        self.commit()
         e = s.encode("utf-8")
         if len(e) < 256:
             self.op(b"\x8c", bytes([len(e)]) + e)  # SHORT_BINUNICODE
@@ -204,6 +229,7 @@ class _Writer:
         self.memoize()
 
     def value(self, v: Any) -> None:
+        self.commit()
         if v is None:
             self.op(b"N")
         elif v is True:
@@ -275,10 +301,12 @@ class _Writer:
 
     def bytearray(self, raw: bytes) -> None:
         self.glob("builtins", "bytearray")
-        if len(raw) < 2**32:
-            self.op(b"B", struct.pack("<I", len(raw)) + raw)  # BINBYTES
+        self.commit()
+        head = b"B" + struct.pack("<I", len(raw)) if len(raw) < 2**32 else b"\x8e" + struct.pack("<Q", len(raw))
+        if len(raw) >= _FRAME_TARGET:
+            self.large(head, bytes(raw))  # BINBYTES / BINBYTES8 outside the frames
         else:
-            self.op(b"\x8e", struct.pack("<Q", len(raw)) + raw)  # BINBYTES8
+            self.op(head, bytes(raw))
         self.memoize()
         self.op(b"\x85")  # TUPLE1
         self.memoize()
@@ -289,7 +317,7 @@ class _Writer:
 def encode_xgb_classifier(state: dict[str, Any], booster_raw: bytes) -> bytes:
     """Pickle (protocol 4) an ``xgboost.sklearn.XGBClassifier`` with ``state`` and a UBJSON booster."""
     w = _Writer()
-    w.op(b"\x80", bytes([4]))  # PROTO 4
+    w.out.write(b"\x80" + bytes([4]))  # PROTO 4 (before the first frame)
     w.glob("xgboost.sklearn", "XGBClassifier")
     w.op(b")")  # EMPTY_TUPLE
     w.op(b"\x81")  # NEWOBJ
@@ -314,7 +342,7 @@ def encode_xgb_classifier(state: dict[str, Any], booster_raw: bytes) -> bytes:
     w.op(b"u")  # SETITEMS
     w.op(b"b")  # BUILD (XGBClassifier)
     w.op(b".")  # STOP
-    return w.b.getvalue()
+    return w.getvalue()
 
 
 def read_xgb_classifier_pickle(data: bytes) -> tuple[dict[str, Any], bytes]:

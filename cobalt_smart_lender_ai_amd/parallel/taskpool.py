@@ -40,10 +40,11 @@ def _init_slot(counter, n_gpus: int) -> None:
     os.environ.setdefault("OMP_NUM_THREADS", "2")
 
 
-def worker_device() -> str:
-    """The device string of the current pool worker (``cuda:N``; ``cpu`` without GPUs)."""
+def worker_device(device_type: str = "cuda") -> str:
+    """The device string of the current pool worker (``cuda:N``; ``cpu`` without GPUs or when the
+    caller asked for CPU work)."""
     gpu = _SLOT.get("gpu")
-    if gpu is None:
+    if gpu is None or device_type != "cuda":
         return "cpu"
     import torch
 
@@ -85,3 +86,22 @@ def resolve_workers(fits_in_parallel: int | None) -> int:
     if fits_in_parallel is None:
         return max(1, visible_gpus())
     return max(1, int(fits_in_parallel))
+
+
+def can_auto_pool(device=None) -> bool:
+    """Whether a caller may create a :class:`GpuTaskPool` on its own: only for GPU work, and only from
+    a process that has not initialised HIP yet (its children would inherit the runtime's state, and
+    the pool refuses such spawns). Otherwise the caller logs why and runs in-process."""
+    import logging
+
+    import torch
+
+    dev_type = torch.device(device).type if device is not None else ("cuda" if visible_gpus() else "cpu")
+    if dev_type != "cuda":
+        return False
+    if torch.cuda.is_initialized():
+        logging.getLogger(__name__).warning(
+            "not creating a GPU task pool: HIP is already initialised in this process (create the pool "
+            "before the first GPU call and pass it in); running the fits in this process")
+        return False
+    return True

@@ -46,13 +46,14 @@ def run_training(df_tree: pd.DataFrame, cfg: TrainConfig | None = None, store: A
                  pool=None) -> dict:
     """``pool``: a :class:`~..parallel.taskpool.GpuTaskPool` for the search's task-parallel fits.
     Without one, ``cfg.fits_in_parallel`` > 1 (None = all visible GPUs) creates a pool here -- before
-    this function's own GPU work, so the workers are spawned from a process without HIP state (when
-    the caller has not touched the GPU yet either; ``cli train`` guarantees that)."""
-    from ..parallel.taskpool import GpuTaskPool, resolve_workers
+    this function's own GPU work, so the workers are spawned from a process without HIP state. Only
+    for GPU work and only if this process has not initialised HIP yet (``can_auto_pool``; ``cli
+    train`` guarantees it); otherwise the fits run in this process."""
+    from ..parallel.taskpool import GpuTaskPool, can_auto_pool, resolve_workers
 
     cfg = cfg or TrainConfig()
     own_pool = None
-    if pool is None and resolve_workers(cfg.fits_in_parallel) > 1:
+    if pool is None and resolve_workers(cfg.fits_in_parallel) > 1 and can_auto_pool(device):
         pool = own_pool = GpuTaskPool(resolve_workers(cfg.fits_in_parallel))
     try:
         return _run_training(df_tree, cfg, store, local_dir, device, rfe_params, pool)

@@ -86,6 +86,23 @@ def _host_bytes(src) -> torch.Tensor:
     return read_file_pinned(path)
 
 
+def dedup_names(names: list[str]) -> list[str]:
+    """pandas.read_csv's (C parser) renaming of repeated header names: the second ``a`` becomes
+    ``a.1``, the third ``a.2``, skipping suffixed names the header already holds."""
+    out = list(names)
+    counts: dict[str, int] = {}
+    for i, col in enumerate(out):
+        old = col
+        cur = counts.get(col, 0)
+        while cur > 0:
+            counts[old] = cur + 1
+            col = f"{old}.{cur}"
+            cur = cur + 1 if col in out else counts.get(col, 0)
+        out[i] = col
+        counts[col] = cur + 1
+    return out
+
+
 def _header(host: np.ndarray) -> tuple[list[str], int]:
     """Column names and the byte offset of the first data row (the header may be quoted)."""
     inq = False
@@ -102,7 +119,7 @@ def _header(host: np.ndarray) -> tuple[list[str], int]:
         i += 1
     line = head[:i].decode("utf-8").rstrip("\r")
     names = next(_csv.reader(io.StringIO(line))) if line else []
-    return names, min(i + 1, n)
+    return dedup_names(names), min(i + 1, n)
 
 
 def _chk(rc: int, name: str) -> None:
@@ -220,7 +237,7 @@ def read_csv_gpu(src, device, hash_unique_share: float = 0.2, timings: dict | No
                 cols[name] = DCol("b", (st == ST_TRUE).to(torch.uint8), "bool")
             else:
                 v = torch.where(st == ST_TRUE, 1.0, torch.where(st == ST_FALSE, 0.0, float("nan"))).to(torch.float64)
-                cols[name] = DCol("f", v, "float64")
+                cols[name] = DCol("f", v, "boolnull")  # 1 / 0 / NaN; exported as pandas' object bools
         else:
             cols[name] = scols[c]
     if timings is not None:
@@ -415,6 +432,10 @@ def frame_to_csv_bytes(frame, timings: dict | None = None) -> memoryview | bytes
     for j, name in enumerate(names):
         c = frame[name]
         d = descs[j]
+        if c.kind == "f" and c.dtype == "boolnull":  # pandas writes object bools: True / False / empty
+            from .device_frame import DCol
+
+            c = DCol("c", torch.where(torch.isnan(c.data), -1.0, c.data).to(torch.int32), "object", [False, True])
         if c.kind == "f":
             v = c.data.to(torch.float64).contiguous()
             keep.append(v)

@@ -37,7 +37,9 @@ class DCol:
     kind: str                 # "f" float64 values, "c" int32 dictionary codes (-1 = missing), "b" uint8 flags,
                               # "h" int64 device hashes of a near-unique string column (0 = missing)
     data: torch.Tensor        # [N] on the frame's device
-    dtype: str                # pandas dtype on export: "float64" | "int64" | "bool" | "object"
+    dtype: str                # pandas dtype on export: "float64" | "int64" | "bool" | "object" | "boolnull"
+                              # (a true/false column with missing values: 1 / 0 / NaN on the device, object
+                              # True / False / NaN in pandas, as pandas.read_csv types it)
     vocab: list | None = None  # "c": code -> value
     src: object = None        # "h": the ORIGINAL rows' text (host Arrow column, or csv_gpu.DeviceStrings in
                               # HBM), decoded lazily through rowid
@@ -159,6 +161,9 @@ class DeviceFrame:
             elif pa.types.is_boolean(t) and col.null_count == 0:
                 a = col.to_numpy(zero_copy_only=False).astype(np.uint8)
                 cols[name] = DCol("b", torch.from_numpy(a).to(dev), "bool")
+            elif pa.types.is_boolean(t):
+                a = np.array(col.cast(pa.float64()).to_numpy(zero_copy_only=False), dtype=np.float64)
+                cols[name] = DCol("f", torch.from_numpy(a).to(dev), "boolnull")
             elif pa.types.is_null(t):
                 cols[name] = DCol("f", torch.full((n,), float("nan"), dtype=torch.float64, device=dev), "float64")
             else:
@@ -202,6 +207,10 @@ class DeviceFrame:
         tab = pcsv.read_csv(src, read_options=pcsv.ReadOptions(use_threads=threads, block_size=1 << 26),
                             convert_options=pcsv.ConvertOptions(strings_can_be_null=True, null_values=PANDAS_NA,
                                                                 quoted_strings_can_be_null=True))
+        from .csv_gpu import dedup_names
+
+        if len(set(tab.column_names)) != len(tab.column_names):  # repeated headers: pandas' a, a.1, ...
+            tab = tab.rename_columns(dedup_names(tab.column_names))
         _ = io
         return cls.from_arrow(tab, device)
 
@@ -224,6 +233,11 @@ class DeviceFrame:
                 out[name] = pd.Series(voc[np.where(a < 0, len(c.vocab), a)], dtype=object)
             elif c.kind == "b":
                 out[name] = a.astype(bool) if c.dtype == "bool" else a.astype(np.int64)
+            elif c.dtype == "boolnull":
+                v = np.empty(len(a), dtype=object)
+                v[:] = a == 1.0
+                v[np.isnan(a)] = np.nan
+                out[name] = v
             elif c.dtype == "int64" and not np.isnan(a).any():
                 out[name] = a.astype(np.int64)
             else:

@@ -97,8 +97,8 @@ def _worker(args):
     """Pool task: the fold scores of a candidate subset on this worker's GPU (parallel/taskpool.py)."""
     from ..parallel.taskpool import worker_device
 
-    X, y, folds, base, cands = args
-    return _fold_scores(X, y, folds, base, cands, worker_device())
+    X, y, folds, base, cands, dev_type = args
+    return _fold_scores(X, y, folds, base, cands, worker_device(dev_type))
 
 
 def randomized_search(X, y, param_distributions: dict, base_params: dict, n_iter: int = 20, cv: int = 3,
@@ -107,7 +107,7 @@ def randomized_search(X, y, param_distributions: dict, base_params: dict, n_iter
     """``pool`` (a :class:`~..parallel.taskpool.GpuTaskPool`, created before this process touched the
     GPU) runs the (candidate x fold) fits task-parallel, candidates dealt round-robin to its workers;
     otherwise ``n_gpus`` > 1 (None = all visible) creates one for this call."""
-    from ..parallel.taskpool import GpuTaskPool, visible_gpus
+    from ..parallel.taskpool import GpuTaskPool, can_auto_pool, visible_gpus
 
     X = np.asarray(X, dtype=np.float32)
     y = np.asarray(y, dtype=np.float32)
@@ -117,14 +117,15 @@ def randomized_search(X, y, param_distributions: dict, base_params: dict, n_iter
     own = None
     if pool is None:
         ngpu = visible_gpus() if n_gpus is None else min(int(n_gpus), visible_gpus())
-        if ngpu > 1:
+        if ngpu > 1 and can_auto_pool(device):
             pool = own = GpuTaskPool(ngpu, ngpu)
     try:
         if pool is not None:
             nw = pool.workers
             shards = [list(range(i, len(cands), nw)) for i in range(nw)]
             shards = [sh for sh in shards if sh]
-            parts = pool.map(_worker, [(X, y, folds, base_params, [cands[j] for j in sh]) for sh in shards])
+            dev_type = torch.device(device).type if device is not None else "cuda"
+            parts = pool.map(_worker, [(X, y, folds, base_params, [cands[j] for j in sh], dev_type) for sh in shards])
             scores = np.zeros((len(cands), len(folds)))
             for sh, part in zip(shards, parts):
                 scores[sh] = part

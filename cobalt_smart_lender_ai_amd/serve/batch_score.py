@@ -300,15 +300,25 @@ def rank_segments(sizes: list[int], rank: int, world: int) -> list[tuple[int, in
 
 
 def score_files(booster: Booster, paths, out_dir, rank: int = 0, world: int = 1, device=None,
-                chunk: int = 1 << 20, slots: int = 4, stage_threads: int = 8, h2d_streams: int = 2) -> dict:
+                chunk: int = 1 << 20, slots: int = 4, stage_threads: int = 8, h2d_streams: int = 2,
+                max_rows: int | None = None) -> dict:
     """Score this rank's share of the shard files and write ``out_dir/scores_rank{rank:05d}.npy`` (+ a
     JSON index with the global row offset). GPU: the pipelined :class:`HostStreamScorer`; CPU: the
-    host predictor (the multi-rank rehearsal of the sharding, tests/test_batch_score.py)."""
+    host predictor (the multi-rank rehearsal of the sharding, tests/test_batch_score.py).
+    ``max_rows``: score only the first rows of the share (warm-ups)."""
     import json
     from pathlib import Path
 
     arrs = open_shards(paths)  # validates the headers (and serves the CPU path)
     segs = rank_segments([len(a) for a in arrs], rank, world)
+    if max_rows is not None:
+        cut, left = [], int(max_rows)
+        for i, b, e, g in segs:
+            if left <= 0:
+                break
+            cut.append((i, b, min(e, b + left), g))
+            left -= cut[-1][2] - b
+        segs = cut
     n = sum(e - b for _, b, e, _ in segs)
     out_dir = Path(out_dir)
     out_dir.mkdir(parents=True, exist_ok=True)
@@ -347,13 +357,36 @@ def score_files(booster: Booster, paths, out_dir, rank: int = 0, world: int = 1,
 
 
 def gather_scores(out_dir) -> np.ndarray:
-    """Concatenate the per-rank score files of ``out_dir`` in global row order."""
+    """Concatenate the per-rank score files of ``out_dir`` in global row order.
+
+    Only the ranks of the LAST job are used: the world size comes from rank 0's index, ranks
+    ``0 .. world - 1`` must all be present with that world size, and their global row ranges must
+    tile ``[0, total)`` without gaps or overlaps -- files left by an earlier run with more ranks are
+    ignored, and an inconsistent directory raises instead of returning shifted rows."""
     import json
     from pathlib import Path
 
-    metas = sorted((json.loads(p.read_text()) for p in Path(out_dir).glob("scores_rank*.json")),
-                   key=lambda m: (m["global_offset"] is None, m["global_offset"] or 0))
-    parts = [np.load(str(Path(out_dir) / f"scores_rank{m['rank']:05d}.npy"), allow_pickle=False) for m in metas]
+    d = Path(out_dir)
+    p0 = d / "scores_rank00000.json"
+    if not p0.exists():
+        return np.empty(0, np.float32)
+    world = int(json.loads(p0.read_text())["world"])
+    metas = []
+    for r in range(world):
+        p = d / f"scores_rank{r:05d}.json"
+        if not p.exists():
+            raise ValueError(f"{d}: rank {r} of a {world}-rank job has no score index")
+        m = json.loads(p.read_text())
+        if int(m["world"]) != world:
+            raise ValueError(f"{d}: rank {r} was written by a {m['world']}-rank job, rank 0 by a {world}-rank job")
+        metas.append(m)
+    live = sorted((m for m in metas if m["rows"]), key=lambda m: m["global_offset"])
+    pos = 0
+    for m in live:
+        if int(m["global_offset"]) != pos:
+            raise ValueError(f"{d}: rank {m['rank']} starts at row {m['global_offset']}, expected {pos}")
+        pos += int(m["rows"])
+    parts = [np.load(str(d / f"scores_rank{m['rank']:05d}.npy"), allow_pickle=False) for m in live]
     return np.concatenate(parts) if parts else np.empty(0, np.float32)
 
 
@@ -462,9 +495,11 @@ def main(argv=None) -> int:
         paths = sorted(p for g in a.input for p in (glob.glob(g) or [g]))
         arrs = open_shards(paths)
         total = sum(len(x) for x in arrs)
-        # warm-up: scorer construction (pinned buffers, graphs) + one chunk
-        score_files(b, [paths[0]], Path(a.output) / "_warm", 0, 1, dev, chunk=min(a.host_chunk, len(arrs[0])),
-                    slots=a.slots, stage_threads=a.stage_threads)
+        # warm-up: scorer construction (pinned buffers, graphs) + ONE chunk, in a directory of this
+        # rank's own (ranks must not truncate / remap each other's warm-up file)
+        wchunk = min(a.host_chunk, len(arrs[0]))
+        score_files(b, [paths[0]], Path(a.output) / "_warm" / f"rank{ctx.rank}", 0, 1, dev, chunk=wchunk,
+                    slots=a.slots, stage_threads=a.stage_threads, max_rows=wchunk)
         ctx.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()

@@ -73,3 +73,35 @@ def test_open_shards_refuses_pickles(tmp_path):
     np.save(p, np.array([{"a": 1}], dtype=object), allow_pickle=True)
     with pytest.raises(ValueError):
         bs.open_shards([p])
+
+
+def test_gather_ignores_stale_ranks_and_rejects_gaps(tmp_path, reference_model_bytes):
+    """A 3-rank run followed by a 2-rank run into the same directory: gather uses the 2 live ranks
+    only (the 3-rank run's rank 2 file is stale); a missing rank or an overlap raises. ``max_rows``
+    (the CLI's one-chunk warm-up) scores only the head of a share."""
+    import json
+
+    from cobalt_smart_lender_ai_amd.models.booster import load_pickle_bytes, predict_margin_host, sigmoid32
+
+    _, b = load_pickle_bytes(reference_model_bytes)
+    X = np.random.default_rng(3).normal(size=(5000, 20)).astype(np.float32) * 50 + 100
+    p = tmp_path / "s.npy"
+    np.save(p, X)
+    out = tmp_path / "out"
+    for r in range(3):
+        bs.score_files(b, [str(p)], out, r, 3, device="cpu", chunk=1000)
+    for r in range(2):
+        bs.score_files(b, [str(p)], out, r, 2, device="cpu", chunk=1000)
+    ref = sigmoid32(predict_margin_host(b, X))
+    assert np.array_equal(bs.gather_scores(out), ref)
+    m = json.loads((out / "scores_rank00001.json").read_text())
+    m["global_offset"] += 1
+    (out / "scores_rank00001.json").write_text(json.dumps(m))
+    with pytest.raises(ValueError):
+        bs.gather_scores(out)
+    (out / "scores_rank00001.json").unlink()
+    with pytest.raises(ValueError):
+        bs.gather_scores(out)
+    meta = bs.score_files(b, [str(p)], tmp_path / "warm", 0, 1, device="cpu", chunk=1000, max_rows=700)
+    assert meta["rows"] == 700
+    assert np.array_equal(np.load(tmp_path / "warm" / "scores_rank00000.npy"), ref[:700])

@@ -193,3 +193,45 @@ def test_pair_gain_equals_sum_of_child_gains(alpha):
     pair = H._calc_gain_pair(gl, hl, gr, hr, lam, alpha)
     ref = H._calc_gain(gl, hl, lam, alpha, 1.0) + H._calc_gain(gr, hr, lam, alpha, 1.0)
     assert np.allclose(pair, ref, rtol=1e-12, atol=1e-12)
+
+
+def _pickle_skeleton(data: bytes) -> list:
+    """Opcode stream with scalar values / byte payloads abstracted and pickle's FRAME markers dropped
+    (frame splits follow payload sizes); state keys and every structural opcode are kept."""
+    import pickletools
+
+    scal = {"NONE", "NEWTRUE", "NEWFALSE", "BININT1", "BININT2", "BININT", "BINFLOAT"}
+    out = []
+    for op, arg, _ in pickletools.genops(data):
+        if op.name == "FRAME":
+            continue
+        if op.name in scal:
+            out.append("SCALAR")
+        elif op.name in ("BINBYTES", "SHORT_BINBYTES", "BINBYTES8"):
+            out.append("BYTES")
+        else:
+            out.append((op.name, arg) if op.name == "SHORT_BINUNICODE" else op.name)
+    return out
+
+
+def test_pickle_writer_reencodes_reference_checkpoint_byte_exactly(reference_model_bytes):
+    """The checkpoint writer (protocol 4, pickle's framing) re-encodes the reference joblib pickle of
+    its own decoded state + booster into the SAME bytes (xgboost is not installed here: the reference
+    file is the only available pin of what real xgboost / joblib write)."""
+    st, raw = safe_pickle.read_xgb_classifier_pickle(reference_model_bytes)
+    assert safe_pickle.encode_xgb_classifier(st, raw) == reference_model_bytes
+
+
+def test_training_job_pickle_has_reference_opcode_skeleton(reference_model_bytes):
+    """What the training job writes (pipeline/train_tree.py -> dump_pickle_bytes) has the reference
+    checkpoint's opcode skeleton: same globals, same state keys in the same order, same structure."""
+    from cobalt_smart_lender_ai_amd.models.booster import dump_pickle_bytes
+
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(3000, 20)).astype(np.float32)
+    y = (X[:, 0] + 0.3 * rng.normal(size=3000) > 0).astype(np.float32)
+    b = gbdt.train(X, y, dict(n_estimators=3, max_depth=3), device="cpu")
+    sk = {"scale_pos_weight": 6.7, "random_state": 78, "n_estimators": 300, "max_depth": 7, "learning_rate": 0.05,
+          "gamma": 5, "subsample": 1.0, "colsample_bytree": 1.0, "eval_metric": "logloss",
+          "kwargs": {"use_label_encoder": False}}
+    assert _pickle_skeleton(dump_pickle_bytes(b, sk)) == _pickle_skeleton(reference_model_bytes)

@@ -74,7 +74,7 @@ def test_tricky_csv_matches_pyarrow(crlf):
     assert_frames_identical(g, a)
     assert g["uniq"].kind == "h" and g["name"].kind == "c"
     assert g["neg0"].dtype == "int64" and g["plus"].dtype == "float64" and g["big"].dtype == "float64"
-    assert g["flag"].kind == "b" and g["flag_null"].dtype == "float64"
+    assert g["flag"].kind == "b" and g["flag_null"].dtype == "boolnull"
 
 
 def test_no_trailing_newline_and_small_frame():
@@ -228,3 +228,19 @@ def test_prep_flow_gpu_engine_writes_the_pandas_artifacts(tmp_path):
     # vs the pandas engine: pandas' default float parser reads some raw values a few dozen ulp off
     for a, b in zip(outs["gpu"], outs["pandas"]):
         assert_frames_equal(a, b, rtol=1e-13)
+
+
+def test_gpu_reader_pandas_typing_duplicates_and_nullable_bools():
+    """read_table's GPU path equals pandas.read_csv on repeated headers (a, a.2, ...) and nullable
+    bools (object True / False / NaN), and the GPU writer renders that frame as pandas.to_csv does."""
+    import io
+
+    import pandas as pd
+
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import frame_to_csv_bytes
+
+    data = b"a,b,a,flag,flagn,a.1\n1,x,2.5,True,True,7\n2,y,3.5,False,,8\n3,,4.5,True,False,9\n"
+    ref = pd.read_csv(io.BytesIO(data), float_precision="round_trip")
+    g = DeviceFrame.read_csv(data, "cuda", engine="gpu")
+    pd.testing.assert_frame_equal(g.to_pandas(), ref)
+    assert bytes(frame_to_csv_bytes(g)) == ref.to_csv(index=False).encode()

@@ -167,3 +167,24 @@ def test_notebook_preset_matches_pandas_oracle():
                 d[c] = d[c].fillna(0)
         d = d.drop_duplicates()
     pd.testing.assert_frame_equal(ours.reset_index(drop=True), d.reset_index(drop=True), check_dtype=False)
+
+
+def test_read_table_pandas_typing_duplicates_and_nullable_bools():
+    """the CSV readers behind read_table type a frame like pandas.read_csv -- repeated
+    header names become a, a.1, a.2 (pandas' renaming) instead of collapsing into one column, and a
+    true/false column with missing values is pandas' object True / False / NaN (not float64); the
+    CSV writer renders it as pandas does."""
+    import io
+
+    import pandas as pd
+
+    from cobalt_smart_lender_ai_amd.prep.csv_gpu import dedup_names
+    from cobalt_smart_lender_ai_amd.prep.device_frame import DeviceFrame
+
+    assert dedup_names(["a", "b", "a", "a", "a.1"]) == ["a", "b", "a.2", "a.3", "a.1"]
+    data = b"a,b,a,flag,flagn,a.1\n1,x,2.5,True,True,7\n2,y,3.5,False,,8\n3,,4.5,True,False,9\n"
+    ref = pd.read_csv(io.BytesIO(data), float_precision="round_trip")
+    got = DeviceFrame.read_csv(data, "cpu", engine="arrow").to_pandas()
+    assert list(got.columns) == list(ref.columns)
+    pd.testing.assert_frame_equal(got, ref)
+    assert ref["flagn"].dtype == object

@@ -27,3 +27,19 @@ def test_pooled_search_equals_single_process_cpu():
     got = np.stack([res.cv_results_[f"split{k}_test_score"] for k in range(3)], 1)
     assert np.array_equal(got, ref)
     assert res.best_index_ == int(np.argmax(ref.mean(1)))
+
+
+def test_no_automatic_pool_for_cpu_work_or_an_initialised_process(monkeypatch):
+    """run_training / randomized_search create a pool on their own only for GPU work from
+    a process without HIP state; a CPU request stays in-process (and on the CPU in pool workers)."""
+    import torch
+
+    from cobalt_smart_lender_ai_amd.parallel import taskpool
+
+    assert not taskpool.can_auto_pool("cpu")
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    assert not taskpool.can_auto_pool("cuda")
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
+    assert taskpool.can_auto_pool("cuda")
+    monkeypatch.setitem(taskpool._SLOT, "gpu", 0)
+    assert taskpool.worker_device("cpu") == "cpu"
