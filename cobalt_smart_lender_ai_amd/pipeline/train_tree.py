@@ -11,6 +11,12 @@ the local ``models/`` directory.
 Deliberate, documented difference: rows whose ``loan_default`` is missing (loan statuses outside the
 reference's map, e.g. "Does not meet the credit policy...") are dropped before the split, since a
 NaN label has no defined gradient (XGBoost rejects such labels).
+
+The tree dataset may be a pandas frame (the reference's hand-off: ``pd.read_csv`` of the tree CSV,
+``model_tree_train_test.py:77``) or a :class:`~..prep.device_frame.DeviceFrame` straight from the
+device preprocessing: then the feature matrix is built in HBM (``tree_training_matrix``), the split,
+RFE repacking, search folds and evaluation rows are device gathers, and only labels, split indices and
+the small per-fit results touch the host. Both hand-offs train the same models (tested).
 """
 from __future__ import annotations
 
@@ -41,7 +47,57 @@ def _matrix(df: pd.DataFrame) -> np.ndarray:
     return df.to_numpy(dtype=np.float32, na_value=np.nan)
 
 
-def run_training(df_tree: pd.DataFrame, cfg: TrainConfig | None = None, store: ArtifactStore | None = None,
+def _host_inputs(df_tree: pd.DataFrame):
+    df = df_tree.drop(columns=LEAKAGE_COLUMNS, errors="ignore")
+    n_nan = int(df["loan_default"].isna().sum())
+    if n_nan:
+        log.info("Dropping %d rows with a missing loan_default label", n_nan)
+        df = df.loc[df["loan_default"].notna()]
+    X = df.drop(columns=["loan_default"])
+    names, types = gbdt._feature_info(X)
+    return _matrix(X), df["loan_default"].to_numpy(dtype=np.float32), names, types
+
+
+def _device_inputs(frame):
+    """(X [N, F] float32 device matrix, y host labels, names, XGBoost feature types) of a DeviceFrame,
+    typed as the pandas hand-off would be (bool -> "i", integer -> "int", else "float")."""
+    import torch
+
+    from ..prep.device_prep import tree_training_matrix
+
+    n0 = frame.n
+    X, y, names = tree_training_matrix(frame, drop=LEAKAGE_COLUMNS)
+    if X.shape[0] != n0:
+        log.info("Dropping %d rows with a missing loan_default label", n0 - X.shape[0])
+    types = []
+    for c in names:
+        col = frame[c]
+        if col.dtype == "bool":
+            types.append("i")
+        elif col.dtype == "int64" and (col.kind == "b" or not bool(torch.isnan(col.data).any())):
+            types.append("int")
+        else:
+            types.append("float")
+    return X, y.cpu().numpy().astype(np.float32), names, types
+
+
+def _rows(X, idx):
+    if isinstance(X, np.ndarray):
+        return X[idx]
+    import torch
+
+    return X.index_select(0, torch.as_tensor(np.asarray(idx, dtype=np.int64), device=X.device))
+
+
+def _cols(X, idx):
+    if isinstance(X, np.ndarray):
+        return np.ascontiguousarray(X[:, idx])
+    import torch
+
+    return X.index_select(1, torch.as_tensor(np.asarray(idx, dtype=np.int64), device=X.device)).contiguous()
+
+
+def run_training(df_tree, cfg: TrainConfig | None = None, store: ArtifactStore | None = None,
                  local_dir: str | Path = "models", device=None, rfe_params: dict | None = None,
                  pool=None) -> dict:
     """``pool``: a :class:`~..parallel.taskpool.GpuTaskPool` for the search's task-parallel fits.
@@ -62,37 +118,37 @@ def run_training(df_tree: pd.DataFrame, cfg: TrainConfig | None = None, store: A
             own_pool.close()
 
 
-def _run_training(df_tree: pd.DataFrame, cfg: TrainConfig, store: ArtifactStore | None, local_dir, device,
+def _run_training(df_tree, cfg: TrainConfig, store: ArtifactStore | None, local_dir, device,
                   rfe_params: dict | None, pool) -> dict:
+    from ..prep.device_frame import DeviceFrame
+
     t0 = time.perf_counter()
-    df = df_tree.drop(columns=LEAKAGE_COLUMNS, errors="ignore")
-    n_nan = int(df["loan_default"].isna().sum())
-    if n_nan:
-        log.info("Dropping %d rows with a missing loan_default label", n_nan)
-        df = df.loc[df["loan_default"].notna()]
-    X = df.drop(columns=["loan_default"])
-    y = df["loan_default"].to_numpy(dtype=np.float32)
-    tr, te = train_test_split_indices(len(df), cfg.test_size, cfg.split_random_state)
-    Xtr, Xte, ytr, yte = X.iloc[tr], X.iloc[te], y[tr], y[te]
-    log.info("Train shape: %s, Test shape: %s", Xtr.shape, Xte.shape)
+    on_device = isinstance(df_tree, DeviceFrame)
+    X, y, names, types = _device_inputs(df_tree) if on_device else _host_inputs(df_tree)
+    if on_device and device is None:
+        device = X.device
+    tr, te = train_test_split_indices(len(y), cfg.test_size, cfg.split_random_state)
+    Xtr, Xte, ytr, yte = _rows(X, tr), _rows(X, te), y[tr], y[te]
+    log.info("Train shape: %s, Test shape: %s", tuple(Xtr.shape), tuple(Xte.shape))
     spw = float((ytr == 0).sum() / max((ytr == 1).sum(), 1))
     log.info("scale_pos_weight=%.4f", spw)
+    t_split = time.perf_counter() - t0
 
-    names, types = gbdt._feature_info(Xtr)
     # ---- RFE to exactly n features (XGBoost defaults: 100 trees, depth 6, eta 0.3)
     base_rfe = dict(gbdt.XGB_DEFAULTS, scale_pos_weight=spw, random_state=cfg.rfe_random_state)
     base_rfe.update(rfe_params or {})
     tr_rfe = time.perf_counter()
-    r = rfe(_matrix(Xtr), ytr, base_rfe, n_features_to_select=cfg.rfe_n_features, step=cfg.rfe_step,
+    r = rfe(Xtr, ytr, base_rfe, n_features_to_select=cfg.rfe_n_features, step=cfg.rfe_step,
             device=device, feature_names=names)
     selected = r.selected(names)
+    sel_idx = [names.index(c) for c in selected]
     t_rfe = time.perf_counter() - tr_rfe
     log.info("Selected %d features: %s", len(selected), selected)
 
     # ---- randomized search on the selected features
     base = dict(gbdt.XGB_DEFAULTS, scale_pos_weight=spw, random_state=cfg.base_random_state)
     ts = time.perf_counter()
-    sr = randomized_search(_matrix(Xtr[selected]), ytr, cfg.search_space, base, n_iter=cfg.search_n_iter,
+    sr = randomized_search(_cols(Xtr, sel_idx), ytr, cfg.search_space, base, n_iter=cfg.search_n_iter,
                            cv=cfg.search_cv_folds, random_state=cfg.search_random_state, device=device,
                            n_gpus=1, pool=pool)
     t_search = time.perf_counter() - ts
@@ -100,10 +156,11 @@ def _run_training(df_tree: pd.DataFrame, cfg: TrainConfig, store: ArtifactStore 
     log.info("Best params: %s", sr.best_params_)
     best = sr.best_estimator_
     best.feature_names = list(selected)
-    best.feature_types = [types[names.index(c)] for c in selected] if types else None
+    best.feature_types = [types[i] for i in sel_idx] if types else None
 
     # ---- evaluation
-    proba = best.predict_proba(_matrix(Xte[selected]), device=device)
+    te0 = time.perf_counter()
+    proba = best.predict_proba(_cols(Xte, sel_idx), device=device)
     proba = np.asarray(proba.cpu().numpy() if hasattr(proba, "cpu") else proba)
     pred = (proba > 0.5).astype(np.int64)
     report = cls_metrics.classification_report(yte.astype(np.int64), pred, output_dict=True)
@@ -140,7 +197,10 @@ def _run_training(df_tree: pd.DataFrame, cfg: TrainConfig, store: ArtifactStore 
         store.save_figure(fig_imp, out + "feature_importance.png")
     plots.close(fig_cm)
     plots.close(fig_imp)
-    metrics["timing_s"] = {"rfe": t_rfe, "search": t_search, "total": time.perf_counter() - t0}
+    metrics["timing_s"] = {"inputs_split": t_split, "rfe": t_rfe, "search": t_search,
+                           "eval_artifacts": time.perf_counter() - te0, "total": time.perf_counter() - t0}
+    metrics["rfe_fit_s"] = [h["fit_s"] for h in r.history]
+    metrics["hand_off"] = "device" if on_device else "pandas"
     metrics["selected_features"] = selected
     metrics["config"] = {k: v for k, v in asdict(cfg).items() if k != "search_space"}
     return metrics

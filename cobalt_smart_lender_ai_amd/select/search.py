@@ -52,17 +52,26 @@ def _fold_scores(X, y, folds, base: dict, candidates: list[dict], device, stream
     from concurrent.futures import ThreadPoolExecutor
 
     Xn = X if isinstance(X, (np.ndarray, torch.Tensor)) else np.asarray(X, dtype=np.float32)
-    yn = np.asarray(y, dtype=np.float32)
+    yn = np.asarray(y.cpu().numpy() if isinstance(y, torch.Tensor) else y, dtype=np.float32)
     scores = np.zeros((len(candidates), len(folds)))
     params0 = gbdt.GBDTParams.from_kwargs(**base)
-    bds = [gbdt.bin_dataset(Xn[tr], max_bin=params0.max_bin, sketch_rows=params0.sketch_rows, device=device)
+    on_dev = isinstance(Xn, torch.Tensor) and Xn.is_cuda
+
+    def rows(idx):  # a fold's rows: a device gather when the matrix is device-resident
+        return Xn.index_select(0, torch.as_tensor(idx, device=Xn.device)) if on_dev else Xn[idx]
+
+    bds = [gbdt.bin_dataset(rows(tr), max_bin=params0.max_bin, sketch_rows=params0.sketch_rows, device=device)
            for tr, _ in folds]
+    # labels and validation rows of every fold, staged once (not once per candidate)
+    ytr = [torch.as_tensor(yn[tr], device=bd.device) if bd.device.type == "cuda" else yn[tr]
+           for (tr, _), bd in zip(folds, bds)]
+    Xva = [rows(va) for _, va in folds]
 
     def fit(i: int, k: int, bd=None) -> None:
-        tr, va = folds[k]
+        _, va = folds[k]
         p = gbdt.GBDTParams.from_kwargs(**{**base, **candidates[i]})
-        bst = gbdt.train_binned(bd if bd is not None else bds[k], yn[tr], p)
-        prob = bst.predict_proba(Xn[va], device=str(bds[k].device))
+        bst = gbdt.train_binned(bd if bd is not None else bds[k], ytr[k], p)
+        prob = bst.predict_proba(Xva[k], device=str(bds[k].device))
         scores[i, k] = roc_auc(yn[va], prob)
 
     tasks = [(i, k) for k in range(len(folds)) for i in range(len(candidates))]
@@ -109,8 +118,15 @@ def randomized_search(X, y, param_distributions: dict, base_params: dict, n_iter
     otherwise ``n_gpus`` > 1 (None = all visible) creates one for this call."""
     from ..parallel.taskpool import GpuTaskPool, can_auto_pool, visible_gpus
 
-    X = np.asarray(X, dtype=np.float32)
-    y = np.asarray(y, dtype=np.float32)
+    if isinstance(X, torch.Tensor) and X.is_cuda:  # device-resident matrix: fits stay in this process
+        X = X.to(torch.float32).contiguous()
+        if pool is not None:
+            log.info("randomized_search: device-resident matrix, fits run on this process's streams")
+            pool = None
+        n_gpus = 1
+    else:
+        X = np.asarray(X.cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float32)
+    y = np.asarray(y.cpu().numpy() if isinstance(y, torch.Tensor) else y, dtype=np.float32)
     cands = sample_candidates(param_distributions, n_iter, random_state)
     folds = stratified_kfold_indices(y, cv)
     t0 = time.perf_counter()

@@ -18,7 +18,9 @@
                  2.9M-row x 143-column synthetic raw export: pandas path vs the device-resident path
                  (scripts/bench_prep.py)
   pipeline-100k  the reference's training job (RFE 106 -> 20 + 20 x 3-fold search + refit) end to end
-                 on a 100k-row synthetic sample (scripts/bench_pipeline.py)
+                 on a 100k-row synthetic sample (scripts/bench_pipeline.py), device-resident hand-off
+  pipeline-full  the same job at the reference's production scale: 2.9M raw rows -> ~2.3M training
+                 rows, device-resident from the GPU CSV reader to the artifacts (+ the pandas hand-off)
 """
 from __future__ import annotations
 
@@ -130,6 +132,7 @@ CONFIGS = {
     "plumbing-10k": lambda: plumbing_10k(),
     "cpu-hist-gbdt-10m": lambda: cpu_hist_gbdt(),
     "pipeline-100k": lambda: {"config": "pipeline-100k", **_run(["scripts/bench_pipeline.py"], 1100)},
+    "pipeline-full": lambda: _run(["scripts/bench_pipeline.py", "--full", "--also-pandas"], 1100),
     "gbdt-1m": lambda: _named("gbdt-1m", _run(["bench.py", "--rows", "1000000", "--steps", "3"], 600)),
     "gbdt-10m": lambda: _named("gbdt-10m", _run(["bench.py", "--steps", "3"], 600)),
     "ooc-100m": lambda: {"config": "ooc-100m",

@@ -140,6 +140,27 @@ def test_training_pipeline_writes_reference_artifacts(lake, tmp_path):
     assert bst.num_trees == saved["best_params"]["n_estimators"]
 
 
+def test_device_frame_hand_off_trains_the_same_models(lake, tmp_path):
+    """run_training on a DeviceFrame (device-resident matrix, device gathers for split / RFE repack /
+    folds / eval rows) selects the same features and best params, with the same AUC and the same
+    pickled model, as the pandas hand-off of the same tree CSV."""
+    from cobalt_smart_lender_ai_amd.dataio.artifacts import LocalStore
+    from cobalt_smart_lender_ai_amd.pipeline.train_tree import run_training
+    from cobalt_smart_lender_ai_amd.prep.device_frame import DeviceFrame
+
+    st = LocalStore(lake)
+    cfg = TrainConfig(rfe_n_features=6, search_n_iter=2,
+                      search_space={"n_estimators": [5, 10], "max_depth": [2, 3], "learning_rate": [0.3]})
+    kw = dict(device="cpu", rfe_params=dict(n_estimators=5, max_depth=3))
+    ref = run_training(st.read_csv(CLEAN_DATA_KEY_TREE), cfg, local_dir=tmp_path / "pd", **kw)
+    frame = DeviceFrame.read_csv(st.get_bytes(CLEAN_DATA_KEY_TREE), "cpu", engine="arrow")
+    got = run_training(frame, cfg, local_dir=tmp_path / "dev", **kw)
+    assert got["hand_off"] == "device" and ref["hand_off"] == "pandas"
+    assert got["selected_features"] == ref["selected_features"]
+    assert got["best_params"] == ref["best_params"] and got["auc"] == ref["auc"]
+    assert (tmp_path / "dev" / BEST_MODEL_FILENAME).read_bytes() == (tmp_path / "pd" / BEST_MODEL_FILENAME).read_bytes()
+
+
 # ------------------------------------------------------------------------------ UI + automation
 def test_ui_payload_matches_api_schema():
     from cobalt_smart_lender_ai_amd.serve.app import SingleInput
@@ -214,3 +235,27 @@ def test_baseline_plumbing_config_runs_end_to_end():
     r = mod.plumbing_10k(rows=4_000, trees=20)
     assert r["rows_after_prep"] > 3_500 and r["features"] > 40
     assert r["logreg_auc"] > 0.85 and r["gbdt_cpu_auc"] > 0.85
+
+
+def test_rfe_repacked_fits_equal_masked_fits():
+    """RFE fits on the surviving columns only (repacked bins) grow exactly the trees of masked fits on
+    the full-width matrix: same boosters at every step, same support and ranking."""
+    from cobalt_smart_lender_ai_amd.select.rfe import rfe
+
+    rng = np.random.default_rng(4)
+    n, F = 6000, 12
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    X[:, 3] = np.round(X[:, 3])
+    X[rng.random((n, F)) < 0.05] = np.nan
+    y = (np.nan_to_num(X[:, 0]) + 0.5 * np.nan_to_num(X[:, 5]) - np.nan_to_num(X[:, 7]) + rng.normal(size=n) > 0)
+    y = y.astype(np.float32)
+    params = dict(n_estimators=8, max_depth=4, learning_rate=0.3, colsample_bytree=0.7, random_state=3)
+    names = [f"c{i}" for i in range(F)]
+    got, ref = [], []
+    a = rfe(X, y, params, n_features_to_select=5, step=2, device="cpu", feature_names=names,
+            step_score=lambda b, s: got.append(b.save_raw("ubj")))
+    b = rfe(X, y, params, n_features_to_select=5, step=2, device="cpu", feature_names=names, repack=False,
+            step_score=lambda b, s: ref.append(b.save_raw("ubj")))
+    assert got == ref and len(got) == 5
+    assert np.array_equal(a.support_, b.support_) and np.array_equal(a.ranking_, b.ranking_)
+    assert a.estimator_.save_raw("ubj") == b.estimator_.save_raw("ubj")
