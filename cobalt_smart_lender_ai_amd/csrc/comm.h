@@ -15,6 +15,23 @@ struct CobaltComm {
   IpcGroup* ipc;     // (kind 2)
 };
 
+constexpr int kMaxIpcRanks = 16;
+constexpr int kIpcStickyWord = 32;  // flag words: [0] = published epoch, [32] = sticky failure
+
+// One epoch of the IPC group as seen by a kernel that performs the exchange itself (the GBDT split
+// evaluation sums the ranks' histogram slots while it reads them): rank r's send slot of this
+// epoch, the device table of the ranks' flag words, this rank's flag word (+ sticky failure word at
+// [32]), the pinned host error word, the epoch and the wait deadline. n == 0: no fused exchange.
+struct IpcFusedView {
+  const char* slot[kMaxIpcRanks];
+  const unsigned* const* ftab;
+  unsigned* myflag;
+  unsigned* err_host;
+  unsigned epoch;
+  int n;
+  unsigned long long timeout;
+};
+
 // dtype: 0 int64, 1 uint8, 2 int32, 3 f32, 4 f64; op: 0 sum, 2 max, 3 min
 int loop_allreduce(CobaltComm* c, void* buf, int64_t count, int dtype, int op, hipStream_t stream);
 int loop_allgather(CobaltComm* c, const void* send, void* recv, int64_t count, int dtype, hipStream_t stream);
@@ -34,3 +51,5 @@ int ipc_zero_send(CobaltComm* c, int64_t bytes, hipStream_t stream);
 // One exchange: publish the send buffer, wait for every peer's, out = sum over ranks (rank order),
 // then zero the first `zero_bytes` of the following send buffer.
 int ipc_exchange(CobaltComm* c, void* out, int64_t count, int dtype, int op, int64_t zero_bytes, hipStream_t stream);
+// Start the next epoch for a kernel that exchanges by itself (publish + wait + sum inside it).
+int ipc_fused_view(CobaltComm* c, IpcFusedView* out);

@@ -24,6 +24,7 @@
 //    histogram slots per level, issued on the same stream through a native RCCL communicator.
 #include "common.h"
 #include "comm.h"
+#include "ipc_device.h"
 #include <math.h>
 #include <string.h>
 #include <stdlib.h>
@@ -159,6 +160,9 @@ struct GbdtDev {
   int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
   int64_t* hist_red;      // k_hist_reduce destination: nullptr = hist_b[parity]; the IPC group's send slot
                           // under IPC data parallelism (the exchange then writes the global sums to hist_b)
+  int64_t* zero_red;      // the next reduce destination, zeroed by k_grad* (root) / k_partition (next level):
+                          // nullptr = hist_b; the IPC group's next send slot under the fused exchange
+  IpcFusedView ipc;       // k_eval only: fused IPC exchange of this level (ipc.n == 0: hist_b is global)
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
   BlockStamp stamp_(d);
   extern __shared__ uint32_t s_tree[];
   {  // zero the root histogram slot
-    int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
+    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[0]);
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
          e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
 // root histogram slot zeroed (k_hist_reduce accumulates into it; k_grad does this on the normal path).
 __global__ __launch_bounds__(256) void k_tree_begin(GbdtDev d) {
   BlockStamp stamp_(d);
-  int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
+  int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[0]);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
        e += (int64_t)gridDim.x * blockDim.x)
     zp[e] = make_int4(0, 0, 0, 0);
@@ -864,7 +868,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries);
   float* s_leaf = reinterpret_cast<float*>(s_meta + d.max_nodes);
   {  // zero the root histogram slot (k_hist_reduce accumulates into it)
-    int4* zp = reinterpret_cast<int4*>(d.hist_b[0]);
+    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[0]);
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
          e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
@@ -1425,6 +1429,16 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int lane = lane_id();
   const int nw = (int)(blockDim.x / kWave);
   const uint8_t* fm = d.fmask + (int64_t)tree * d.F;
+  // Fused IPC exchange (data parallel over the one-shot IPC group): this level's histograms are the
+  // SUM of every rank's send slot, read here directly -- no separate all-reduce launch. Block (0, 0)
+  // publishes this rank's slot (complete: the reduce kernel before this one wrote it), every block
+  // waits for all ranks, then sums the ranks' cells as it loads them; the built child's global
+  // histogram is stored to hist_b for the next level's subtraction.
+  const bool fused = d.ipc.n > 0;
+  if (fused) {
+    if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(d.ipc.myflag, d.ipc.epoch);
+    if (!ipc_wait(d.ipc.ftab, d.ipc.n, d.ipc.myflag, d.ipc.epoch, d.ipc.err_host, d.ipc.timeout)) return;
+  }
   // Per-feature metadata (mask, bin count, compact offset, cut values) does not depend on the node:
   // it is loaded in the same round trip as the node record (unconditional, in-bounds loads).
   EvalFeat ef[2];
@@ -1449,7 +1463,24 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
   const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
-  const int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
+  int64_t rg = 0, rh = 0;
+  if (fused) {
+#pragma unroll
+    for (int r = 0; r < kMaxIpcRanks; ++r)
+      if (r < d.ipc.n) {
+        const int64_t* t = reinterpret_cast<const int64_t*>(d.ipc.slot[r]) + pair * SE + (int64_t)d.ncells * 2;
+        rg += t[0];
+        rh += t[1];
+      }
+    if (level == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // the global root totals (k_eval_finish reads them)
+      int64_t* tw = d.hist_b[parity] + (int64_t)d.ncells * 2;
+      tw[0] = rg;
+      tw[1] = rh;
+    }
+  } else {
+    rg = hb[(int64_t)d.ncells * 2];
+    rh = hb[(int64_t)d.ncells * 2 + 1];
+  }
   const int64_t ng = nodes[n].G, nh = nodes[n].H;
   // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
   const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
@@ -1491,11 +1522,40 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       cofs[s][c] = (uint32_t)(ef[s].off + min(c * kWave + lane, max(ef[s].nb - 1, 0))) * (uint32_t)sizeof(longlong2);
+  if (fused) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      v[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c]);
+      for (int c = 0; c < 4; ++c) v[s][c] = make_longlong2(0, 0);
+#pragma unroll
+    for (int r = 0; r < kMaxIpcRanks; ++r) {
+      if (r < d.ipc.n) {
+        const char* src = d.ipc.slot[r] + (int64_t)pair * SE * (int64_t)sizeof(int64_t);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const longlong2 t = *reinterpret_cast<const longlong2*>(src + cofs[s][c]);
+            v[s][c].x += t.x;
+            v[s][c].y += t.y;
+          }
+      }
+    }
+    if (built && active) {  // the built child's GLOBAL histogram, for the next level's subtraction
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c * kWave + lane < ef[s].nb)
+            *reinterpret_cast<longlong2*>(reinterpret_cast<char*>(const_cast<longlong2*>(hb2)) + cofs[s][c]) = v[s][c];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c]);
+  }
   if (!built) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -1875,7 +1935,7 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   __shared__ int32_t s_base[2];
   __shared__ int s_plan[5];
   {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
-    int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
+    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
     const int64_t nz = zero_next / 2;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
@@ -2004,7 +2064,7 @@ __global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, i
   __shared__ int64_t s_tot[2][16];
   static_assert(kPS <= 32 && kPS % 4 == 0, "step bit masks are 32-bit; hist pipeline of 4 steps");
   {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
-    int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
+    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
     const int64_t nz = zero_next / 2;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
@@ -2478,6 +2538,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // measures slower than the separate passes (COBALT_FUSED_PART=1)
   const bool env_fuse_part = getenv("COBALT_FUSED_PART") != nullptr && atoi(getenv("COBALT_FUSED_PART")) != 0;
   const bool fuse_part = fuse_root && env_fuse_part;
+  // IPC exchange fused into the split evaluation (k_eval publishes, waits and sums the ranks' slots
+  // itself: one launch per level fewer); COBALT_IPC_FUSED=0 keeps the separate exchange kernel
+  static const int env_ipc_fused = getenv("COBALT_IPC_FUSED") ? atoi(getenv("COBALT_IPC_FUSED")) : 1;
+  const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part;
+  d.ipc.n = 0;
+  d.zero_red = nullptr;
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
   static const int env_root = getenv("COBALT_ROOT_CHUNK") ? atoi(getenv("COBALT_ROOT_CHUNK")) : 0;
@@ -2504,6 +2570,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     d.prev_nodes = d.nodes_buf[(t + 1) & 1];
     d.stamps = stamp_tree(c, t) ? c->stamp_buf : nullptr;
     const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
+    // the root pass zeroes the root's reduce destination (under the fused exchange: the next send slot)
+    d.zero_red = ipc_fused ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
     if (sampled)
       GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
               stream, d);
@@ -2549,7 +2617,9 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           CK_LAUNCH();
         }
         int rc;
-        if (ipc) {  // the exchange also zeroes the next level's send slot (next tree's root after the last)
+        if (ipc_fused) {  // k_eval exchanges this epoch itself
+          rc = ipc_fused_view(cc, &d.ipc);
+        } else if (ipc) {  // the exchange also zeroes the next level's send slot (next tree's root after the last)
           const int64_t next_slots = level + 1 < D ? (1 << level) : 1;
           rc = ipc_exchange(cc, d.hist_b[parity], (int64_t)slots * d.slot_elems, 0, 0,
                             next_slots * d.slot_elems * (int64_t)sizeof(int64_t), stream);
@@ -2568,11 +2638,14 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       } else {
         GLAUNCH("k_eval", k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
       }
+      d.ipc.n = 0;
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
-        // (under IPC the exchange overwrites the next level's hist_b slots whole: nothing to zero)
-        const int64_t zero_next = ipc ? 0 : (int64_t)(1 << level) * d.slot_elems;
+        // (under the separate IPC exchange it overwrites the next level's hist_b slots whole: nothing to
+        // zero; under the fused one the next level's send slot is the reduce destination to zero)
+        const int64_t zero_next = (ipc && !ipc_fused) ? 0 : (int64_t)(1 << level) * d.slot_elems;
+        d.zero_red = ipc_fused ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
         const int pw = part_wide(d) ? 16 : 4;
         const int steps = ceil_div(chp, pw * kWave);  // <= kPartSteps (chunk_part's cap)
         if (pw == 16 && steps <= 4)
@@ -2592,6 +2665,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     }
     c->grown = t + 1;
     if (sampled) c->applied = t + 1;  // no training margins on a per-tree sample
+    d.zero_red = nullptr;
   }
   // archive the last tree of this call (later trees are archived by the next tree's k_grad)
   if (c->grown > t0) {

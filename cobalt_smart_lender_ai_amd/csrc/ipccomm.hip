@@ -22,6 +22,7 @@
 // multi-process configuration a 1-GPU box can run (RCCL refuses two ranks on one device).
 #include "comm.h"
 #include "common.h"
+#include "ipc_device.h"
 
 #include <string.h>
 #include <algorithm>
@@ -30,8 +31,6 @@
 using cobalt::kWave;
 
 namespace {
-
-constexpr int kMaxIpcRanks = 16;
 
 struct IpcPeers {  // by value: no pointer-table upload per exchange
   const char* x[kMaxIpcRanks];
@@ -43,42 +42,17 @@ __device__ __forceinline__ T combine(T a, T b) {
   return OP == 0 ? a + b : (OP == 2 ? (b > a ? b : a) : (b < a ? b : a));
 }
 
-// Flag words: [0] = this rank's last published epoch (read by the peers), [32] = sticky failure
-// (a wait of this rank timed out; later exchanges skip waiting). Both in the uncached allocation.
-constexpr int kStickyWord = 32;
+// Flag words: [0] = this rank's last published epoch (read by the peers), [kIpcStickyWord] = sticky
+// failure (a wait of this rank timed out; later exchanges skip waiting). Both in the uncached
+// allocation. The publish / wait protocol itself is ipc_publish / ipc_wait (ipc_device.h).
 
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void k_ipc_exchange(IpcPeers p, const unsigned* const* __restrict__ ftab, int n,
                                                       unsigned* myflag, unsigned epoch, int64_t slot_off,
                                                       int64_t count, T* __restrict__ out, int4* __restrict__ zero_dst,
                                                       int64_t zero_vec, unsigned* err_host, uint64_t timeout) {
-  __shared__ int ok;
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_store(myflag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (threadIdx.x < kWave) {
-    // wave 0 polls every peer's flag at once (lane r <- rank r): one round trip per poll, not n
-    const int lane = threadIdx.x;
-    int good = __hip_atomic_load(myflag + kStickyWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-    const unsigned* f = ftab[lane < n ? lane : 0];
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (good) {
-      const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (__ballot((int)(v - epoch) < 0) == 0) break;  // every rank has published this epoch
-      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-        good = 0;
-        if (lane == 0) {
-          __hip_atomic_store(myflag + kStickyWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: peers' slots are read fresh
-    if (lane == 0) ok = good;
-  }
-  __syncthreads();
-  if (!ok) return;
+  if (blockIdx.x == 0) ipc_publish(myflag, epoch);
+  if (!ipc_wait(ftab, n, myflag, epoch, err_host, timeout)) return;
   const T* src[kMaxIpcRanks];
 #pragma unroll
   for (int r = 0; r < kMaxIpcRanks; ++r) src[r] = reinterpret_cast<const T*>(p.x[r < n ? r : 0] + slot_off);
@@ -246,6 +220,21 @@ int ipc_exchange(CobaltComm* c, void* out, int64_t count, int dtype, int op, int
     default: launch_exchange<double>(op, grid, stream, g, e, off, count, out, zd, zv); break;
   }
   IPC_CK(hipGetLastError());
+  return 0;
+}
+
+int ipc_fused_view(CobaltComm* c, IpcFusedView* v) {
+  IpcGroup* g = c->ipc;
+  if (!g->ftab) { comm_set_error("ipc: exchange before cobalt_ipc_connect"); return -3; }
+  const unsigned e = ++g->epoch;
+  *v = IpcFusedView{};
+  for (int r = 0; r < g->n; ++r) v->slot[r] = g->peers.x[r] + (int64_t)(e & 1u) * g->cap;
+  v->ftab = g->ftab;
+  v->myflag = g->flags;
+  v->err_host = g->err_dev;
+  v->epoch = e;
+  v->n = g->n;
+  v->timeout = g->timeout_ticks;
   return 0;
 }
 

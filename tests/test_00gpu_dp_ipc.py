@@ -1,6 +1,7 @@
 """Data parallelism across PROCESSES on one GPU (the multi-rank configuration a 1-GPU box can run):
 2 and 3 ranks share cuda:0, bootstrap over gloo and all-reduce their per-level histograms through the
-IPC one-shot group (csrc/ipccomm.hip). The model must equal the 1-process fit byte for byte, and a
+IPC one-shot group (csrc/ipccomm.hip; the exchange fused into k_eval or as its own kernel). The model
+must equal the 1-process fit byte for byte, and a
 rank that dies mid-fit must make its peer fail fast through the group's deadline + the watchdog's
 abort instead of hanging.
 
@@ -27,8 +28,10 @@ def test_ipc_data_parallel_processes_equal_single_process():
     _check_clean(torch.cuda.is_initialized())
     ref = dp_check.run(1, ROWS)[0]
     assert ref["ok"], ref
-    for procs in (2, 3):
-        got = dp_check.run(procs, ROWS, timeout_s=400)
+    # the exchange fused into the split evaluation (default) with 2 and 3 ranks, and the separate
+    # exchange kernel (COBALT_IPC_FUSED=0)
+    for procs, env in ((2, None), (3, None), (2, {"COBALT_IPC_FUSED": "0"})):
+        got = dp_check.run(procs, ROWS, timeout_s=400, env=env)
         for g in got:
             assert g["ok"], g
             assert g["transport"] == "ipc"
