@@ -28,7 +28,7 @@ struct IpcFusedView {
   unsigned* myflag;
   unsigned* err_host;
   unsigned epoch;
-  int n;
+  int n, me;
   unsigned long long timeout;
 };
 

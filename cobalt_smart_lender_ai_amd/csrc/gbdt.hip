@@ -1437,7 +1437,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const bool fused = d.ipc.n > 0;
   if (fused) {
     if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(d.ipc.myflag, d.ipc.epoch);
-    if (!ipc_wait(d.ipc.ftab, d.ipc.n, d.ipc.myflag, d.ipc.epoch, d.ipc.err_host, d.ipc.timeout)) return;
+    if (!ipc_wait(d.ipc.ftab, d.ipc.n, d.ipc.me, d.ipc.myflag, d.ipc.epoch, d.ipc.err_host, d.ipc.timeout)) return;
   }
   // Per-feature metadata (mask, bin count, compact offset, cut values) does not depend on the node:
   // it is loaded in the same round trip as the node record (unconditional, in-bounds loads).
@@ -2540,7 +2540,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const bool fuse_part = fuse_root && env_fuse_part;
   // IPC exchange fused into the split evaluation (k_eval publishes, waits and sums the ranks' slots
   // itself: one launch per level fewer); COBALT_IPC_FUSED=0 keeps the separate exchange kernel
-  static const int env_ipc_fused = getenv("COBALT_IPC_FUSED") ? atoi(getenv("COBALT_IPC_FUSED")) : 1;
+  const int env_ipc_fused = getenv("COBALT_IPC_FUSED") ? atoi(getenv("COBALT_IPC_FUSED")) : 1;
   const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part;
   d.ipc.n = 0;
   d.zero_red = nullptr;

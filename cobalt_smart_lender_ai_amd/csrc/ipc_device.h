@@ -17,17 +17,19 @@ __device__ __forceinline__ void ipc_publish(unsigned* myflag, unsigned epoch) {
 // deadline; on timeout the sticky word and the pinned host error word are set (the host watchdog
 // aborts) and every later wait of this rank fails at once. A system-scope acquire follows, so the
 // block reads the peers' slots fresh. Returns the same value in every thread; call from all threads.
-__device__ __forceinline__ bool ipc_wait(const unsigned* const* ftab, int n, unsigned* myflag, unsigned epoch,
-                                         unsigned* err_host, unsigned long long timeout) {
+__device__ __forceinline__ bool ipc_wait(const unsigned* const* ftab, int n, int me, unsigned* myflag,
+                                         unsigned epoch, unsigned* err_host, unsigned long long timeout) {
   __shared__ int ipc_ok;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     int good = __hip_atomic_load(myflag + kIpcStickyWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-    const unsigned* f = ftab[lane < n ? lane : 0];
+    // this rank's own slot is complete by stream order: its lane does not wait on its own flag store
+    const bool peer = lane < n && lane != me;
+    const unsigned* f = ftab[peer ? lane : 0];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (good) {
-      const unsigned v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (__ballot((int)(v - epoch) < 0) == 0) break;  // every rank has published this epoch
+      const unsigned v = peer ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : epoch;
+      if (__ballot((int)(v - epoch) < 0) == 0) break;  // every peer has published this epoch
       if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
         good = 0;
         if (lane == 0) {

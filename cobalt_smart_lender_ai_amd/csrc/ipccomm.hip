@@ -48,11 +48,11 @@ __device__ __forceinline__ T combine(T a, T b) {
 
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void k_ipc_exchange(IpcPeers p, const unsigned* const* __restrict__ ftab, int n,
-                                                      unsigned* myflag, unsigned epoch, int64_t slot_off,
+                                                      int me, unsigned* myflag, unsigned epoch, int64_t slot_off,
                                                       int64_t count, T* __restrict__ out, int4* __restrict__ zero_dst,
                                                       int64_t zero_vec, unsigned* err_host, uint64_t timeout) {
   if (blockIdx.x == 0) ipc_publish(myflag, epoch);
-  if (!ipc_wait(ftab, n, myflag, epoch, err_host, timeout)) return;
+  if (!ipc_wait(ftab, n, me, myflag, epoch, err_host, timeout)) return;
   const T* src[kMaxIpcRanks];
 #pragma unroll
   for (int r = 0; r < kMaxIpcRanks; ++r) src[r] = reinterpret_cast<const T*>(p.x[r < n ? r : 0] + slot_off);
@@ -189,7 +189,7 @@ static void launch_exchange(int op, dim3 grid, hipStream_t s, const IpcGroup* g,
                             int64_t count, void* out, int4* zd, int64_t zv) {
   T* o = static_cast<T*>(out);
 #define IPC_LAUNCH(OPC)                                                                                       \
-  hipLaunchKernelGGL((k_ipc_exchange<T, OPC>), grid, dim3(256), 0, s, g->peers, g->ftab, g->n, g->flags, epoch, \
+  hipLaunchKernelGGL((k_ipc_exchange<T, OPC>), grid, dim3(256), 0, s, g->peers, g->ftab, g->n, g->rank, g->flags, epoch, \
                      off, count, o, zd, zv, g->err_dev, g->timeout_ticks)
   if (op == 0) IPC_LAUNCH(0);
   else if (op == 2) IPC_LAUNCH(2);
@@ -234,6 +234,7 @@ int ipc_fused_view(CobaltComm* c, IpcFusedView* v) {
   v->err_host = g->err_dev;
   v->epoch = e;
   v->n = g->n;
+  v->me = g->rank;
   v->timeout = g->timeout_ticks;
   return 0;
 }
