@@ -44,6 +44,8 @@ def main() -> None:
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--profile-fit", action="store_true", help="print per-phase timings to stderr")
+    ap.add_argument("--sketch-rows", type=int, default=1 << 18,
+                    help="rows of the quantile-sketch sample; 0 = every row (full-data sketch)")
     a = ap.parse_args()
 
     from cobalt_smart_lender_ai_amd.dataio import synth
@@ -66,7 +68,7 @@ def main() -> None:
     spw = (n_global - pos) / pos
     params = gbdt.GBDTParams(n_estimators=a.trees, max_depth=a.depth, learning_rate=0.05, gamma=5.0,
                              reg_lambda=1.0, min_child_weight=1.0, max_bin=256, scale_pos_weight=spw,
-                             random_state=78)
+                             random_state=78, sketch_rows=a.sketch_rows or None)
 
     def fit():
         rep = gbdt.FitReport(sync_phases=a.profile_fit)
@@ -132,6 +134,7 @@ def main() -> None:
                 "max_depth": a.depth,
             },
             "rows_global": n_global,
+            "sketch_rows": a.sketch_rows or "all",
             "dp_transport": ctx.transport if world > 1 else None,
             "auc": None if auc is None else round(auc, 5),
             "test_rows": a.test_rows,

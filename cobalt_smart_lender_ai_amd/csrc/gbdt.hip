@@ -1138,50 +1138,70 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
       for (int u = 0; u < U; ++u) hist_add_rec32<FT4>(s_hist, hl, a[u], b2[u]);
     }
   } else {
-  const int nchunks = (ft + 7) >> 3;
-  for (int i0 = w.begin + threadIdx.x; i0 < w.end; i0 += U * B) {
-    int r[U];
-    uint64_t gp[U];
+    // Generic records (F > 24: the RFE stage's wide fits, or F <= 8): the tile's <= 32 bins are bytes
+    // [f0, f0 + 32) of the record (f0 % 16 == 0, pitch a multiple of 16) -> two 16-byte loads, plus the
+    // packed (g, h) pair at goff, issued together for U rows, with the next rows' ids prefetched one
+    // iteration ahead (the 32-byte path's pipeline): one memory round trip per iteration instead of a
+    // dependent ridx -> (g, h) -> chunk-by-chunk chain. Tile metadata is uniform (SGPRs); a masked or
+    // padding feature is skipped by a scalar branch (no trash-cell atomics).
+    constexpr int UW = 2;  // rows in flight per thread (4 needs more VGPRs than 6 waves / SIMD allow)
+    const bool lo_ok = f0 + 16 <= d.stride, hi_ok = f0 + 32 <= d.stride;  // block-uniform
+    uint32_t fmv[32];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * B;
-      r[u] = i < w.end ? (identity ? i : rix[i]) : -1;
+    for (int fl = 0; fl < 32; ++fl) fmv[fl] = fl < ft ? hist_meta_of(s_fm, fl) : (3u << 16);
+    const int ilast = max(w.end - 1, w.begin);
+    int rn[UW];
+#pragma unroll
+    for (int u = 0; u < UW; ++u) {
+      const int i = w.begin + threadIdx.x + u * B;
+      const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
+      rn[u] = i < w.end ? rv : -1;
     }
+    char* base = reinterpret_cast<char*>(s_hist);
+    for (int i0 = w.begin + threadIdx.x; i0 < w.end; i0 += UW * B) {
+      int r[UW];
+      uint4 a[UW], b[UW];
+      uint64_t gp[UW];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      gp[u] = r[u] >= 0 ? *reinterpret_cast<const uint64_t*>(d.bins + (int64_t)r[u] * d.stride + d.goff) : 0ull;
-      tg += (int64_t)(int32_t)(uint32_t)(gp[u] >> 32);
-      th += (int64_t)(uint32_t)gp[u];
-    }
-    for (int c = 0; c < nchunks; ++c) {
-      uint32_t lo[U], hi[U];
+      for (int u = 0; u < UW; ++u) r[u] = rn[u];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int rr = r[u] >= 0 ? r[u] : r[0];
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(d.bins + (int64_t)rr * d.stride + f0 + c * 8);
-        lo[u] = row[0];
-        hi[u] = (c * 8 + 4 < ft) ? row[1] : 0xFFFFFFFFu;
+      for (int u = 0; u < UW; ++u) {
+        const uint8_t* rec = d.bins + (int64_t)(r[u] >= 0 ? r[u] : r[0]) * d.stride;
+        const uint4* t = reinterpret_cast<const uint4*>(rec + f0);
+        a[u] = lo_ok ? t[0] : make_uint4(0, 0, 0, 0);
+        b[u] = hi_ok ? t[1] : make_uint4(0, 0, 0, 0);
+        gp[u] = *reinterpret_cast<const uint64_t*>(rec + d.goff);
       }
-      const uint32_t fbc = (uint32_t)(fbits >> (c * 8)) & 0xFFu;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if ((fbc >> k) & 1u) {
-          // as hist_add_rec32: the missing code clamps to the feature's unread cell nbins
-          const uint32_t m = hist_meta_of(s_fm, c * 8 + k);
-          const uint32_t nb = m & 0xffffu, sh3 = m >> 16;
-          const uint32_t lb8 = ((uint32_t)((c * 8 + k) * kMaxBins) + (lane & ((1u << (sh3 - 3)) - 1u))) * 8u;
+      for (int u = 0; u < UW; ++u) {
+        const int i = i0 + UW * B + u * B;
+        const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
+        rn[u] = i < w.end ? rv : -1;
+      }
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const uint32_t b = ((k < 4 ? lo[u] : hi[u]) >> (8 * (k & 3))) & 0xffu;
-            const uint32_t off = lb8 + (min(b, nb) << sh3);
-            if (d.ablate == 1) tg += off; else
-            atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_hist) + off),
-                      (unsigned long long)gp[u]);
-          }
+      for (int u = 0; u < UW; ++u) {
+        if (r[u] < 0) gp[u] = 0ull;
+        tg += (int64_t)(int32_t)(uint32_t)(gp[u] >> 32);
+        th += (int64_t)(uint32_t)gp[u];
+      }
+#pragma unroll
+      for (int fl = 0; fl < 32; ++fl) {
+        const uint32_t m = fmv[fl];
+        const uint32_t nb = m & 0xffffu, sh3 = m >> 16;
+        if (nb == 0) continue;  // uniform: masked by colsample, or past the tile
+        // as hist_add_rec32: the missing code clamps to the feature's unread cell nbins
+        const uint32_t lb8 = ((uint32_t)(fl * kMaxBins) + (lane & ((1u << (sh3 - 3)) - 1u))) * 8u;
+        const int q = fl >> 2;
+#pragma unroll
+        for (int u = 0; u < UW; ++u) {
+          const uint32_t word = q == 0 ? a[u].x : q == 1 ? a[u].y : q == 2 ? a[u].z : q == 3 ? a[u].w
+                              : q == 4 ? b[u].x : q == 5 ? b[u].y : q == 6 ? b[u].z : b[u].w;
+          const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
+          atomicAdd(reinterpret_cast<unsigned long long*>(base + lb8 + (min(bb, nb) << sh3)),
+                    (unsigned long long)gp[u]);
         }
       }
     }
-  }
   }
   __syncthreads();
   stamp_.probe(3);
