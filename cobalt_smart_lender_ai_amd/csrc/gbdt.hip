@@ -313,14 +313,17 @@ __device__ __forceinline__ void stage_tree(const GbdtDev& d, const Node* tr, uin
   }
 }
 
-// Leaf of row `r` in a staged tree, walking the bins exactly like the partition step does.
-__device__ __forceinline__ float tree_leaf(const GbdtDev& d, int64_t r, const uint32_t* s_meta, const float* s_leaf) {
-  const uint8_t* row = d.bins + r * d.stride;
+// Leaf of row i in a staged tree (the partition step's routing), walked over the FEATURE-MAJOR bins:
+// row i's bin of feature f is binsT[f][i], so the lanes of a wave (consecutive rows) read consecutive
+// bytes of each column they visit -- a coalesced load per level
+// while the lanes share a node, instead of one record line per lane (wide records are 48-128 bytes).
+__device__ __forceinline__ float tree_leaf_T(const GbdtDev& d, int64_t i, const uint32_t* s_meta,
+                                             const float* s_leaf) {
   int n = 0;
   uint32_t m = s_meta[0];
   while (m & (1u << 25)) {
     const int f = m & 0xFFFF;
-    const uint32_t b = row[f];
+    const uint32_t b = d.binsT[(int64_t)f * d.ldt + i];
     const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
     n = 2 * n + (left ? 1 : 2);
     m = s_meta[n];
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
         }
         mf += s_leaf[n];
       } else {
-        mf += tree_leaf(d, i, s_meta, s_leaf);
+        mf += tree_leaf_T(d, i, s_meta, s_leaf);
       }
       d.margin[i] = mf;
     }
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(256) void k_apply_tree(GbdtDev d, int t) {
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n;
        i += (int64_t)gridDim.x * blockDim.x)
-    d.margin[i] += tree_leaf(d, i, s_meta, s_leaf);
+    d.margin[i] += tree_leaf_T(d, i, s_meta, s_leaf);
 }
 
 // Start of a tree grown from precomputed gradients (external-memory path): node-table reset and the
