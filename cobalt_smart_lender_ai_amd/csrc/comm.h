@@ -18,16 +18,16 @@ struct CobaltComm {
 constexpr int kMaxIpcRanks = 16;
 constexpr int kIpcStickyWord = 32;  // flag words: [0] = published epoch, [32] = sticky failure
 
-// One epoch of the IPC group as seen by a kernel that performs the exchange itself (the GBDT split
-// evaluation sums the ranks' histogram slots while it reads them): rank r's send slot of this
-// epoch, the device table of the ranks' flag words, this rank's flag word (+ sticky failure word at
-// [32]), the pinned host error word, the epoch and the wait deadline. n == 0: no fused exchange.
+// The IPC group as seen by a kernel that performs the exchange itself (the GBDT split evaluation sums
+// the ranks' histogram slots while it reads them), for one slot parity: rank r's send slot, the device
+// table of the ranks' flag words, this rank's flag word (+ sticky failure word), the pinned host error
+// word and the wait deadline. Two of them (parity 0 / 1) live in device memory for the group's
+// lifetime, so a kernel takes one pointer + the epoch instead of a per-launch copy.
 struct IpcFusedView {
   const char* slot[kMaxIpcRanks];
   const unsigned* const* ftab;
   unsigned* myflag;
   unsigned* err_host;
-  unsigned epoch;
   int n, me;
   unsigned long long timeout;
 };
@@ -51,5 +51,7 @@ int ipc_zero_send(CobaltComm* c, int64_t bytes, hipStream_t stream);
 // One exchange: publish the send buffer, wait for every peer's, out = sum over ranks (rank order),
 // then zero the first `zero_bytes` of the following send buffer.
 int ipc_exchange(CobaltComm* c, void* out, int64_t count, int dtype, int op, int64_t zero_bytes, hipStream_t stream);
-// Start the next epoch for a kernel that exchanges by itself (publish + wait + sum inside it).
-int ipc_fused_view(CobaltComm* c, IpcFusedView* out);
+// Start the next epoch for a kernel that exchanges by itself (publish + wait + sum inside it): returns
+// the epoch; the kernel reads ipc_device_views(c)[epoch & 1].
+unsigned ipc_next_epoch(CobaltComm* c);
+const IpcFusedView* ipc_device_views(CobaltComm* c);

@@ -162,7 +162,8 @@ struct GbdtDev {
                           // under IPC data parallelism (the exchange then writes the global sums to hist_b)
   int64_t* zero_red;      // the next reduce destination, zeroed by k_grad* (root) / k_partition (next level):
                           // nullptr = hist_b; the IPC group's next send slot under the fused exchange
-  IpcFusedView ipc;       // k_eval only: fused IPC exchange of this level (ipc.n == 0: hist_b is global)
+  const IpcFusedView* ipcv;  // fused IPC exchange: the group's device views (per slot parity) ...
+  unsigned ipc_epoch;        // ... and this level's epoch (k_eval only; 0 = hist_b already holds global sums)
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
@@ -1455,13 +1456,11 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   // Fused IPC exchange (data parallel over the one-shot IPC group): this level's histograms are the
   // SUM of every rank's send slot, read here directly -- no separate all-reduce launch. Block (0, 0)
   // publishes this rank's slot (complete: the reduce kernel before this one wrote it), every block
-  // waits for all ranks, then sums the ranks' cells as it loads them; the built child's global
-  // histogram is stored to hist_b for the next level's subtraction.
-  const bool fused = d.ipc.n > 0;
-  if (fused) {
-    if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(d.ipc.myflag, d.ipc.epoch);
-    if (!ipc_wait(d.ipc.ftab, d.ipc.n, d.ipc.me, d.ipc.myflag, d.ipc.epoch, d.ipc.err_host, d.ipc.timeout)) return;
-  }
+  // waits for all ranks (after issuing its node-record loads, which do not depend on the exchange),
+  // then sums the ranks' cells as it loads them; the built child's global histogram is stored to
+  // hist_b for the next level's subtraction.
+  const bool fused = d.ipc_epoch != 0;
+  const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
   // Per-feature metadata (mask, bin count, compact offset, cut values) does not depend on the node:
   // it is loaded in the same round trip as the node record (unconditional, in-bounds loads).
   EvalFeat ef[2];
@@ -1486,12 +1485,17 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
   const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
+  const int64_t ng = nodes[n].G, nh = nodes[n].H;
   int64_t rg = 0, rh = 0;
+  int ipc_n = 0;
   if (fused) {
+    if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
+    if (!ipc_wait(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout)) return;
+    ipc_n = __builtin_amdgcn_readfirstlane(iv->n);
 #pragma unroll
     for (int r = 0; r < kMaxIpcRanks; ++r)
-      if (r < d.ipc.n) {
-        const int64_t* t = reinterpret_cast<const int64_t*>(d.ipc.slot[r]) + pair * SE + (int64_t)d.ncells * 2;
+      if (r < ipc_n) {
+        const int64_t* t = reinterpret_cast<const int64_t*>(iv->slot[r]) + pair * SE + (int64_t)d.ncells * 2;
         rg += t[0];
         rh += t[1];
       }
@@ -1504,7 +1508,6 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     rg = hb[(int64_t)d.ncells * 2];
     rh = hb[(int64_t)d.ncells * 2 + 1];
   }
-  const int64_t ng = nodes[n].G, nh = nodes[n].H;
   // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
   const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
   const int pbuild = level > 0 ? pbuild_raw : 1;
@@ -1552,8 +1555,8 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       for (int c = 0; c < 4; ++c) v[s][c] = make_longlong2(0, 0);
 #pragma unroll
     for (int r = 0; r < kMaxIpcRanks; ++r) {
-      if (r < d.ipc.n) {
-        const char* src = d.ipc.slot[r] + (int64_t)pair * SE * (int64_t)sizeof(int64_t);
+      if (r < ipc_n) {
+        const char* src = iv->slot[r] + (int64_t)pair * SE * (int64_t)sizeof(int64_t);
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -2565,7 +2568,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // itself: one launch per level fewer); COBALT_IPC_FUSED=0 keeps the separate exchange kernel
   const int env_ipc_fused = getenv("COBALT_IPC_FUSED") ? atoi(getenv("COBALT_IPC_FUSED")) : 1;
   const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part;
-  d.ipc.n = 0;
+  d.ipc_epoch = 0;
+  d.ipcv = ipc_fused ? ipc_device_views(cc) : nullptr;
   d.zero_red = nullptr;
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
@@ -2641,7 +2645,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         }
         int rc;
         if (ipc_fused) {  // k_eval exchanges this epoch itself
-          rc = ipc_fused_view(cc, &d.ipc);
+          d.ipc_epoch = ipc_next_epoch(cc);
+          rc = 0;
         } else if (ipc) {  // the exchange also zeroes the next level's send slot (next tree's root after the last)
           const int64_t next_slots = level + 1 < D ? (1 << level) : 1;
           rc = ipc_exchange(cc, d.hist_b[parity], (int64_t)slots * d.slot_elems, 0, 0,
@@ -2661,7 +2666,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       } else {
         GLAUNCH("k_eval", k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
       }
-      d.ipc.n = 0;
+      d.ipc_epoch = 0;
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);

@@ -92,6 +92,7 @@ struct IpcGroup {
   unsigned* err_dev = nullptr;
   IpcPeers peers{};
   const unsigned** ftab = nullptr;  // device copy of peers.flag (polled lane-parallel)
+  IpcFusedView* views = nullptr;    // device [2]: the group per slot parity (ipc_device_views)
   std::vector<void*> opened;
   unsigned epoch = 0;          // exchanges enqueued so far (identical on every rank)
   uint64_t timeout_ticks = 0;  // s_memrealtime ticks (100 MHz)
@@ -161,6 +162,18 @@ COBALT_API int cobalt_ipc_connect(void* comm, const void* all_handles) {
   }
   IPC_CK(hipMalloc((void**)&g->ftab, kMaxIpcRanks * sizeof(unsigned*)));
   IPC_CK(hipMemcpy(g->ftab, g->peers.flag, kMaxIpcRanks * sizeof(unsigned*), hipMemcpyHostToDevice));
+  IpcFusedView hv[2] = {};
+  for (int p = 0; p < 2; ++p) {
+    for (int r = 0; r < g->n; ++r) hv[p].slot[r] = g->peers.x[r] + (int64_t)p * g->cap;
+    hv[p].ftab = g->ftab;
+    hv[p].myflag = g->flags;
+    hv[p].err_host = g->err_dev;
+    hv[p].n = g->n;
+    hv[p].me = g->rank;
+    hv[p].timeout = g->timeout_ticks;
+  }
+  IPC_CK(hipMalloc((void**)&g->views, sizeof(hv)));
+  IPC_CK(hipMemcpy(g->views, hv, sizeof(hv), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -223,21 +236,9 @@ int ipc_exchange(CobaltComm* c, void* out, int64_t count, int dtype, int op, int
   return 0;
 }
 
-int ipc_fused_view(CobaltComm* c, IpcFusedView* v) {
-  IpcGroup* g = c->ipc;
-  if (!g->ftab) { comm_set_error("ipc: exchange before cobalt_ipc_connect"); return -3; }
-  const unsigned e = ++g->epoch;
-  *v = IpcFusedView{};
-  for (int r = 0; r < g->n; ++r) v->slot[r] = g->peers.x[r] + (int64_t)(e & 1u) * g->cap;
-  v->ftab = g->ftab;
-  v->myflag = g->flags;
-  v->err_host = g->err_dev;
-  v->epoch = e;
-  v->n = g->n;
-  v->me = g->rank;
-  v->timeout = g->timeout_ticks;
-  return 0;
-}
+unsigned ipc_next_epoch(CobaltComm* c) { return ++c->ipc->epoch; }
+
+const IpcFusedView* ipc_device_views(CobaltComm* c) { return c->ipc->views; }
 
 // In-place all-reduce of `buf` (generic path: the buffer is first copied into the send slot).
 int ipc_allreduce(CobaltComm* c, void* buf, int64_t count, int dtype, int op, hipStream_t stream) {
@@ -260,6 +261,7 @@ void ipc_release(CobaltComm* c) {
   if (g->xbuf) (void)hipFree(g->xbuf);
   if (g->flags) (void)hipFree(g->flags);
   if (g->ftab) (void)hipFree(g->ftab);
+  if (g->views) (void)hipFree(g->views);
   if (g->err_host) (void)hipHostFree(g->err_host);
   delete g;
   c->ipc = nullptr;
