@@ -158,12 +158,6 @@ struct GbdtDev {
   int2* layout;           // [F] histogram LDS layout: x = cell offset within tile, y = log2(copies)
   int32_t* tile_entries;  // [n_tiles] LDS cells per feature tile
   int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
-  int64_t* hist_red;      // k_hist_reduce destination: nullptr = hist_b[parity]; the IPC group's send slot
-                          // under IPC data parallelism (the exchange then writes the global sums to hist_b)
-  int64_t* zero_red;      // the next reduce destination, zeroed by k_grad* (root) / k_partition (next level):
-                          // nullptr = hist_b; the IPC group's next send slot under the fused exchange
-  const IpcFusedView* ipcv;  // fused IPC exchange: the group's device views (per slot parity) ...
-  unsigned ipc_epoch;        // ... and this level's epoch (k_eval only; 0 = hist_b already holds global sums)
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
@@ -184,6 +178,13 @@ struct GbdtDev {
   uint64_t* stamps;       // COBALT_STAMPS diagnostics: [launch][kStampBlocks][2] block {start, end} in 10 ns
                           // ticks; nullptr in normal runs and in unsampled trees
   int32_t seq;            // launch index into `stamps` (set by the host before every launch)
+  // data-parallel IPC exchange (appended: the single-GPU kernels' argument layout is unchanged)
+  int64_t* hist_red;      // k_hist_reduce destination: nullptr = hist_b[parity]; the IPC group's send slot
+                          // under IPC data parallelism (the exchange then writes the global sums to hist_b)
+  int64_t* zero_red;      // the next reduce destination, zeroed by k_grad* (root) / k_partition (next level):
+                          // nullptr = hist_b; the IPC group's next send slot under the fused exchange
+  const IpcFusedView* ipcv;  // fused IPC exchange: the group's device views (per slot parity) ...
+  unsigned ipc_epoch;        // ... and this level's epoch (k_eval only; 0 = hist_b already holds global sums)
 };
 
 // In-kernel timing (diagnostic switch COBALT_STAMPS, off by default): the block's first thread
@@ -1456,9 +1457,10 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   // Fused IPC exchange (data parallel over the one-shot IPC group): this level's histograms are the
   // SUM of every rank's send slot, read here directly -- no separate all-reduce launch. Block (0, 0)
   // publishes this rank's slot (complete: the reduce kernel before this one wrote it), every block
-  // waits for all ranks (after issuing its node-record loads, which do not depend on the exchange),
-  // then sums the ranks' cells as it loads them; the built child's global histogram is stored to
-  // hist_b for the next level's subtraction.
+  // waits for all ranks after issuing its node-record loads (they do not depend on the exchange), then
+  // sums the ranks' cells as it loads them; the built child's global histogram is stored to hist_b for
+  // the next level's subtraction. Without it the instruction stream is the single-GPU one: the hist_b
+  // loads below are unconditional and the exchange only overrides their results.
   const bool fused = d.ipc_epoch != 0;
   const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
   // Per-feature metadata (mask, bin count, compact offset, cut values) does not depend on the node:
@@ -1485,13 +1487,15 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
   const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
+  int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
   const int64_t ng = nodes[n].G, nh = nodes[n].H;
-  int64_t rg = 0, rh = 0;
   int ipc_n = 0;
   if (fused) {
     if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
     if (!ipc_wait(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout)) return;
     ipc_n = __builtin_amdgcn_readfirstlane(iv->n);
+    rg = 0;
+    rh = 0;
 #pragma unroll
     for (int r = 0; r < kMaxIpcRanks; ++r)
       if (r < ipc_n) {
@@ -1504,9 +1508,6 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       tw[0] = rg;
       tw[1] = rh;
     }
-  } else {
-    rg = hb[(int64_t)d.ncells * 2];
-    rh = hb[(int64_t)d.ncells * 2 + 1];
   }
   // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
   const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
@@ -1548,7 +1549,12 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       cofs[s][c] = (uint32_t)(ef[s].off + min(c * kWave + lane, max(ef[s].nb - 1, 0))) * (uint32_t)sizeof(longlong2);
-  if (fused) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      v[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c]);
+  if (fused) {  // the ranks' sum replaces the (local, unreduced) hist_b values
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1575,12 +1581,6 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
           if (c * kWave + lane < ef[s].nb)
             *reinterpret_cast<longlong2*>(reinterpret_cast<char*>(const_cast<longlong2*>(hb2)) + cofs[s][c]) = v[s][c];
     }
-  } else {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        v[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c]);
   }
   if (!built) {
 #pragma unroll
