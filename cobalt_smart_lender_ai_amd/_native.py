@@ -70,6 +70,7 @@ _SIGS: dict[str, tuple] = {
     "cobalt_ipc_create": (c_int, [c_int, c_int, c_int64, c_double, ctypes.POINTER(c_void_p), c_void_p]),
     "cobalt_ipc_connect": (c_int, [c_void_p, c_void_p]),
     "cobalt_ipc_epoch": (ctypes.c_uint, [c_void_p]),
+    "cobalt_ipc_set_timeout": (ctypes.c_int, [c_void_p, ctypes.c_double]),
     # loopcomm.hip
     "cobalt_comm_loop_group": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "cobalt_comm_loop_rank": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),

@@ -206,6 +206,10 @@ struct BlockStamp {
   __device__ __forceinline__ void probe(int k) {
     if (p && threadIdx.x == 0) p[1 + k] = __builtin_amdgcn_s_memrealtime();
   }
+  // the LAST wave's time at probe point k (every wave's lane 0 contributes)
+  __device__ __forceinline__ void probe_max(int k) {
+    if (p && (threadIdx.x & (kWave - 1)) == 0) atomicMax(p + 1 + k, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
   __device__ __forceinline__ ~BlockStamp() {
     if (p && (threadIdx.x & (kWave - 1)) == 0) atomicMax(p + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
@@ -1429,6 +1433,46 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
   }
 }
 
+// Fused exchange, phase A: the block's histogram cells [cb, cb + m - 1) and the totals cell (LDS slot
+// m - 1), summed over the NR ranks' send slots into LDS. Every cell's NR loads are in flight together
+// (one remote round trip per block instead of one per rank); `store`: the sums also go to hist_b
+// (the built child's global histogram, for the next level's subtraction), `store_tot`: the totals too.
+template <int NR>
+__device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pair_bytes, int cb, int m, int ncells,
+                                              longlong2* s_cells, longlong2* hbw, bool store, bool store_tot) {
+  const char* sp[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) sp[r] = iv->slot[r] + pair_bytes;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    const int cell = i < m - 1 ? cb + i : ncells;
+    longlong2 t[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) t[r] = *reinterpret_cast<const longlong2*>(sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2));
+    longlong2 acc = t[0];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+      acc.x += t[r].x;
+      acc.y += t[r].y;
+    }
+    s_cells[i] = acc;
+    if (i < m - 1 ? store : store_tot) hbw[cell] = acc;
+  }
+}
+
+__device__ __forceinline__ void ipc_sum_cells_n(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int m,
+                                                int ncells, longlong2* s_cells, longlong2* hbw, bool store,
+                                                bool store_tot) {
+  switch (nr) {
+#define IPC_SUM_CASE(K) \
+    case K: ipc_sum_cells<K>(iv, pair_bytes, cb, m, ncells, s_cells, hbw, store, store_tot); break;
+    IPC_SUM_CASE(1) IPC_SUM_CASE(2) IPC_SUM_CASE(3) IPC_SUM_CASE(4) IPC_SUM_CASE(5) IPC_SUM_CASE(6)
+    IPC_SUM_CASE(7) IPC_SUM_CASE(8) IPC_SUM_CASE(9) IPC_SUM_CASE(10) IPC_SUM_CASE(11) IPC_SUM_CASE(12)
+    IPC_SUM_CASE(13) IPC_SUM_CASE(14) IPC_SUM_CASE(15) IPC_SUM_CASE(16)
+#undef IPC_SUM_CASE
+    default: break;
+  }
+}
+
 // kGroups: the node's features are split over gridDim.y blocks of `fg` features each (one CU per
 // group instead of one per node: the fp64 gain scan of a wide node -- 106 features in the RFE stage --
 // is issue-bound on a single CU); each group writes its best candidate and k_eval_finish reduces them.
@@ -1439,8 +1483,22 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
 // cost every feature four) -- and each chunk is one coalesced 16-byte (g, h) load per lane. A chunk's
 // left sums are a DPP int64 wave scan plus the carry of the chunks before it. Candidates, keys and
 // tie-breaks are unchanged, so the trees are bit-identical.
-template <bool kGroups>
-__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg) {
+//
+// Without groups (one 1024-thread block per node) the feature -> wave assignment is the host's
+// eval_assignment table (asg*: slot 2 w + s = wave w's s-th feature, 8 bits each, 0xFF = none): the
+// fp64 candidate work is ceil(nb / 64) chunk steps per feature and the 16 waves share 4 SIMDs (wave w
+// on SIMD w mod 4), so the table balances chunk steps per SIMD, not per wave.
+//
+// kFused (data parallel over the one-shot IPC group): this level's histograms are the SUM of every
+// rank's send slot, read here -- no separate all-reduce launch. Block (0, 0) publishes this rank's slot
+// (complete: the reduce kernel before this one wrote it), every block waits for all ranks after issuing
+// its node-record loads (they do not depend on the exchange), sums its cells over the ranks into LDS
+// (ipc_sum_cells: dynamic LDS of (cells + 1) x 16 bytes) and reads them from there; the built child's
+// global histogram is stored to hist_b for the next level's subtraction. The single-GPU instantiation
+// (kFused = false) has none of it.
+template <bool kGroups, bool kFused>
+__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg, uint64_t asg0,
+                                               uint64_t asg1, uint64_t asg2, uint64_t asg3) {
   BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   const int fbeg = kGroups ? blockIdx.y * fg : 0;
@@ -1454,15 +1512,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int lane = lane_id();
   const int nw = (int)(blockDim.x / kWave);
   const uint8_t* fm = d.fmask + (int64_t)tree * d.F;
-  // Fused IPC exchange (data parallel over the one-shot IPC group): this level's histograms are the
-  // SUM of every rank's send slot, read here directly -- no separate all-reduce launch. Block (0, 0)
-  // publishes this rank's slot (complete: the reduce kernel before this one wrote it), every block
-  // waits for all ranks after issuing its node-record loads (they do not depend on the exchange), then
-  // sums the ranks' cells as it loads them; the built child's global histogram is stored to hist_b for
-  // the next level's subtraction. Without it the instruction stream is the single-GPU one: the hist_b
-  // loads below are unconditional and the exchange only overrides their results.
-  const bool fused = d.ipc_epoch != 0;
-  const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
+  extern __shared__ longlong2 s_cells[];  // kFused: the block's cells summed over the ranks
   // Per-feature metadata (mask, bin count, compact offset, cut values) does not depend on the node:
   // it is loaded in the same round trip as the node record (unconditional, in-bounds loads).
   EvalFeat ef[2];
@@ -1470,7 +1520,14 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       EvalFeat& e = ef[s];
-      e.f = fbase + s * nw;
+      if (kGroups) {
+        e.f = fbase + s * nw;
+      } else {
+        const int slot = __builtin_amdgcn_readfirstlane(wave_id() * 2 + s);
+        const uint64_t word = slot < 8 ? asg0 : slot < 16 ? asg1 : slot < 24 ? asg2 : asg3;
+        const int fi = (int)((word >> (8 * (slot & 7))) & 0xFFu);
+        e.f = fi == 0xFF ? fend : fi;
+      }
       const int fc = min(e.f, d.F - 1);
       const bool valid = e.f < fend;
       const uint8_t fmv = fm[fc];  // unconditional loads, masked after (no per-load branch)
@@ -1487,27 +1544,27 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
   const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
-  int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
+  int64_t rg = 0, rh = 0;
+  if (!kFused) {
+    rg = hb[(int64_t)d.ncells * 2];
+    rh = hb[(int64_t)d.ncells * 2 + 1];
+  }
   const int64_t ng = nodes[n].G, nh = nodes[n].H;
-  int ipc_n = 0;
-  if (fused) {
+  int cb = 0;  // kFused: the block's first cell (LDS slot 0)
+  if (kFused) {
+    const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
+    cb = kGroups ? d.hoff[fbeg] : 0;
+    const int ce = kGroups ? d.hoff[fend] : d.ncells;
     if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
     if (!ipc_wait(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout)) return;
-    ipc_n = __builtin_amdgcn_readfirstlane(iv->n);
-    rg = 0;
-    rh = 0;
-#pragma unroll
-    for (int r = 0; r < kMaxIpcRanks; ++r)
-      if (r < ipc_n) {
-        const int64_t* t = reinterpret_cast<const int64_t*>(iv->slot[r]) + pair * SE + (int64_t)d.ncells * 2;
-        rg += t[0];
-        rh += t[1];
-      }
-    if (level == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // the global root totals (k_eval_finish reads them)
-      int64_t* tw = d.hist_b[parity] + (int64_t)d.ncells * 2;
-      tw[0] = rg;
-      tw[1] = rh;
-    }
+    // the global root totals are stored at level 0 (k_eval_finish reads them)
+    ipc_sum_cells_n(__builtin_amdgcn_readfirstlane(iv->n), iv, (int64_t)pair * SE * (int64_t)sizeof(int64_t), cb,
+                    ce - cb + 1, d.ncells, s_cells, reinterpret_cast<longlong2*>(d.hist_b[parity] + pair * SE),
+                    built && status == kActive, level == 0 && blockIdx.y == 0);
+    __syncthreads();
+    const longlong2 tot = s_cells[ce - cb];
+    rg = tot.x;
+    rh = tot.y;
   }
   // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
   const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
@@ -1518,6 +1575,12 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   stamp_.probe(1);
   __shared__ Cand s_best[16];
   __shared__ float s_cut[16];
+  __shared__ int s_nb[32];  // !kGroups: bin count per feature, for the winner's bin (no global load after the reduction)
+  if (!kGroups && lane == 0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (ef[s].f < 32) s_nb[ef[s].f] = ef[s].nb;
+  }
   const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
   const int64_t* parent = hb;  // the sibling's parent histogram (unused when this child was built)
   if (!built) {
@@ -1549,45 +1612,31 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       cofs[s][c] = (uint32_t)(ef[s].off + min(c * kWave + lane, max(ef[s].nb - 1, 0))) * (uint32_t)sizeof(longlong2);
+  // Only lanes holding a real bin of an evaluated feature load (exec-masked): the CU's address path
+  // costs per active lane, and unmasked, the 16 waves' 2 x 4 chunks (+ the parent's) were 256 full
+  // 1 KB load instructions per block for ~26 chunks of real bins -- ~2 us per level at 1M rows.
+  bool ld[2][4];
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      v[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c]);
-  if (fused) {  // the ranks' sum replaces the (local, unreduced) hist_b values
+    for (int c = 0; c < 4; ++c) ld[s][c] = ef[s].on && c * kWave + lane < ef[s].nb;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) v[s][c] = make_longlong2(0, 0);
-#pragma unroll
-    for (int r = 0; r < kMaxIpcRanks; ++r) {
-      if (r < ipc_n) {
-        const char* src = iv->slot[r] + (int64_t)pair * SE * (int64_t)sizeof(int64_t);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const longlong2 t = *reinterpret_cast<const longlong2*>(src + cofs[s][c]);
-            v[s][c].x += t.x;
-            v[s][c].y += t.y;
-          }
-      }
+    for (int c = 0; c < 4; ++c) {
+      if (kFused)  // the ranks' sums, from LDS
+        v[s][c] = ld[s][c] ? s_cells[cofs[s][c] / (uint32_t)sizeof(longlong2) - (uint32_t)cb] : make_longlong2(0, 0);
+      else
+        v[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c])
+                           : make_longlong2(0, 0);
     }
-    if (built && active) {  // the built child's GLOBAL histogram, for the next level's subtraction
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (c * kWave + lane < ef[s].nb)
-            *reinterpret_cast<longlong2*>(reinterpret_cast<char*>(const_cast<longlong2*>(hb2)) + cofs[s][c]) = v[s][c];
-    }
-  }
   if (!built) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        pv[s][c] = *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(pa2) + cofs[s][c]);
+        pv[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(pa2) + cofs[s][c])
+                            : make_longlong2(0, 0);
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1709,7 +1758,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     o.hl = best.hl;
     return;
   }
-  eval_finalize(d, level, n, G, H, best, best_cut);
+  eval_finalize(d, level, n, G, H, best, best_cut, best.key != 0x7fffffff ? s_nb[(best.key >> 10) & 31] : 0);
   stamp_.probe(4);
 }
 
@@ -2226,6 +2275,9 @@ struct GbdtCtx {
   int applied = 0;         // number of leading trees whose leaves are already in the margins
   int grown = 0;            // number of trees grown so far
   std::vector<void*> allocs;
+  // k_eval<false> feature -> (wave, slot) table: 32 slots of 8 bits (0xFF = empty), see eval_assignment
+  uint64_t eval_asg[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  std::vector<int32_t> hoff_h;  // host copy of d.hoff (sizes k_eval's fused-exchange LDS)
   // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
   const char* stamp_path = nullptr;
   int stamp_cap = 0;
@@ -2456,6 +2508,50 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   return 0;
 }
 
+// Feature -> (wave, slot) table of k_eval<false> (F <= 32; 16 waves x 2 slots). Longest-processing-
+// time first over chunk steps (ceil(nb / 64), 1..4): each feature goes to the least-loaded SIMD that
+// still has a free slot (wave w runs on SIMD w mod 4), on its least-loaded wave. The 20 deployed
+// features by index order put 11 chunk steps on one SIMD (mean 6.5); the table evens that out. The
+// candidate keys, not the wave, order ties: the trees do not depend on the table.
+// COBALT_EVAL_ASSIGN=0 restores the index-order assignment (feature f on wave f mod 16, slot f / 16).
+static void eval_assignment(const std::vector<int32_t>& nb, uint64_t out[4]) {
+  const int F = (int)nb.size();
+  uint8_t slot[32];
+  memset(slot, 0xFF, sizeof(slot));
+  const bool lpt = !(getenv("COBALT_EVAL_ASSIGN") && atoi(getenv("COBALT_EVAL_ASSIGN")) == 0);
+  if (F <= 32 && !lpt) {
+    for (int f = 0; f < F; ++f) slot[(f % 16) * 2 + f / 16] = (uint8_t)f;
+  } else if (F <= 32) {
+    std::vector<int> order(F), steps(F);
+    for (int f = 0; f < F; ++f) {
+      order[f] = f;
+      steps[f] = std::max(1, ceil_div(std::max(1, std::min(256, nb[f])), kWave));
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return steps[a] > steps[b]; });
+    int simd_load[4] = {0, 0, 0, 0}, wave_load[16] = {0}, wave_cnt[16] = {0};
+    for (int f : order) {
+      int bs = -1;
+      for (int s = 0; s < 4; ++s) {
+        const bool free = wave_cnt[s] < 2 || wave_cnt[s + 4] < 2 || wave_cnt[s + 8] < 2 || wave_cnt[s + 12] < 2;
+        if (free && (bs < 0 || simd_load[s] < simd_load[bs])) bs = s;
+      }
+      int bw = -1;
+      for (int w = bs; w < 16; w += 4)
+        if (wave_cnt[w] < 2 && (bw < 0 || wave_load[w] < wave_load[bw] ||
+                                (wave_load[w] == wave_load[bw] && wave_cnt[w] < wave_cnt[bw])))
+          bw = w;
+      slot[bw * 2 + wave_cnt[bw]++] = (uint8_t)f;
+      simd_load[bs] += steps[f];
+      wave_load[bw] += steps[f];
+    }
+  }
+  for (int k = 0; k < 4; ++k) {
+    uint64_t w = 0;
+    for (int j = 0; j < 8; ++j) w |= (uint64_t)slot[k * 8 + j] << (8 * j);
+    out[k] = w;
+  }
+}
+
 COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT, const float* cuts,
                                     const int32_t* nbins, const float* label, const float* weight,
                                     float* margin, const uint8_t* fmask) {
@@ -2499,6 +2595,8 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   std::vector<int32_t> hoff(F + 1, 0);
   for (int f = 0; f < F; ++f) hoff[f + 1] = hoff[f] + std::max(1, std::min(256, nb[f]));
   CK(hipMemcpy(c->d.hoff, hoff.data(), (F + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->hoff_h = hoff;
+  eval_assignment(nb, c->eval_asg);
   c->d.ncells = hoff[F];
   c->d.slot_elems = (int64_t)(hoff[F] + 1) * 2;
   CK(hipMemcpy(c->d.tile_entries, ent.data(), ntiles * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -2567,7 +2665,15 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // IPC exchange fused into the split evaluation (k_eval publishes, waits and sums the ranks' slots
   // itself: one launch per level fewer); COBALT_IPC_FUSED=0 keeps the separate exchange kernel
   const int env_ipc_fused = getenv("COBALT_IPC_FUSED") ? atoi(getenv("COBALT_IPC_FUSED")) : 1;
-  const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part;
+  // LDS of the fused k_eval: the block's cells (+ the totals cell) summed over the ranks
+  int fused_cells = c->d.ncells;
+  if (eval_fg > 0) {
+    fused_cells = 0;
+    for (int f0 = 0; f0 < d.F; f0 += eval_fg)
+      fused_cells = std::max(fused_cells, c->hoff_h[std::min(d.F, f0 + eval_fg)] - c->hoff_h[f0]);
+  }
+  const size_t fused_lds = (size_t)(fused_cells + 1) * 16;
+  const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part && fused_lds <= 65536;
   d.ipc_epoch = 0;
   d.ipcv = ipc_fused ? ipc_device_views(cc) : nullptr;
   d.zero_red = nullptr;
@@ -2658,13 +2764,22 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       }
       if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
         const int ng = ceil_div(d.F, eval_fg);
-        GLAUNCH("k_eval", k_eval<true>, dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream, d, level,
-                parity, t, eval_fg);
+        if (d.ipc_epoch)
+          GLAUNCH("k_eval", (k_eval<true, true>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), fused_lds,
+                  stream, d, level, parity, t, eval_fg, 0ull, 0ull, 0ull, 0ull);
+        else
+          GLAUNCH("k_eval", (k_eval<true, false>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream,
+                  d, level, parity, t, eval_fg, 0ull, 0ull, 0ull, 0ull);
         GLAUNCH("k_eval_finish", k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
       } else if (eval_compact) {
         GLAUNCH("k_eval", k_eval_compact, dim3(1 << level), dim3(kEvalThreads), 0, stream, d, level, parity, t);
       } else {
-        GLAUNCH("k_eval", k_eval<false>, dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F);
+        if (d.ipc_epoch)
+          GLAUNCH("k_eval", (k_eval<false, true>), dim3(1 << level), dim3(1024), fused_lds, stream, d, level, parity,
+                  t, d.F, c->eval_asg[0], c->eval_asg[1], c->eval_asg[2], c->eval_asg[3]);
+        else
+          GLAUNCH("k_eval", (k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F,
+                  c->eval_asg[0], c->eval_asg[1], c->eval_asg[2], c->eval_asg[3]);
       }
       d.ipc_epoch = 0;
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed

@@ -177,6 +177,22 @@ COBALT_API int cobalt_ipc_connect(void* comm, const void* all_handles) {
   return 0;
 }
 
+// Change the wait deadline (host + device views). Call with no exchange in flight (device idle): the
+// connect self-test runs under a short deadline, the training under the long one.
+COBALT_API int cobalt_ipc_set_timeout(void* comm, double timeout_s) {
+  CobaltComm* c = static_cast<CobaltComm*>(comm);
+  if (!c || c->kind != 2) return -3;
+  IpcGroup* g = c->ipc;
+  g->timeout_ticks = (uint64_t)(std::max(0.001, timeout_s) * 1e8);
+  if (g->views) {
+    IpcFusedView hv[2];
+    IPC_CK(hipMemcpy(hv, g->views, sizeof(hv), hipMemcpyDeviceToHost));
+    hv[0].timeout = hv[1].timeout = g->timeout_ticks;
+    IPC_CK(hipMemcpy(g->views, hv, sizeof(hv), hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
 void* ipc_send_buffer(CobaltComm* c) {
   IpcGroup* g = c->ipc;
   return g->xbuf + (int64_t)((g->epoch + 1) & 1u) * g->cap;

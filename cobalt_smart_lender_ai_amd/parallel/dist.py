@@ -189,7 +189,10 @@ def create_ipc_comm(ctx: DistContext) -> int:
     nb = int(lib.cobalt_ipc_handle_bytes())
     mine = (ctypes.c_uint8 * nb)()
     h = ctypes.c_void_p()
-    rc = lib.cobalt_ipc_create(ctx.rank, ctx.world, ipc_slot_bytes(), ipc_timeout_s(), ctypes.byref(h), mine)
+    # the connect self-test runs under a short deadline (the ranks enter it together, right after the
+    # handle all-gather): a group whose peer mappings do not work fails in seconds, not minutes
+    connect_s = min(ipc_timeout_s(), float(os.environ.get("COBALT_IPC_CONNECT_TIMEOUT_S", "30")))
+    rc = lib.cobalt_ipc_create(ctx.rank, ctx.world, ipc_slot_bytes(), connect_s, ctypes.byref(h), mine)
     if rc != 0:
         raise RuntimeError(f"cobalt_ipc_create failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
     try:
@@ -206,6 +209,8 @@ def create_ipc_comm(ctx: DistContext) -> int:
         if rc != 0:
             raise RuntimeError(f"cobalt_ipc_connect failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
         _ipc_selftest(ctx, int(h.value))
+        if lib.cobalt_ipc_set_timeout(h, ipc_timeout_s()) != 0:
+            raise RuntimeError(f"cobalt_ipc_set_timeout failed: {lib.cobalt_comm_last_error().decode()}")
     except Exception:
         lib.cobalt_comm_destroy(h, 1)
         raise
