@@ -850,8 +850,113 @@ __device__ __forceinline__ bool dd_convert(uint64_t m, int dexp, double& out) {
   return true;
 }
 
-// Status + value of one field (see the status codes above).
-__device__ uint8_t parse_field(const uint8_t* __restrict__ buf, const Field& f, double& out) {
+// The C literals 1e0 .. 1e308 (correctly rounded doubles), the scale table of pandas_xstrtod.
+__constant__ double kPow10Lit[309] = {
+    1.0, 10.0, 100.0, 1000.0, 10000.0, 100000.0, 1000000.0, 10000000.0,
+    100000000.0, 1000000000.0, 10000000000.0, 100000000000.0, 1000000000000.0, 10000000000000.0, 100000000000000.0, 1000000000000000.0,
+    1e+16, 1e+17, 1e+18, 1e+19, 1e+20, 1e+21, 1e+22, 1e+23,
+    1e+24, 1e+25, 1e+26, 1e+27, 1e+28, 1e+29, 1e+30, 1e+31,
+    1e+32, 1e+33, 1e+34, 1e+35, 1e+36, 1e+37, 1e+38, 1e+39,
+    1e+40, 1e+41, 1e+42, 1e+43, 1e+44, 1e+45, 1e+46, 1e+47,
+    1e+48, 1e+49, 1e+50, 1e+51, 1e+52, 1e+53, 1e+54, 1e+55,
+    1e+56, 1e+57, 1e+58, 1e+59, 1e+60, 1e+61, 1e+62, 1e+63,
+    1e+64, 1e+65, 1e+66, 1e+67, 1e+68, 1e+69, 1e+70, 1e+71,
+    1e+72, 1e+73, 1e+74, 1e+75, 1e+76, 1e+77, 1e+78, 1e+79,
+    1e+80, 1e+81, 1e+82, 1e+83, 1e+84, 1e+85, 1e+86, 1e+87,
+    1e+88, 1e+89, 1e+90, 1e+91, 1e+92, 1e+93, 1e+94, 1e+95,
+    1e+96, 1e+97, 1e+98, 1e+99, 1e+100, 1e+101, 1e+102, 1e+103,
+    1e+104, 1e+105, 1e+106, 1e+107, 1e+108, 1e+109, 1e+110, 1e+111,
+    1e+112, 1e+113, 1e+114, 1e+115, 1e+116, 1e+117, 1e+118, 1e+119,
+    1e+120, 1e+121, 1e+122, 1e+123, 1e+124, 1e+125, 1e+126, 1e+127,
+    1e+128, 1e+129, 1e+130, 1e+131, 1e+132, 1e+133, 1e+134, 1e+135,
+    1e+136, 1e+137, 1e+138, 1e+139, 1e+140, 1e+141, 1e+142, 1e+143,
+    1e+144, 1e+145, 1e+146, 1e+147, 1e+148, 1e+149, 1e+150, 1e+151,
+    1e+152, 1e+153, 1e+154, 1e+155, 1e+156, 1e+157, 1e+158, 1e+159,
+    1e+160, 1e+161, 1e+162, 1e+163, 1e+164, 1e+165, 1e+166, 1e+167,
+    1e+168, 1e+169, 1e+170, 1e+171, 1e+172, 1e+173, 1e+174, 1e+175,
+    1e+176, 1e+177, 1e+178, 1e+179, 1e+180, 1e+181, 1e+182, 1e+183,
+    1e+184, 1e+185, 1e+186, 1e+187, 1e+188, 1e+189, 1e+190, 1e+191,
+    1e+192, 1e+193, 1e+194, 1e+195, 1e+196, 1e+197, 1e+198, 1e+199,
+    1e+200, 1e+201, 1e+202, 1e+203, 1e+204, 1e+205, 1e+206, 1e+207,
+    1e+208, 1e+209, 1e+210, 1e+211, 1e+212, 1e+213, 1e+214, 1e+215,
+    1e+216, 1e+217, 1e+218, 1e+219, 1e+220, 1e+221, 1e+222, 1e+223,
+    1e+224, 1e+225, 1e+226, 1e+227, 1e+228, 1e+229, 1e+230, 1e+231,
+    1e+232, 1e+233, 1e+234, 1e+235, 1e+236, 1e+237, 1e+238, 1e+239,
+    1e+240, 1e+241, 1e+242, 1e+243, 1e+244, 1e+245, 1e+246, 1e+247,
+    1e+248, 1e+249, 1e+250, 1e+251, 1e+252, 1e+253, 1e+254, 1e+255,
+    1e+256, 1e+257, 1e+258, 1e+259, 1e+260, 1e+261, 1e+262, 1e+263,
+    1e+264, 1e+265, 1e+266, 1e+267, 1e+268, 1e+269, 1e+270, 1e+271,
+    1e+272, 1e+273, 1e+274, 1e+275, 1e+276, 1e+277, 1e+278, 1e+279,
+    1e+280, 1e+281, 1e+282, 1e+283, 1e+284, 1e+285, 1e+286, 1e+287,
+    1e+288, 1e+289, 1e+290, 1e+291, 1e+292, 1e+293, 1e+294, 1e+295,
+    1e+296, 1e+297, 1e+298, 1e+299, 1e+300, 1e+301, 1e+302, 1e+303,
+    1e+304, 1e+305, 1e+306, 1e+307, 1e+308,
+};
+
+// pandas.read_csv's DEFAULT float conversion (float_precision None = "high": its tokenizer's
+// precise_xstrtod), reproduced operation by operation so a device-parsed frame equals pandas' bit for
+// bit: the first 17 digits -- leading zeros included -- accumulated as number = number * 10 + digit in
+// double arithmetic (no FMA contraction), further integer digits counted into the exponent, further
+// fraction digits dropped, the sign applied, then ONE multiply or divide by the double 10^|exponent|
+// (two divides below 1e-308). Not correctly rounded (~1 ulp off on 17-digit inputs). Pinned against
+// pandas on 20k generated strings (tests/test_gpu_csv.py). [i, e): the field after its sign.
+// Returns false for what pandas types as text (an exponent past 308 or an overflow to inf).
+__device__ bool pandas_xstrtod(const uint8_t* __restrict__ buf, int64_t i, int64_t e, bool neg, double& out) {
+#pragma clang fp contract(off)
+  double number = 0.0;
+  int exponent = 0, nd = 0;
+  for (; i < e; ++i) {
+    const unsigned dg = (unsigned)buf[i] - '0';
+    if (dg > 9) break;
+    if (nd < 17) { number = number * 10.0 + (double)dg; ++nd; }
+    else ++exponent;
+  }
+  if (i < e && buf[i] == '.') {
+    int ndec = 0;
+    for (++i; i < e && nd < 17; ++i) {
+      const unsigned dg = (unsigned)buf[i] - '0';
+      if (dg > 9) break;
+      number = number * 10.0 + (double)dg;
+      ++nd;
+      ++ndec;
+    }
+    while (i < e && (unsigned)buf[i] - '0' <= 9u) ++i;
+    exponent -= ndec;
+  }
+  if (neg) number = -number;
+  if (i < e && (buf[i] == 'e' || buf[i] == 'E')) {
+    ++i;
+    bool eneg = false;
+    if (i < e && (buf[i] == '+' || buf[i] == '-')) { eneg = buf[i] == '-'; ++i; }
+    int n = 0;
+    for (; i < e; ++i) {
+      const unsigned dg = (unsigned)buf[i] - '0';
+      if (dg > 9) break;
+      if (n < 100000) n = n * 10 + (int)dg;
+    }
+    exponent += eneg ? -n : n;
+  }
+  if (exponent > 308) return false;
+  if (exponent > 0) {
+    number *= kPow10Lit[exponent];
+  } else if (exponent < -308) {
+    if (exponent < -616) {
+      number = 0.0;
+    } else {
+      number /= kPow10Lit[-308 - exponent];
+      number /= kPow10Lit[308];
+    }
+  } else {
+    number /= kPow10Lit[-exponent];
+  }
+  if (__builtin_isinf(number)) return false;
+  out = number;
+  return true;
+}
+
+// Status + value of one field (see the status codes above). pandas_fp: float-syntax fields take
+// pandas' default conversion (pandas_xstrtod) instead of the correctly rounded one.
+__device__ uint8_t parse_field(const uint8_t* __restrict__ buf, const Field& f, double& out, bool pandas_fp = false) {
   out = __builtin_nan("");
   if (is_na(buf, f)) return kStNull;
   const int64_t len = f.e - f.s;
@@ -903,6 +1008,14 @@ __device__ uint8_t parse_field(const uint8_t* __restrict__ buf, const Field& f, 
     dexp += eneg ? -ex : ex;
   }
   if (i != f.e) return kStStr;
+  if (pandas_fp && frac) {  // syntax checked above: the digits and exponent are well formed
+    int64_t b = f.s;
+    if (buf[b] == '+' || buf[b] == '-') ++b;
+    double v;
+    if (!pandas_xstrtod(buf, b, f.e, neg, v)) return kStNeedHost;
+    out = v;
+    return kStFrac;
+  }
   if (lost) return kStNeedHost;
   double v;
   if (m == 0) {
@@ -921,6 +1034,7 @@ __device__ uint8_t parse_field(const uint8_t* __restrict__ buf, const Field& f, 
   return frac ? kStFrac : kStInt;
 }
 
+template <bool kPandasFp>
 __global__ __launch_bounds__(256) void k_csv_parse(const uint8_t* __restrict__ buf, const int64_t* __restrict__ fend,
                                                    int64_t nrows, int C, uint8_t* __restrict__ status,
                                                    double* __restrict__ vals) {
@@ -928,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_csv_parse(const uint8_t* __restrict__ b
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
     const Field f = field_of(buf, fend, r * C + c, C);
     double v;
-    const uint8_t st = parse_field(buf, f, v);
+    const uint8_t st = parse_field(buf, f, v, kPandasFp);
     status[(int64_t)c * nrows + r] = st;
     vals[(int64_t)c * nrows + r] = v;
   }
@@ -1059,11 +1173,16 @@ COBALT_API int cobalt_csv_fields(const uint8_t* buf, int64_t n, const int64_t* q
 }
 
 // Pass 4: status [C][nrows] (uint8) and values [C][nrows] (float64) of every field.
+// pandas_fp: 0 = correctly rounded floats (pandas float_precision="round_trip"), 1 = pandas' default
+// conversion (pandas_xstrtod)
 COBALT_API int cobalt_csv_parse(const uint8_t* buf, const int64_t* fend, int64_t nrows, int C, uint8_t* status,
-                                double* vals, hipStream_t st) {
+                                double* vals, int pandas_fp, hipStream_t st) {
   if (nrows <= 0) return 0;
   if (C < 1 || C > 65535) return -1;
-  hipLaunchKernelGGL(k_csv_parse, dim3(grid_rows(nrows), C), dim3(256), 0, st, buf, fend, nrows, C, status, vals);
+  if (pandas_fp)
+    hipLaunchKernelGGL(k_csv_parse<true>, dim3(grid_rows(nrows), C), dim3(256), 0, st, buf, fend, nrows, C, status, vals);
+  else
+    hipLaunchKernelGGL(k_csv_parse<false>, dim3(grid_rows(nrows), C), dim3(256), 0, st, buf, fend, nrows, C, status, vals);
   CK_LAUNCH();
   return 0;
 }

@@ -37,7 +37,7 @@ _native.register("cobalt_csv_chunk", ctypes.c_int, [])
 _native.register("cobalt_csv_quotes", ctypes.c_int, [_P, _I64, _P, _P])
 _native.register("cobalt_csv_delims", ctypes.c_int, [_P, _I64, _P, _P, _P])
 _native.register("cobalt_csv_fields", ctypes.c_int, [_P, _I64, _P, _P, _I32, _P, _P, _P])
-_native.register("cobalt_csv_parse", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P])
+_native.register("cobalt_csv_parse", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _I32, _P])
 _native.register("cobalt_csv_hash", ctypes.c_int, [_P, _P, _I64, _I32, _P, _I32, _P, _P])
 _native.register("cobalt_csv_verify", ctypes.c_int, [_P, _P, _I64, _I32, _P, _I32, _P, _P, _P])
 _native.register("cobalt_csv_span", ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _P])
@@ -148,10 +148,18 @@ def _strings_array(host_data: np.ndarray, off: np.ndarray, quoted: np.ndarray, v
     return arr
 
 
-def read_csv_gpu(src, device, hash_unique_share: float = 0.2, timings: dict | None = None):
-    """Parse a CSV (path, bytes, optionally gzip) on the GPU into a DeviceFrame (see module doc)."""
+def read_csv_gpu(src, device, hash_unique_share: float = 0.2, timings: dict | None = None,
+                 float_precision: str = "round_trip"):
+    """Parse a CSV (path, bytes, optionally gzip) on the GPU into a DeviceFrame (see module doc).
+
+    ``float_precision``: ``"round_trip"`` (correctly rounded, = pandas ``float_precision="round_trip"``)
+    or ``"high"`` (= pandas' DEFAULT conversion, which is up to ~1 ulp off on 17-digit inputs; the
+    device reproduces its arithmetic, csrc/csv.hip pandas_xstrtod)."""
     from .device_frame import DCol, DeviceFrame
 
+    if float_precision not in ("round_trip", "high"):
+        raise ValueError(f"float_precision must be 'round_trip' or 'high', got {float_precision!r}")
+    pandas_fp = float_precision == "high"
     dev = torch.device(device)
     if dev.type != "cuda":
         raise CsvLayoutError("the GPU CSV reader needs a GPU device")
@@ -193,8 +201,8 @@ def read_csv_gpu(src, device, hash_unique_share: float = 0.2, timings: dict | No
     t_tok = time.perf_counter()
     status = torch.empty((C, N), dtype=torch.uint8, device=dev)
     vals = torch.empty((C, N), dtype=torch.float64, device=dev)
-    _chk(lib.cobalt_csv_parse(buf.data_ptr(), fend.data_ptr(), N, C, status.data_ptr(), vals.data_ptr(), stream),
-         "cobalt_csv_parse")
+    _chk(lib.cobalt_csv_parse(buf.data_ptr(), fend.data_ptr(), N, C, status.data_ptr(), vals.data_ptr(),
+                              int(pandas_fp), stream), "cobalt_csv_parse")
     counts = torch.bincount((torch.arange(C, device=dev)[:, None] * 8 + status.long()).reshape(-1),
                             minlength=C * 8).reshape(C, 8).cpu().numpy()
     t_parse = time.perf_counter()
@@ -202,6 +210,14 @@ def read_csv_gpu(src, device, hash_unique_share: float = 0.2, timings: dict | No
     def host_reparse(c: int) -> None:
         rows = torch.nonzero(status[c] == ST_HOST).reshape(-1)
         txt = _texts(lib, stream, buf, fend, C, torch.full_like(rows, c, dtype=torch.int32), rows, None, dev)
+        if pandas_fp:  # the few fields the device left: pandas itself (it types overflows as text)
+            import pandas as pd
+
+            col = pd.read_csv(io.StringIO("x\n" + "\n".join(txt) + "\n"), dtype=None)["x"]
+            if col.dtype != np.float64:
+                raise CsvLayoutError(f"column {names[c]!r} holds values pandas reads as text")
+            vals[c][rows] = torch.from_numpy(col.to_numpy()).to(dev)
+            return
         vals[c][rows] = torch.tensor([float(t) for t in txt], dtype=torch.float64, device=dev)
 
     kinds: dict[int, str] = {}

@@ -175,13 +175,14 @@ class DeviceFrame:
 
     @classmethod
     def read_csv(cls, path_or_bytes, device, threads: bool = True, engine: str = "auto",
-                 timings: dict | None = None) -> "DeviceFrame":
+                 timings: dict | None = None, float_precision: str = "round_trip") -> "DeviceFrame":
         """Parse a (optionally gzipped) CSV with pandas' missing values into device columns.
 
         ``engine="gpu"`` (the default on a GPU device, ``"auto"``): the bytes go to HBM and the
         tokenizer / parser / dictionary encoder of ``csrc/csv.hip`` run there (prep/csv_gpu.py); a file
         it cannot lay out as a rectangle falls back to ``"arrow"``: pyarrow's multithreaded C++ reader
-        on the host, then every column is uploaded."""
+        on the host, then every column is uploaded. ``float_precision="high"`` reproduces pandas'
+        default float conversion (GPU engine only: the Arrow reader rounds correctly)."""
         import io
 
         import pyarrow as pa
@@ -189,13 +190,15 @@ class DeviceFrame:
 
         if engine not in ("auto", "gpu", "arrow"):
             raise ValueError(f"engine must be auto, gpu or arrow, got {engine!r}")
+        if float_precision == "high" and (engine == "arrow" or torch.device(device).type != "cuda"):
+            raise ValueError('float_precision="high" needs the GPU engine')
         if engine in ("auto", "gpu") and torch.device(device).type == "cuda":
             from .csv_gpu import CsvLayoutError, read_csv_gpu
 
             try:
-                return read_csv_gpu(path_or_bytes, device, timings=timings)
+                return read_csv_gpu(path_or_bytes, device, timings=timings, float_precision=float_precision)
             except CsvLayoutError:
-                if engine == "gpu":
+                if engine == "gpu" or float_precision == "high":
                     raise
 
         src = path_or_bytes

@@ -20,6 +20,9 @@ from ..models.booster import Booster
 from ..ops import predict_ops
 
 
+_SCORE_GRAPH_CACHE = 8  # captured score_device_matrix graphs kept per booster
+
+
 class GraphScorer:
     """A predictor launch over a static [chunk, F] device buffer, captured into a hipGraph."""
 
@@ -52,28 +55,46 @@ def score_device_matrix(booster: Booster, X: torch.Tensor, out: torch.Tensor | N
     """Probabilities of a device-resident [N, F] matrix.
 
     Row-contiguous fp32 input is scored in place: the predictor launches for every ``chunk`` rows run
-    straight on views of X and ``out``, captured into one hipGraph and replayed once. (The earlier
-    form staged each chunk into a GraphScorer's static buffer: a D2D copy per chunk plus the
-    scorer's warm-up launch, ~10% of the 125M-row shard.) Other layouts go through a GraphScorer's
-    static buffer chunk by chunk."""
+    straight on views of X and ``out``. (The earlier form staged each chunk into a GraphScorer's
+    static buffer: a D2D copy per chunk plus the scorer's warm-up launch, ~10% of the 125M-row
+    shard.) The launch sequence is captured into a hipGraph the SECOND time the same (X, out) buffers
+    are scored and replayed from then on (a serving loop over static buffers); a one-off call
+    launches directly instead of paying a capture it would replay once. Other layouts go through a
+    GraphScorer's static buffer chunk by chunk."""
     N, F = X.shape
     out = out if out is not None else torch.empty(N, dtype=torch.float32, device=X.device)
     if N == 0:
         return out
     if (X.dtype == torch.float32 and X.stride(1) == 1 and out.is_contiguous()
             and out.dtype == torch.float32 and out.device == X.device):
-        predict_ops.gpu_forest(booster, X.device)  # pack + upload the forest outside the capture
+        gf = predict_ops.gpu_forest(booster, X.device)  # pack + upload the forest outside any capture
         cur = torch.cuda.current_stream(X.device)
         side = torch.cuda.Stream(X.device)
         side.wait_stream(cur)  # X (and out) may still be in flight on the caller's stream
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=side):
+
+        def launches():
             for s in range(0, N, chunk):
                 e = min(N, s + chunk)
                 predict_ops.predict_gpu(booster, X[s:e], None, out_prob=out[s:e])
+
+        cache = booster.__dict__.setdefault("_score_graphs", {})
+        key = (str(X.device), X.data_ptr(), X.stride(0), N, F, out.data_ptr(), int(chunk), id(gf))
+        graph = cache.get(key)
+        if graph is None and key in cache:  # second sighting of these buffers: capture
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=side):
+                launches()
+            cache[key] = graph
         with torch.cuda.stream(side):
-            graph.replay()
+            if graph is not None:
+                graph.replay()
+            else:
+                launches()
+                if len(cache) >= _SCORE_GRAPH_CACHE:  # bounded: drop the oldest entry
+                    cache.pop(next(iter(cache)))
+                cache[key] = None
         side.synchronize()
+        cur.wait_stream(side)
         return out
     sc = GraphScorer(booster, min(chunk, N), F, X.device)
     sc.stream.wait_stream(torch.cuda.current_stream(X.device))  # X may still be in flight there

@@ -244,3 +244,55 @@ def test_gpu_reader_pandas_typing_duplicates_and_nullable_bools():
     g = DeviceFrame.read_csv(data, "cuda", engine="gpu")
     pd.testing.assert_frame_equal(g.to_pandas(), ref)
     assert bytes(frame_to_csv_bytes(g)) == ref.to_csv(index=False).encode()
+
+
+def _float_strings(n=20000, seed=1):
+    import random
+
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        k = rng.randint(0, 7)
+        if k == 0:
+            s = repr(float(np.float32(rng.uniform(0, 1000))))  # 17-digit float32 values (the API's echo)
+        elif k == 1:
+            s = repr(rng.uniform(-1e6, 1e6))
+        elif k == 2:
+            s = "0.0000" + "".join(rng.choice("0123456789") for _ in range(rng.randint(1, 22)))
+        elif k == 3:
+            s = ("".join(rng.choice("0123456789") for _ in range(rng.randint(1, 25))) + "." +
+                 "".join(rng.choice("0123456789") for _ in range(rng.randint(1, 10))))
+        elif k == 4:
+            s = repr(rng.uniform(0, 1) * 10 ** rng.randint(-30, 30))
+        elif k == 5:
+            s = "%.20e" % rng.uniform(1, 10)
+        elif k == 6:
+            s = "-" + repr(rng.uniform(0, 1) * 10 ** rng.randint(-320, -300))  # subnormal range
+        else:
+            s = "00" + repr(rng.uniform(0, 100))
+        out.append(s)
+    return out
+
+
+def test_pandas_default_float_conversion_bit_exact():
+    """float_precision="high" reproduces pandas.read_csv's DEFAULT float conversion (not correctly
+    rounded: 17 leading digits accumulated in double, one scale by 10^k) bit for bit; "round_trip"
+    equals pandas' round_trip mode. The strings include 17-digit float32 reprs, leading zeros, > 17
+    digits, exponents and subnormals."""
+    import io
+
+    import pandas as pd
+
+    strs = _float_strings()
+    body = ("x,y\n" + "\n".join(f"{s},{i}" for i, s in enumerate(strs)) + "\n").encode()
+    want_hi = pd.read_csv(io.BytesIO(body))["x"].to_numpy()
+    want_rt = pd.read_csv(io.BytesIO(body), float_precision="round_trip")["x"].to_numpy()
+    assert (want_hi != want_rt).sum() > 100  # the two pandas modes do differ on these strings
+    hi = DeviceFrame.read_csv(body, "cuda", engine="gpu", float_precision="high")
+    rt = DeviceFrame.read_csv(body, "cuda", engine="gpu")
+    got_hi, got_rt = hi["x"].data.cpu().numpy(), rt["x"].data.cpu().numpy()
+    assert np.array_equal(got_hi.view(np.int64), want_hi.view(np.int64))
+    assert np.array_equal(got_rt.view(np.int64), want_rt.view(np.int64))
+    # an overflow is text to pandas: the device reader refuses the file instead of guessing
+    with pytest.raises(Exception):
+        DeviceFrame.read_csv(b"x\n1e400\n1.5\n", "cuda", engine="gpu", float_precision="high")

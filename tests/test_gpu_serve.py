@@ -140,6 +140,19 @@ def test_batch_scoring_chunks_match_host(reference_booster):
     Xd.mul_(1.0)  # pending work on the current stream when the scorer starts
     pd = score_device_matrix(reference_booster, Xd, chunk=chunk).cpu().numpy()
     np.testing.assert_allclose(pd, ref, rtol=0, atol=2e-7)
+    # the same (X, out) buffers again: direct launches, then a capture, then replays of that graph,
+    # which read X's CURRENT contents
+    out = torch.empty(n, dtype=torch.float32, device=Xd.device)
+    for _ in range(3):
+        np.testing.assert_array_equal(score_device_matrix(reference_booster, Xd, out, chunk=chunk).cpu().numpy(), pd)
+    assert any(g is not None for g in reference_booster.__dict__["_score_graphs"].values())
+    X2 = X.copy()
+    X2[: n // 2] = X[n // 2: 2 * (n // 2)]
+    Xd.copy_(torch.from_numpy(X2))
+    ref2 = sigmoid32(predict_margin_host(reference_booster, X2))
+    np.testing.assert_allclose(score_device_matrix(reference_booster, Xd, out, chunk=chunk).cpu().numpy(), ref2,
+                               rtol=0, atol=2e-7)
+    Xd.copy_(torch.from_numpy(X))
     # column-major input takes the GraphScorer staging path (static buffer + replay per chunk)
     Xc = Xd.t().contiguous().t()
     assert Xc.stride(1) != 1
@@ -193,3 +206,41 @@ def test_host_stream_scorer_files_equal_device_path(reference_booster, tmp_path)
     Xd = torch.from_numpy(np.concatenate(parts)).cuda()
     ref = bs.score_device_matrix(reference_booster, Xd).cpu().numpy()
     assert np.array_equal(got, ref)
+
+
+def test_bulk_csv_device_parse_equals_pandas_path(reference_booster, monkeypatch):
+    """/predict_bulk_csv with a large upload on a GPU engine: parsed by the GPU CSV reader and scored
+    from HBM -- the response equals the pandas path's (the reference's pd.read_csv + predict_proba)."""
+    import io
+
+    import pandas as pd
+    from fastapi.testclient import TestClient
+
+    from cobalt_smart_lender_ai_amd.config import DEPLOYED_FEATURES, ServeConfig
+    from cobalt_smart_lender_ai_amd.serve import app as app_mod
+
+    n = 12_000
+    X = _rows(n, len(DEPLOYED_FEATURES), seed=11)
+    df = pd.DataFrame(X.astype(np.float64), columns=DEPLOYED_FEATURES)
+    df["term"] = np.where(np.arange(n) % 2 == 0, 36, 60)  # an integer column (int64 in both parsers)
+    buf = io.StringIO()
+    df.to_csv(buf, index=False)
+    body = buf.getvalue().encode()
+    assert len(body) >= 1 << 20
+    app = app_mod.create_app(ServeConfig(device="cuda:0"), booster=reference_booster)
+    with TestClient(app) as c:
+        files = {"file": ("x.csv", body, "text/csv")}
+        monkeypatch.setattr(app_mod, "GPU_CSV_MIN_BYTES", 1 << 40)
+        host = c.post("/predict_bulk_csv", files=files)
+        monkeypatch.setattr(app_mod, "GPU_CSV_MIN_BYTES", 0)
+        calls = []
+        real = app_mod._score_device
+        monkeypatch.setattr(app_mod, "_score_device", lambda b, Xd: calls.append(Xd.shape) or real(b, Xd))
+        dev = c.post("/predict_bulk_csv", files=files)
+    assert host.status_code == 200 and dev.status_code == 200, (host.text[:200], dev.text[:200])
+    assert calls == [(n, len(DEPLOYED_FEATURES))]  # the device path ran
+    hp, dp = host.json()["predictions"], dev.json()["predictions"]
+    assert len(hp) == len(dp) == n
+    diff = [(i, k, hp[i][k], dp[i].get(k)) for i in range(n) for k in hp[i] if hp[i][k] != dp[i].get(k)]
+    assert not diff, (len(diff), diff[:8])
+    assert dev.json() == host.json()
