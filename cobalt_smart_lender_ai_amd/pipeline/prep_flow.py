@@ -40,17 +40,22 @@ def _engine(engine: str | None, device) -> str:
 def read_table(store: ArtifactStore, key: str, device=None) -> pd.DataFrame:
     """``store.read_csv(key)`` -- parsed on the GPU when one is used (prep/csv_gpu.py: a 3.3 GB
     full-data tree CSV in well under a second instead of about a minute), then handed over as a pandas
-    frame. Numbers are correctly rounded (pandas' default C parser can be an ulp off); the frame equals
-    ``pd.read_csv(..., float_precision="round_trip")``."""
+    frame equal to ``pd.read_csv``'s (the reference job's read, model_tree_train_test.py:77): pandas'
+    default float conversion is reproduced on the device (float_precision="high"); a file the device
+    reader refuses (ragged rows, values pandas types as text) is read by pandas itself."""
     import torch
 
     dev = torch.device(device) if device is not None else (
         torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
     if dev.type != "cuda":
         return store.read_csv(key)
+    from ..prep.csv_gpu import CsvLayoutError
     from ..prep.device_frame import DeviceFrame
 
-    return DeviceFrame.read_csv(store.get_bytes(key), dev).to_pandas()
+    try:
+        return DeviceFrame.read_csv(store.get_bytes(key), dev, float_precision="high").to_pandas()
+    except CsvLayoutError:
+        return store.read_csv(key)
 
 
 def _write_frame(store: ArtifactStore, dfr, key: str) -> None:

@@ -174,7 +174,7 @@ def test_writer_splices_host_formatted_values():
     assert bytes(frame_to_csv_bytes(fr)) == _pandas_bytes(fr)
 
 
-def test_read_table_equals_pandas_round_trip(tmp_path):
+def test_read_table_equals_pandas_read_csv(tmp_path):
     """The train / train-nn CLI input read on the GPU equals pandas' correctly rounded reader."""
     import io
 
@@ -193,8 +193,10 @@ def test_read_table_equals_pandas_round_trip(tmp_path):
     for key in ("tree", "nn"):
         st.put_bytes(f"{key}.csv", frame_to_csv_bytes(res[key]))
         got = read_table(st, f"{key}.csv", "cuda")
-        want = pd.read_csv(io.BytesIO(st.get_bytes(f"{key}.csv")), low_memory=False, float_precision="round_trip")
+        # what the reference's job reads: pandas' DEFAULT float conversion, reproduced on the device
+        want = pd.read_csv(io.BytesIO(st.get_bytes(f"{key}.csv")), low_memory=False)
         pd.testing.assert_frame_equal(got, want, check_exact=True)
+        assert got.equals(st.read_csv(f"{key}.csv"))  # = the CPU path of read_table
 
 
 def test_prep_flow_gpu_engine_writes_the_pandas_artifacts(tmp_path):
