@@ -57,7 +57,9 @@ def main() -> None:
     world, rank = ctx.world, ctx.rank
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = torch.device("cuda", ctx.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    # COBALT_BENCH_SHARED_DEVICE=1: every rank on cuda:0 (the 1-GPU multi-process rehearsal)
+    dev_index = 0 if os.environ.get("COBALT_BENCH_SHARED_DEVICE") == "1" else ctx.local_rank
+    dev = torch.device("cuda", dev_index) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
 

@@ -121,7 +121,12 @@ def init_from_env(backend: str | None = None, native: bool | None = None, timeou
         _CTX = DistContext()
         return _CTX
     use_gpu = torch.cuda.is_available()
-    backend = backend or ("nccl" if use_gpu else "gloo")
+    # COBALT_DIST_BACKEND / COBALT_DIST_NATIVE: a gloo bootstrap with the native (IPC) communicator lets
+    # several ranks share ONE GPU (RCCL refuses two ranks per device) -- the 1-GPU rehearsal of the
+    # multi-rank bench (scripts/gpu_bench_multirank.sh)
+    backend = backend or os.environ.get("COBALT_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+    if native is None and os.environ.get("COBALT_DIST_NATIVE"):
+        native = os.environ["COBALT_DIST_NATIVE"] not in ("0", "")
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -55,3 +55,21 @@ def test_ipc_dead_peer_fails_fast():
     assert r0.get("error") == "CollectiveTimeout", r0
     assert "deadline" in r0.get("message", "") or "communicator error" in r0.get("message", ""), r0
     assert r0["elapsed_s"] < 120, r0
+
+
+@pytest.mark.timeout(900)
+def test_bench_torchrun_two_ranks_share_gpu():
+    """The driver's multi-rank bench entry point on real HIP: torchrun starts 2 ranks of bench.py on
+    cuda:0 (gloo bootstrap + the IPC communicator: COBALT_DIST_BACKEND / COBALT_DIST_NATIVE /
+    COBALT_BENCH_SHARED_DEVICE), one JSON line with dp2 / ipc, and the AUC of the 1-rank bench of the
+    same rows (scripts/gpu_bench_multirank.sh asserts both)."""
+    import os
+    import subprocess
+    from pathlib import Path
+
+    _check_clean(torch.cuda.is_initialized())
+    root = Path(__file__).resolve().parents[1]
+    r = subprocess.run(["bash", "scripts/gpu_bench_multirank.sh", "2"], cwd=root, capture_output=True, text=True,
+                       timeout=800, env={**os.environ, "ROWS": "400000"})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert "AUC" in r.stdout and "equal" in r.stdout, r.stdout[-2000:]
