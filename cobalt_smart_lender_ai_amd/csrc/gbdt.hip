@@ -147,7 +147,7 @@ struct GbdtDev {
   int32_t goff;           // byte offset of the packed gradient pair inside a row record
   int32_t* ridx[2];       // [N] x2
   int64_t* hist_b[2];     // [pairs][F+1][256][2]
-  int64_t* hist_s[2];
+  int64_t* hist_s[2];     // [nodes of the level][F+1][256][2]: every node's full histogram (k_eval), by position
   Node* nodes;            // [max_nodes] the tree being grown (one of nodes_buf, alternating per tree)
   Node* prev_nodes;       // [max_nodes] the previous tree (the other buffer), applied + archived by k_grad
   Node* nodes_buf[2];
@@ -161,7 +161,8 @@ struct GbdtDev {
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
-                          // 4 plan only (k_hist); 12 partition without the cursor claims
+                          // 4 plan only (k_hist); 12 partition without the cursor claims; root pass: 20 no exp,
+                          // 21 no LDS atomics, 22 no previous-tree walk
   int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
   int32_t by_hess;        // build k_eval's (global) hessian choice: DP default, COBALT_BUILD_BY_HESS on one GPU
   int32_t hist_pair;      // k_hist gathers each record with a lane pair (hist_rows_pair); COBALT_HIST_PAIR
@@ -928,7 +929,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + (int64_t)u * B;
       if (i >= end) continue;
-      if (apply_tree >= 0) {  // walk the previous tree with the record held in registers
+      if (apply_tree >= 0 && d.ablate != 22) {  // walk the previous tree with the record held in registers
         int nidx = 0;
         uint32_t m = s_meta[0];
         while (m & (1u << 25)) {
@@ -944,7 +945,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
         d.margin[i] = mf[u];
       }
       const double mm = (double)mf[u];
-      const double p = 1.0 / (1.0 + exp(-mm));
+      const double p = d.ablate == 20 ? 0.5 + 0.01 * mm : 1.0 / (1.0 + exp(-mm));  // (20: timing-only, no exp)
       const double y = (double)yl[u];
       const double w = (double)wt[u];
       double g = (p - y) * w;
@@ -960,7 +961,7 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
       reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
       tg += gq;
       th += hq;
-      hist_add_rec32<FT4>(s_hist, hl, ra[u], rb[u]);
+      if (d.ablate != 21) hist_add_rec32<FT4>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
     }
   }
   __syncthreads();
@@ -1496,9 +1497,16 @@ __device__ __forceinline__ void ipc_sum_cells_n(int nr, const IpcFusedView* iv, 
 // (ipc_sum_cells: dynamic LDS of (cells + 1) x 16 bytes) and reads them from there; the built child's
 // global histogram is stored to hist_b for the next level's subtraction. The single-GPU instantiation
 // (kFused = false) has none of it.
+// Per-slot feature metadata of k_eval<false> (the host's eval_assignment table with each feature's bin
+// count and compact offset): slot 2 w + s = wave w's s-th feature, word = f | nb << 8 | off << 17
+// (f = 0xFF: no feature). Kernel arguments, read by scalar loads from the kernarg segment, so the
+// histogram loads need no global metadata load first.
+struct EvalSlots {
+  uint32_t w[32];
+};
+
 template <bool kGroups, bool kFused>
-__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg, uint64_t asg0,
-                                               uint64_t asg1, uint64_t asg2, uint64_t asg3) {
+__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg, EvalSlots es) {
   BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   const int fbeg = kGroups ? blockIdx.y * fg : 0;
@@ -1508,7 +1516,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int pair = level == 0 ? 0 : (pos >> 1);
   const int64_t SE = d.slot_elems;
   const int64_t* hb = d.hist_b[parity] + pair * SE;
-  int64_t* hs = d.hist_s[parity] + pair * SE;
+  int64_t* hs = d.hist_s[parity] + (int64_t)pos * SE;  // this node's full histogram, for its children
   const int lane = lane_id();
   const int nw = (int)(blockDim.x / kWave);
   const uint8_t* fm = d.fmask + (int64_t)tree * d.F;
@@ -1520,21 +1528,26 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       EvalFeat& e = ef[s];
+      int nbv, offv;
       if (kGroups) {
         e.f = fbase + s * nw;
-      } else {
+        const int fc = min(e.f, d.F - 1);
+        nbv = d.nbins[fc];
+        offv = d.hoff[fc];
+      } else {  // from the kernel arguments: no global load in front of the histogram loads
         const int slot = __builtin_amdgcn_readfirstlane(wave_id() * 2 + s);
-        const uint64_t word = slot < 8 ? asg0 : slot < 16 ? asg1 : slot < 24 ? asg2 : asg3;
-        const int fi = (int)((word >> (8 * (slot & 7))) & 0xFFu);
+        const uint32_t sw = es.w[slot];
+        const int fi = (int)(sw & 0xFFu);
         e.f = fi == 0xFF ? fend : fi;
+        nbv = (int)((sw >> 8) & 0x1FFu);
+        offv = (int)(sw >> 17);
       }
       const int fc = min(e.f, d.F - 1);
       const bool valid = e.f < fend;
       const uint8_t fmv = fm[fc];  // unconditional loads, masked after (no per-load branch)
-      const int nbv = d.nbins[fc];
       e.on = valid && fmv != 0;
       e.nb = valid ? nbv : 0;
-      e.off = d.hoff[fc];
+      e.off = offv;
 #pragma unroll
       for (int c = 0; c < 4; ++c) e.cut[c] = d.cuts[fc * kMaxBins + c * kWave + lane];
     }
@@ -1543,7 +1556,6 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   // round trip 1 (uniform scalar loads); unconditional (in-bounds) loads selected after
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
-  const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
   int64_t rg = 0, rh = 0;
   if (!kFused) {
     rg = hb[(int64_t)d.ncells * 2];
@@ -1568,7 +1580,6 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   }
   // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
   const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
-  const int pbuild = level > 0 ? pbuild_raw : 1;
   // No early return for an inactive node: a branch here let hipcc sink the feature metadata loads
   // below it (a third dependent round trip). Its block computes on valid buffers and stores nothing.
   const bool active = status == kActive;
@@ -1582,12 +1593,10 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
       if (ef[s].f < 32) s_nb[ef[s].f] = ef[s].nb;
   }
   const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
-  const int64_t* parent = hb;  // the sibling's parent histogram (unused when this child was built)
-  if (!built) {
-    const int ppos = pos >> 1;
-    const int ppair = level == 1 ? 0 : (ppos >> 1);
-    parent = (pbuild ? d.hist_b[parity ^ 1] : d.hist_s[parity ^ 1]) + ppair * SE;
-  }
+  // the parent's full histogram (the previous level's k_eval stored every node's by position): its
+  // address depends on the block index only, so its loads go out with the node record's (unused when
+  // this child was built)
+  const int64_t* parent = level > 0 ? d.hist_s[parity ^ 1] + (int64_t)(pos >> 1) * SE : hb;
   // wave-uniform: kept in SGPRs (as a VALU result it held a VGPR pair the candidate loop spilled)
   const double parent_gain = __longlong_as_double(
       readlane64(__double_as_longlong(calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw)), 0));
@@ -1615,11 +1624,12 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   // Only lanes holding a real bin of an evaluated feature load (exec-masked): the CU's address path
   // costs per active lane, and unmasked, the 16 waves' 2 x 4 chunks (+ the parent's) were 256 full
   // 1 KB load instructions per block for ~26 chunks of real bins -- ~2 us per level at 1M rows.
+  // (the colsample bit is applied after the loads: it is a global load of round trip 1 itself)
   bool ld[2][4];
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) ld[s][c] = ef[s].on && c * kWave + lane < ef[s].nb;
+    for (int c = 0; c < 4; ++c) ld[s][c] = c * kWave + lane < ef[s].nb;
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1630,13 +1640,18 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
         v[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c])
                            : make_longlong2(0, 0);
     }
-  if (!built) {
+  if (level > 0) {  // kernel argument: uniform, no wait on the node record (whose build flag selects)
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         pv[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(pa2) + cofs[s][c])
                             : make_longlong2(0, 0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pv[s][c] = make_longlong2(0, 0);
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1656,7 +1671,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     if (!e.on) continue;
     const int f = e.f, nb = e.nb;
     const int nch = (nb + kWave - 1) / kWave;  // wave-uniform
-    if (!built && active) {  // materialise the sibling histogram for the next level
+    if (active && level + 1 < d.max_depth) {  // this node's histogram, for its children's subtraction
       longlong2* hs2 = reinterpret_cast<longlong2*>(hs);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -1822,7 +1837,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
   const int64_t SE = d.slot_elems;
   const int pair = level == 0 ? 0 : (pos >> 1);
   const int64_t* hb = d.hist_b[parity] + pair * SE;
-  int64_t* hs = d.hist_s[parity] + pair * SE;
+  int64_t* hs = d.hist_s[parity] + (int64_t)pos * SE;  // this node's full histogram, for its children
   // round trip 1: feature table (LDS) + node record (uniform)
   if (t <= F) s_hoff[t] = d.hoff[t];
   if (t < F) {
@@ -1833,23 +1848,17 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
   // unconditional (in-bounds) loads selected after: one round trip, no per-load branch
-  const int pbuild_raw = nodes[level > 0 ? (1 << (level - 1)) - 1 + (pos >> 1) : 0].build;
   const int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
   const int64_t ng = nodes[n].G, nh = nodes[n].H;
   const int64_t G = level == 0 ? rg : ng, H = level == 0 ? rh : nh;
-  const int pbuild = level > 0 ? pbuild_raw : 1;
   if (status != kActive) return;  // uniform across the block
   __syncthreads();
   stamp_.probe(1);
   const int nc = s_hoff[F];
   const int cpt = (nc + kEvalThreads - 1) / kEvalThreads;  // cells per thread: every wave gets work
   const int c0 = t * cpt;
-  const int64_t* parent = nullptr;
-  if (!built) {
-    const int ppos = pos >> 1;
-    const int ppair = level == 1 ? 0 : (ppos >> 1);
-    parent = (pbuild ? d.hist_b[parity ^ 1] : d.hist_s[parity ^ 1]) + ppair * SE;
-  }
+  // the parent's full histogram, stored by position by the previous level's evaluation
+  const int64_t* parent = level > 0 ? d.hist_s[parity ^ 1] + (int64_t)(pos >> 1) * SE : hb;
   // feature of the thread's first cell (largest f with s_hoff[f] <= c0)
   int f0 = 0;
   {
@@ -1881,7 +1890,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
     const int b0 = c0 - s_hoff[f0];
     if (c0 < nc && b0 > 0) cutm1 = d.cuts[f0 * kMaxBins + b0 - 1];
   }
-  if (!built) {  // materialise the sibling histogram for the next level
+  if (level + 1 < d.max_depth) {  // this node's histogram, for its children's subtraction
 #pragma unroll
     for (int k = 0; k < kEvalCPT; ++k) {
       const int c = c0 + k;
@@ -2277,6 +2286,7 @@ struct GbdtCtx {
   std::vector<void*> allocs;
   // k_eval<false> feature -> (wave, slot) table: 32 slots of 8 bits (0xFF = empty), see eval_assignment
   uint64_t eval_asg[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  EvalSlots eval_slots{};  // the table with each slot's bin count and compact offset (k_eval<false> arguments)
   std::vector<int32_t> hoff_h;  // host copy of d.hoff (sizes k_eval's fused-exchange LDS)
   // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
   const char* stamp_path = nullptr;
@@ -2475,7 +2485,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.ridx[1], N * sizeof(int32_t)))) return rc;
   for (int k = 0; k < 2; ++k) {
     if ((rc = dev_alloc(c, (void**)&d.hist_b[k], hist_bytes))) return rc;
-    if ((rc = dev_alloc(c, (void**)&d.hist_s[k], hist_bytes))) return rc;
+    if ((rc = dev_alloc(c, (void**)&d.hist_s[k], 2 * hist_bytes))) return rc;  // node-indexed
   }
   if ((rc = dev_alloc(c, (void**)&d.nodes_buf[0], c->max_nodes * sizeof(Node)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.nodes_buf[1], c->max_nodes * sizeof(Node)))) return rc;
@@ -2597,6 +2607,12 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   CK(hipMemcpy(c->d.hoff, hoff.data(), (F + 1) * sizeof(int32_t), hipMemcpyHostToDevice));
   c->hoff_h = hoff;
   eval_assignment(nb, c->eval_asg);
+  for (int k = 0; k < 32; ++k) {
+    const uint32_t f = (uint32_t)((c->eval_asg[k / 8] >> (8 * (k % 8))) & 0xFFu);
+    c->eval_slots.w[k] = (f == 0xFFu || (int)f >= F)
+                             ? 0xFFu
+                             : f | ((uint32_t)std::min(std::max(nb[f], 0), 511) << 8) | ((uint32_t)hoff[f] << 17);
+  }
   c->d.ncells = hoff[F];
   c->d.slot_elems = (int64_t)(hoff[F] + 1) * 2;
   CK(hipMemcpy(c->d.tile_entries, ent.data(), ntiles * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -2644,7 +2660,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   }
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const int ft4 = hist_ft4(d);
-  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && d.ablate == 0 &&
+  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.ablate == 0 || d.ablate >= 10) &&
                          getenv("COBALT_NO_FUSED_ROOT") == nullptr;
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
@@ -2766,20 +2782,20 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         const int ng = ceil_div(d.F, eval_fg);
         if (d.ipc_epoch)
           GLAUNCH("k_eval", (k_eval<true, true>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), fused_lds,
-                  stream, d, level, parity, t, eval_fg, 0ull, 0ull, 0ull, 0ull);
+                  stream, d, level, parity, t, eval_fg, EvalSlots{});
         else
           GLAUNCH("k_eval", (k_eval<true, false>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream,
-                  d, level, parity, t, eval_fg, 0ull, 0ull, 0ull, 0ull);
+                  d, level, parity, t, eval_fg, EvalSlots{});
         GLAUNCH("k_eval_finish", k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
       } else if (eval_compact) {
         GLAUNCH("k_eval", k_eval_compact, dim3(1 << level), dim3(kEvalThreads), 0, stream, d, level, parity, t);
       } else {
         if (d.ipc_epoch)
           GLAUNCH("k_eval", (k_eval<false, true>), dim3(1 << level), dim3(1024), fused_lds, stream, d, level, parity,
-                  t, d.F, c->eval_asg[0], c->eval_asg[1], c->eval_asg[2], c->eval_asg[3]);
+                  t, d.F, c->eval_slots);
         else
           GLAUNCH("k_eval", (k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F,
-                  c->eval_asg[0], c->eval_asg[1], c->eval_asg[2], c->eval_asg[3]);
+                  c->eval_slots);
       }
       d.ipc_epoch = 0;
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
