@@ -1505,10 +1505,22 @@ struct EvalSlots {
   uint32_t w[32];
 };
 
-template <bool kGroups, bool kFused>
-__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg, EvalSlots es) {
-  BlockStamp stamp_(d);
-  const int pos = blockIdx.x;
+// A node's best split candidate, reduced over the block (eval_core's result, in LDS).
+struct EvalOut {
+  Cand best;
+  float cut;
+  int nb;           // the winner's bin count (0 without a candidate)
+  int64_t G, H;     // node totals
+};
+
+// Split evaluation of node `pos` of the level by the whole (1024-thread) block. Returns false (in every
+// thread) for an inactive node or a failed exchange; otherwise thread 0 holds the result in *s_out (the
+// other threads see it after a barrier). Shared by k_eval and the fused evaluation + partition pass.
+// `kMerged` (k_eval_part): the node counts as active whatever its status (another block of the same
+// node may already have finalised it), and only `store_hist` blocks store its histogram.
+template <bool kGroups, bool kFused, bool kMerged = false>
+__device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parity, int tree, int fg, const EvalSlots& es,
+                                          int pos, BlockStamp& stamp_, EvalOut* s_out, bool store_hist = true) {
   const int fbeg = kGroups ? blockIdx.y * fg : 0;
   const int fend = kGroups ? min(d.F, fbeg + fg) : d.F;
   const int n = (1 << level) - 1 + pos;
@@ -1568,7 +1580,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     cb = kGroups ? d.hoff[fbeg] : 0;
     const int ce = kGroups ? d.hoff[fend] : d.ncells;
     if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
-    if (!ipc_wait(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout)) return;
+    if (!ipc_wait(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout)) return false;
     // the global root totals are stored at level 0 (k_eval_finish reads them)
     ipc_sum_cells_n(__builtin_amdgcn_readfirstlane(iv->n), iv, (int64_t)pair * SE * (int64_t)sizeof(int64_t), cb,
                     ce - cb + 1, d.ncells, s_cells, reinterpret_cast<longlong2*>(d.hist_b[parity] + pair * SE),
@@ -1582,7 +1594,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
   // No early return for an inactive node: a branch here let hipcc sink the feature metadata loads
   // below it (a third dependent round trip). Its block computes on valid buffers and stores nothing.
-  const bool active = status == kActive;
+  const bool active = kMerged ? status != kNone : status == kActive;
   stamp_.probe(1);
   __shared__ Cand s_best[16];
   __shared__ float s_cut[16];
@@ -1671,7 +1683,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     if (!e.on) continue;
     const int f = e.f, nb = e.nb;
     const int nch = (nb + kWave - 1) / kWave;  // wave-uniform
-    if (active && level + 1 < d.max_depth) {  // this node's histogram, for its children's subtraction
+    if (active && store_hist && level + 1 < d.max_depth) {  // this node's histogram, for its children's subtraction
       longlong2* hs2 = reinterpret_cast<longlong2*>(hs);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -1753,17 +1765,36 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   }
   }
   stamp_.probe(2);
-  if (!active) return;  // block-uniform
+  if (!active) return false;  // block-uniform
   wave_best(best, best_cut);
   if (lane == 0) { s_best[wave_id()] = best; s_cut[wave_id()] = best_cut; }
   __syncthreads();
   stamp_.probe(3);
-  if (wave_id() != 0) return;
-  // the waves' winners, one per lane of wave 0, reduced by the same DPP arg-max
-  if (lane < nw) { best = s_best[lane]; best_cut = s_cut[lane]; }
-  else { best.gain = -INFINITY; best.key = 0x7fffffff; best.gl = 0; best.hl = 0; best_cut = -FLT_MAX; }
-  wave_best(best, best_cut);
-  if (lane != 0) return;
+  if (wave_id() == 0) {
+    // the waves' winners, one per lane of wave 0, reduced by the same DPP arg-max
+    if (lane < nw) { best = s_best[lane]; best_cut = s_cut[lane]; }
+    else { best.gain = -INFINITY; best.key = 0x7fffffff; best.gl = 0; best.hl = 0; best_cut = -FLT_MAX; }
+    wave_best(best, best_cut);
+    if (lane == 0) {
+      s_out->best = best;
+      s_out->cut = best_cut;
+      s_out->nb = (!kGroups && best.key != 0x7fffffff) ? s_nb[(best.key >> 10) & 31] : 0;
+      s_out->G = G;
+      s_out->H = H;
+    }
+  }
+  return true;
+}
+
+template <bool kGroups, bool kFused>
+__global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg, EvalSlots es) {
+  BlockStamp stamp_(d);
+  const int pos = blockIdx.x;
+  __shared__ EvalOut s_out;
+  if (!eval_core<kGroups, kFused>(d, level, parity, tree, fg, es, pos, stamp_, &s_out)) return;
+  if (threadIdx.x != 0) return;  // thread 0 wrote s_out
+  const Cand best = s_out.best;
+  const float best_cut = s_out.cut;
   if (kGroups) {
     CandRec& o = d.cand[(int64_t)pos * gridDim.y + blockIdx.y];
     o.gain = best.gain;
@@ -1773,7 +1804,7 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     o.hl = best.hl;
     return;
   }
-  eval_finalize(d, level, n, G, H, best, best_cut, best.key != 0x7fffffff ? s_nb[(best.key >> 10) & 31] : 0);
+  eval_finalize(d, level, (1 << level) - 1 + pos, s_out.G, s_out.H, best, best_cut, s_out.nb);
   stamp_.probe(4);
 }
 
@@ -2115,6 +2146,128 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
     const uint64_t lm = __ballot(left != 0u), vm = __ballot(valid);
     const uint32_t rk_l = mask_rank(lm);
     // valid lanes are a prefix: a right row's rank among the right rows is lane - rk_l
+    const uint32_t dst = rk_l + (left ? pl_ : pr_ - (uint32_t)lane);
+    if (valid) nxt[dst] = r[k];
+    const uint32_t cl = (uint32_t)__popcll(lm);
+    pl_ += cl;
+    pr_ -= (uint32_t)__popcll(vm) - cl;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Split evaluation fused with the row partition (one GPU, < 4M rows, levels 0 .. max_depth - 2).
+// At small row counts a level is a chain of short launches whose fixed costs dominate (1M rows:
+// k_eval ~6.6 us + a ~1.5 us boundary per level), so every block of the partition pass evaluates its
+// OWN node (the same eval_core, redundantly: ~2 us of fp64 work per block on its own CU, with the
+// node's ~42 KB of histograms hot in L2) and partitions its rows by the result -- one launch per level
+// fewer. The item's row ids are loaded before the evaluation (they do not depend on the split), so
+// their latency hides behind it. The block holding the node's first item finalises the node record
+// and stores its histogram for the children (eval_finalize / eval_core's store, as k_eval does).
+// The plan covers every node of the level with rows (a block that finalised its node changes the
+// status from active to split / leaf; the other blocks accept any status but kNone). A leaf's blocks
+// stop after the evaluation.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool split_decision(const GbdtDev& d, const Cand& best, int nb, int& f, int& j, bool& dl) {
+  const float loss = (float)best.gain;
+  const bool ok = best.key != 0x7fffffff && loss > 1e-6f && loss >= (float)d.gamma;
+  f = best.key >> 10;
+  const int r = best.key & 1023;
+  if (r < 512) { j = r; dl = false; } else { j = (nb - 1 - (r - 512)) - 1; dl = true; }
+  return ok;
+}
+
+template <int kSteps>
+__global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64_t zero_next, int level, int chunk,
+                                                    int tree, EvalSlots es) {
+  constexpr int kPW = 16;  // waves
+  BlockStamp stamp_(d);
+  __shared__ int32_t s_cnt[2][kPW];
+  __shared__ int32_t s_base[2];
+  __shared__ int s_plan[5];
+  __shared__ EvalOut s_out;
+  {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
+    int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
+    const int64_t nz = zero_next / 2;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
+      zp[e] = make_int4(0, 0, 0, 0);
+  }
+  const int item = blockIdx.x;
+  const int first = (1 << level) - 1;
+  const PlanOut pl = block_plan(1 << level, chunk, item, [&](int e) {
+    const Node& n = d.nodes[first + e];
+    const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
+    return (st != kNone && cnt > 0) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
+  }, s_plan);
+  if (pl.node < 0) return;
+  const int node = pl.node;
+  // the item's row ids and the node's range: independent of the split, in flight during the evaluation
+  const bool identity = parity == 0 && node == 0;
+  const int32_t* cur = d.ridx[parity];
+  int32_t* nxt = d.ridx[parity ^ 1];
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
+  const int len = pl.end - pl.begin;
+  const int per = ((len + kPW - 1) / kPW + kWave - 1) / kWave * kWave;
+  const int wb = min(pl.end, pl.begin + wv * per), we = min(pl.end, wb + per);
+  int r[kSteps];
+#pragma unroll
+  for (int k = 0; k < kSteps; ++k) {
+    const int i = wb + k * kWave + lane;
+    const int ic = min(i, pl.end - 1);
+    const int rv = identity ? ic : cur[ic];
+    r[k] = i < we ? rv : -1;
+  }
+  const int nstart = d.nodes[node].start, ncount = d.nodes[node].count;
+  const bool lead = pl.begin == nstart;  // the node's first item
+  eval_core<false, false, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, lead);
+  __syncthreads();
+  const Cand best = s_out.best;
+  int f, j;
+  bool dlb;
+  const bool ok = split_decision(d, best, s_out.nb, f, j, dlb);
+  if (lead && threadIdx.x == 0) eval_finalize(d, level, node, s_out.G, s_out.H, best, s_out.cut, s_out.nb);
+  stamp_.probe(4);
+  if (!ok) return;  // a leaf: its rows are not routed (block-uniform)
+  const uint8_t* col = d.binsT + (int64_t)f * d.ldt;
+  uint8_t bv[kSteps];
+#pragma unroll
+  for (int k = 0; k < kSteps; ++k) bv[k] = col[max(r[k], 0)];
+  // pass 1 / claim / pass 2: k_partition's integer-arithmetic form
+  const int jm1 = j + 1;
+  const uint32_t dlv = dlb ? 1u : 0u;
+  const int nv = max(0, we - wb);
+  uint32_t lbits = 0;
+  int nl = 0;
+#pragma unroll
+  for (int k = 0; k < kSteps; ++k) {
+    const uint32_t b = bv[k];
+    const uint32_t lt = (uint32_t)((int)b - jm1) >> 31;
+    const uint32_t ms = (b + 1u) >> 8;
+    const uint32_t okr = ~(uint32_t)r[k] >> 31;
+    const uint32_t left = (lt | (ms & dlv)) & okr;
+    lbits |= left << k;
+    nl += __popcll(__ballot(left != 0u));
+  }
+  if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nv - nl; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tl = 0, tr = 0;
+    for (int k = 0; k < kPW; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
+    const unsigned long long c = atomicAdd(reinterpret_cast<unsigned long long*>(d.cursors + 2 * node),
+                                           ((unsigned long long)(uint32_t)tr << 32) | (uint32_t)tl);
+    s_base[0] = (int32_t)(uint32_t)c;
+    s_base[1] = (int32_t)(c >> 32);
+  }
+  __syncthreads();
+  int bl = s_base[0], br = s_base[1];
+  for (int k = 0; k < wv; ++k) { bl += s_cnt[0][k]; br += s_cnt[1][k]; }
+  uint32_t pl_ = (uint32_t)(nstart + bl);
+  uint32_t pr_ = (uint32_t)(nstart + ncount - 1 - br);
+#pragma unroll
+  for (int k = 0; k < kSteps; ++k) {
+    const bool valid = r[k] >= 0;
+    const uint32_t left = (lbits >> k) & 1u;
+    const uint64_t lm = __ballot(left != 0u), vm = __ballot(valid);
+    const uint32_t rk_l = mask_rank(lm);
     const uint32_t dst = rk_l + (left ? pl_ : pr_ - (uint32_t)lane);
     if (valid) nxt[dst] = r[k];
     const uint32_t cl = (uint32_t)__popcll(lm);
@@ -2692,6 +2845,15 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part && fused_lds <= 65536;
   d.ipc_epoch = 0;
   d.ipcv = ipc_fused ? ipc_device_views(cc) : nullptr;
+  // split evaluation fused into the partition pass (k_eval_part): one launch per level fewer, but every
+  // partition block repeats its node's evaluation, so only while the level's items fit one block per CU
+  // (1M rows: 248.0 -> 239.3 us per tree in the stamps; 1.25M: 87.0 -> 96.3 ms per fit, 2.5M 112 -> 130:
+  // two evaluations per CU). COBALT_EVAL_PART=0 / 2 disables / forces it.
+  static const int env_ep = getenv("COBALT_EVAL_PART") ? atoi(getenv("COBALT_EVAL_PART")) : 1;
+  const int ep_steps = ceil_div(chunk_part(d), 16 * kWave);
+  const bool eval_part = env_ep != 0 && !dp && eval_fg == 0 && !eval_compact && !fuse_part && part_wide(d) &&
+                         ep_steps <= 8 && d.F <= 32 &&
+                         (env_ep == 2 || ceil_div(d.n, chunk_part(d)) <= device_cu_count());
   d.zero_red = nullptr;
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
@@ -2778,7 +2940,9 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         }
         if (rc) return rc;
       }
-      if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
+      const bool ep_level = eval_part && level + 1 < D;  // this level's evaluation runs in k_eval_part
+      if (ep_level) {
+      } else if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
         const int ng = ceil_div(d.F, eval_fg);
         if (d.ipc_epoch)
           GLAUNCH("k_eval", (k_eval<true, true>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), fused_lds,
@@ -2807,7 +2971,13 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         d.zero_red = ipc_fused ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
         const int pw = part_wide(d) ? 16 : 4;
         const int steps = ceil_div(chp, pw * kWave);  // <= kPartSteps (chunk_part's cap)
-        if (pw == 16 && steps <= 4)
+        if (ep_level && steps <= 4)
+          GLAUNCH("k_eval_part", k_eval_part<4>, dim3(ubp), dim3(1024), 0, stream, d, parity, zero_next, level, chp, t,
+                  c->eval_slots);
+        else if (ep_level)
+          GLAUNCH("k_eval_part", k_eval_part<8>, dim3(ubp), dim3(1024), 0, stream, d, parity, zero_next, level, chp, t,
+                  c->eval_slots);
+        else if (pw == 16 && steps <= 4)
           GLAUNCH("k_partition", (k_partition<16, 4>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
                   level, chp);
         else if (pw == 16 && steps <= 8)
