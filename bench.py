@@ -96,6 +96,17 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     elapsed = ctx.allreduce_scalar(elapsed, "max", dev)
 
+    # (outside the timed region) data parallel: every rank must hold the same model -- a 52-bit digest
+    # of the last fit's UBJSON, compared by a min / max all-reduce
+    replicas_agree = None
+    if world > 1 and booster is not None:
+        import hashlib
+
+        h = float(int.from_bytes(hashlib.sha256(booster.save_raw("ubj")).digest()[:8], "little") >> 12)
+        replicas_agree = ctx.allreduce_scalar(h, "min", dev) == ctx.allreduce_scalar(h, "max", dev)
+        if not replicas_agree and rank == 0:
+            print("[bench] ERROR: data-parallel ranks hold different models", file=sys.stderr)
+
     auc = None
     if rank == 0 and booster is not None:
         Xt, yt = synth.make_lendingclub(a.test_rows, seed=a.seed, row_offset=n_global, device=dev)
@@ -138,6 +149,7 @@ def main() -> None:
             "rows_global": n_global,
             "sketch_rows": a.sketch_rows or "all",
             "dp_transport": ctx.transport if world > 1 else None,
+            "replicas_agree": replicas_agree,
             "auc": None if auc is None else round(auc, 5),
             "test_rows": a.test_rows,
             "fit_breakdown_ms": {

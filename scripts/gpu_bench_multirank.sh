@@ -20,5 +20,6 @@ a = json.loads(open(f"gpurun_out/bench_multirank_{n}.json").read().strip().split
 b = json.loads(open("gpurun_out/bench_multirank_1.json").read().strip().splitlines()[-1])
 assert a["n_gpus"] == int(n) and a["dp_transport"] == "ipc", a
 assert a["auc"] == b["auc"], (a["auc"], b["auc"])
+assert a["replicas_agree"] is True, a  # every rank holds the same model
 print(f"ranks {n}: {a['ms_per_step']} ms/fit (all ranks on one GPU), 1 rank {b['ms_per_step']} ms; AUC {a['auc']} equal")
 PY

@@ -55,3 +55,4 @@ def test_bench_two_gloo_ranks_one_json_line_and_same_auc():
     assert got["metric"] == ref["metric"]
     assert got["value"] > 0 and got["ms_per_step"] > 0
     assert got["auc"] == ref["auc"]
+    assert got["replicas_agree"] is True  # both ranks hold the same model (digest min == max)
