@@ -3084,11 +3084,73 @@ COBALT_API int cobalt_gbdt_destroy(void* h) {
 
 // Quantise n rows into row records (pitch `stride`) and feature-major bins with row pitch `ldt`
 // (ldt = n for a whole matrix; the full row count when a streamed chunk is binned in place).
+// 32-byte records of <= 24 features with 16-byte aligned fp32 rows (F % 4 == 0, ldx == F): lane = row,
+// the row read as F / 4 float4 loads (one 64-lane instruction spans 64 consecutive rows, so the F / 4
+// loads of a wave use every byte of the lines they touch), the bins of all features searched in LDS,
+// the WHOLE record written as two 16-byte stores (bins | zero pad and (g, h): no separate memset of the
+// record array) and the feature-major bytes as one coalesced byte store per feature.
+template <int F4>
+__global__ __launch_bounds__(256) void k_bin_rec32(const float* __restrict__ X, int64_t n,
+                                                   const float* __restrict__ cuts, const int32_t* __restrict__ nbins,
+                                                   uint8_t* __restrict__ bins, uint8_t* __restrict__ binsT,
+                                                   int64_t ldt) {
+  constexpr int F = 4 * F4;
+  __shared__ float s_cuts[F * kMaxBins];
+  __shared__ int s_nb[F];
+  for (int i = threadIdx.x; i < F * kMaxBins; i += blockDim.x) s_cuts[i] = cuts[i];
+  if (threadIdx.x < F) s_nb[threadIdx.x] = nbins[threadIdx.x];
+  __syncthreads();
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < n;
+       row += (int64_t)gridDim.x * blockDim.x) {
+    const float4* x4 = reinterpret_cast<const float4*>(X + row * F);
+    float v[F];
+#pragma unroll
+    for (int q = 0; q < F4; ++q) {
+      const float4 t = x4[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    }
+    uint32_t w[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const int nb = s_nb[f];
+      uint32_t b;
+      if (v[f] != v[f]) {
+        b = kMissingBin;
+      } else {  // upper_bound over cuts[f][0..nb), clamped to nb - 1
+        const float* c = s_cuts + f * kMaxBins;
+        int lo = 0, hi = nb;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (c[mid] <= v[f]) lo = mid + 1; else hi = mid;
+        }
+        b = lo >= nb ? (uint32_t)(nb - 1) : (uint32_t)lo;
+      }
+      binsT[(int64_t)f * ldt + row] = (uint8_t)b;
+      w[f >> 2] |= b << (8 * (f & 3));
+    }
+    uint4* rec = reinterpret_cast<uint4*>(bins + row * 32);
+    rec[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    rec[1] = make_uint4(w[4], w[5], 0u, 0u);
+  }
+}
+
 COBALT_API int cobalt_bin_matrix_ld(const float* X, int64_t n, int F, int64_t ldx, const float* cuts,
                                     const int32_t* nbins, uint8_t* bins, int stride, uint8_t* binsT, int64_t ldt,
                                     hipStream_t stream) {
   if (stride % 4 != 0 || stride < F || ldt < n) return -3;
   const int grid = std::max(1, std::min(ceil_div(n, 256), 256 * 8));
+  // 32-byte records of 16-byte aligned rows: the vectorised kernel (10M x 20: 1.37 ms with k_bin)
+  if (stride == 32 && ldx == F && F % 4 == 0 && F >= 4 && F <= 24 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(bins) & 15) == 0 && getenv("COBALT_BIN_SCALAR") == nullptr) {
+    switch (F / 4) {
+#define BIN_CASE(K) \
+      case K: hipLaunchKernelGGL(k_bin_rec32<K>, dim3(grid), dim3(256), 0, stream, X, n, cuts, nbins, bins, binsT, ldt); break;
+      BIN_CASE(1) BIN_CASE(2) BIN_CASE(3) BIN_CASE(4) BIN_CASE(5) BIN_CASE(6)
+#undef BIN_CASE
+    }
+    CK_LAUNCH();
+    return 0;
+  }
   const size_t lds = (size_t)F * kMaxBins * sizeof(float);
   if (lds <= 64 * 1024) {
     hipLaunchKernelGGL(k_bin<true>, dim3(grid), dim3(256), lds, stream, X, n, F, ldx, cuts, nbins, bins, stride, binsT,

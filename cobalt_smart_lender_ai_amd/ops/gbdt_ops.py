@@ -7,6 +7,8 @@ the current HIP stream without host synchronisation; ``fetch`` copies the node r
 """
 from __future__ import annotations
 
+import os
+
 import ctypes
 
 import numpy as np
@@ -74,7 +76,11 @@ def bin_matrix(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> tupl
     X = X.contiguous()
     N, F = X.shape
     st = row_stride(F)
-    bins = torch.zeros((N, st), dtype=torch.uint8, device=X.device)
+    # the vectorised kernel (k_bin_rec32: 32-byte records, F % 4 == 0, 16-byte aligned rows) writes
+    # every byte of every record; the generic one only the bins
+    whole = (st == 32 and F % 4 == 0 and F <= 24 and X.data_ptr() % 16 == 0
+             and not os.environ.get("COBALT_BIN_SCALAR"))
+    bins = (torch.empty if whole else torch.zeros)((N, st), dtype=torch.uint8, device=X.device)
     binsT = torch.empty((F, N), dtype=torch.uint8, device=X.device)
     lib = _native.lib()
     rc = lib.cobalt_bin_matrix(X.data_ptr(), N, F, F, cuts.contiguous().data_ptr(),

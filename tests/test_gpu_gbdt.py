@@ -33,6 +33,21 @@ def test_bin_matrix_matches_host():
     F = X.shape[1]
     assert np.array_equal(bins[:, :F].cpu().numpy(), ref)
     assert np.array_equal(binsT.cpu().numpy(), ref.T)
+    assert not bins[:, F:].any()  # the vectorised kernel writes whole records: zero pad and (g, h)
+
+
+@pytest.mark.parametrize("F", [4, 7, 12, 21])
+def test_bin_matrix_other_widths_match_host(F):
+    """Record widths on both binning kernels (F % 4 == 0 and <= 24: the vectorised k_bin_rec32)."""
+    from cobalt_smart_lender_ai_amd.ops import gbdt_ops
+
+    X, _ = _data(20_011, seed=F)
+    X = X[:, :F].contiguous() if F <= X.shape[1] else torch.cat([X, X[:, : F - X.shape[1]] * 1.5], 1).contiguous()
+    cuts, nb = sketch.compute_cuts(X, 256)
+    bins, binsT = gbdt_ops.bin_matrix(X.cuda(), cuts.cuda(), nb.cuda())
+    ref = sketch.bin_matrix_host(X.numpy(), cuts.numpy(), nb.numpy())
+    assert np.array_equal(bins[:, :F].cpu().numpy(), ref)
+    assert np.array_equal(binsT.cpu().numpy(), ref.T)
 
 
 def test_sketch_gpu_equals_cpu():
