@@ -90,6 +90,22 @@ def feature_max_bins(max_bin: int, has_missing: torch.Tensor) -> torch.Tensor:
                        torch.tensor(full, device=has_missing.device)).to(torch.int64)
 
 
+def _row_cumsum(x: torch.Tensor, block: int = 1024) -> torch.Tensor:
+    """Inclusive int64 prefix sums along dim 1 of a [F, S] tensor, as a two-level scan over blocks of
+    ``block`` columns (torch's single-pass scan of a few long rows ran at 0.6 ms for 20 x 2^18 on the
+    GPU: one block per row). Integer arithmetic: identical to ``torch.cumsum(x, 1)``."""
+    F, S = x.shape
+    x = x.to(torch.int64)
+    if S <= 4 * block:
+        return torch.cumsum(x, 1)
+    nb = -(-S // block)
+    pad = nb * block - S
+    xb = torch.nn.functional.pad(x, (0, pad)).view(F, nb, block)
+    inner = torch.cumsum(xb, 2)
+    base = torch.cumsum(inner[:, :, -1], 1) - inner[:, :, -1]                   # exclusive block prefixes
+    return (inner + base[:, :, None]).view(F, nb * block)[:, :S]
+
+
 def compute_cuts(sample: torch.Tensor, max_bin: int = 256, weights: torch.Tensor | None = None,
                  has_missing: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """Cut table ``[F, 256]`` float32 and ``nbins [F]`` int32 from a ``[S, F]`` float32 sample.
@@ -107,14 +123,15 @@ def compute_cuts(sample: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     if S == 0:
         return (torch.full((F, 256), FLT_MAX, dtype=torch.float32, device=dev),
                 torch.ones(F, dtype=torch.int32, device=dev))
-    srt = torch.sort(sample.to(torch.float32), dim=0)                          # NaN last
-    xs = srt.values.t().contiguous()                                           # [F, S]
+    # feature-major first: one contiguous segment per feature for the segmented sort
+    srt = torch.sort(sample.to(torch.float32).t().contiguous(), dim=1)         # NaN last
+    xs = srt.values                                                            # [F, S]
     valid = ~torch.isnan(xs)
     cnt = valid.sum(1)                                                          # [F]
     dflag = valid.clone()
     dflag[:, 1:] &= xs[:, 1:] != xs[:, :-1]
     nd = dflag.sum(1)                                                           # distinct count
-    rank = torch.cumsum(dflag.to(torch.int64), 1) - 1
+    rank = _row_cumsum(dflag) - 1
     exact = nd <= maxb
     # Both paths are computed for every feature and selected per feature after, and the cut slots are
     # written by scatters into a trash column 256 instead of nonzero() gathers: no host synchronisation
@@ -128,8 +145,8 @@ def compute_cuts(sample: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
 
     # weighted-quantile path
     wq = quantize_weights(weights, S, dev)                                      # [S] int64
-    ws = wq[srt.indices.t()] * valid                                            # [F, S], 0 for NaN
-    cum = torch.cumsum(ws, 1)                                                   # exact int64
+    ws = wq[srt.indices] * valid                                                # [F, S], 0 for NaN
+    cum = _row_cumsum(ws)                                                       # exact int64
     W = cum[:, -1]                                                              # [F]
     k = torch.arange(1, MAX_BINS, device=dev, dtype=torch.int64)                # j = 1..255
     # first i with cum_i * maxb > j * W  ==  searchsorted(cum * maxb, j * W, right)
