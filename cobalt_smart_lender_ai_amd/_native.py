@@ -39,6 +39,7 @@ class NativeUnavailable(RuntimeError):
 _SIGS: dict[str, tuple] = {
     # gbdt.hip
     "cobalt_gbdt_create": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    "cobalt_heap_to_trees": (ctypes.c_int64, [c_void_p, c_int, c_int] + [c_void_p] * 10),
     "cobalt_gbdt_set_data": (c_int, [c_void_p] * 9),
     "cobalt_gbdt_grow": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "cobalt_gbdt_fetch_trees": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),

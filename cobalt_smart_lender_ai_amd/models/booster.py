@@ -541,9 +541,16 @@ def iter_leaf_paths(t: Tree) -> Iterable[tuple[int, list[tuple[int, int, bool]]]
         stack.append((int(t.left_children[j]), path + [(j, f, True)]))
 
 
-def trees_from_heap_nodes(nodes: np.ndarray, max_depth: int) -> list[Tree]:
+def trees_from_heap_nodes(nodes: np.ndarray, max_depth: int, native: bool | None = None) -> list[Tree]:
     """Convert heap-ordered node records (NODE_DTYPE, [T, 2^(D+1)-1]) of the trainer into XGBoost
-    trees, numbering nodes in XGBoost's depthwise creation order (children allocated in pairs)."""
+    trees, numbering nodes in XGBoost's depthwise creation order (children allocated in pairs).
+
+    ``native`` (default: whenever the native library is loadable): the one-pass C++ conversion
+    (``csrc/treeconv.cpp``, ~0.1 ms for 300 trees); False: the NumPy form below (its oracle)."""
+    if native is not False and nodes.ndim == 2 and nodes.shape[0] > 0:
+        out = _trees_from_heap_nodes_native(nodes, required=native is True)
+        if out is not None:
+            return out
     # Heap indices of one level are contiguous and children are allocated in parent order, so the
     # depthwise creation order is simply ascending heap index over the live nodes.
     # Everything is computed for all trees at once and split per tree at the end.
@@ -562,7 +569,10 @@ def trees_from_heap_nodes(nodes: np.ndarray, max_depth: int) -> list[Tree]:
     parent_heap = (np.arange(M) - 1) // 2
     has_par = np.arange(M) > 0
     par_full[:, has_par] = new_id[:, parent_heap[has_par]]
-    r = nodes[live]
+    # the live records gathered as 64-byte rows of an int32 view (a boolean mask on the structured
+    # array copied field by field: ~4 ms for 300 trees)
+    words = np.ascontiguousarray(nodes).reshape(-1).view(np.int32).reshape(-1, NODE_DTYPE.itemsize // 4)
+    r = words[np.flatnonzero(live.reshape(-1))].view(NODE_DTYPE).reshape(-1)
     split = r["status"] == 2
     lc, rc, par = lc_full[live], rc_full[live], par_full[live]
     si = np.where(split, r["feat"], 0).astype(np.int32)
@@ -571,9 +581,41 @@ def trees_from_heap_nodes(nodes: np.ndarray, max_depth: int) -> list[Tree]:
     lo = np.where(split, r["loss_chg"], 0).astype(np.float32)
     bw = r["base_weight"].astype(np.float32)
     sh = r["sum_hess"].astype(np.float32)
-    cuts = np.cumsum(counts)[:-1]
-    cols = [np.split(a, cuts) for a in (lc, rc, par, si, sc, dl, bw, lo, sh)]
-    return [Tree(*parts) for parts in zip(*cols)]
+    # per-tree views by offsets (np.split's per-piece swapaxes cost ~9 ms for 300 x 9 arrays)
+    ends = np.cumsum(counts).tolist()
+    begins = [0] + ends[:-1]
+    cols = (lc, rc, par, si, sc, dl, bw, lo, sh)
+    return [Tree(*(a[b0:b1] for a in cols)) for b0, b1 in zip(begins, ends)]
+
+
+def _trees_from_heap_nodes_native(nodes: np.ndarray, required: bool = False) -> list[Tree] | None:
+    try:
+        from .. import _native
+
+        lib = _native.lib()
+    except Exception:  # noqa: BLE001 -- no native library (source-only CPU install): NumPy path
+        if required:
+            raise
+        return None
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    T, M = nodes.shape
+    cap = T * M
+    counts = np.empty(T, np.int32)
+    cols = [np.empty(cap, dt) for dt in (np.int32, np.int32, np.int32, np.int32, np.float32, np.uint8,
+                                         np.float32, np.float32, np.float32)]
+    lc, rc, par, si, sc, dl, bw, lo, sh = cols
+    n = lib.cobalt_heap_to_trees(nodes.ctypes.data, T, M, counts.ctypes.data,
+                                 *(a.ctypes.data for a in cols))
+    if n < 0:
+        raise RuntimeError("cobalt_heap_to_trees: bad arguments")
+    ends = np.cumsum(counts).tolist()
+    begins = [0] + ends[:-1]
+    # Tree fields in their declared order: left, right, parents, split_indices, split_conditions,
+    # default_left, base_weights, loss_changes, sum_hessian
+    order = (lc, rc, par, si, sc, dl, bw, lo, sh)
+    spans = list(zip(begins, ends))
+    per_col = [[a[b0:b1] for b0, b1 in spans] for a in order]
+    return [Tree(*parts) for parts in zip(*per_col)]
 
 
 NODE_DTYPE = np.dtype([

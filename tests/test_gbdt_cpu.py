@@ -235,3 +235,33 @@ def test_training_job_pickle_has_reference_opcode_skeleton(reference_model_bytes
           "gamma": 5, "subsample": 1.0, "colsample_bytree": 1.0, "eval_metric": "logloss",
           "kwargs": {"use_label_encoder": False}}
     assert _pickle_skeleton(dump_pickle_bytes(b, sk)) == _pickle_skeleton(reference_model_bytes)
+
+
+def test_native_tree_conversion_equals_numpy():
+    """csrc/treeconv.cpp (the per-fit heap -> XGBoost tree conversion) equals the NumPy form."""
+    from cobalt_smart_lender_ai_amd.models.booster import NODE_DTYPE, trees_from_heap_nodes
+
+    rng = np.random.default_rng(5)
+    T, D = 40, 6
+    M = 2 ** (D + 1) - 1
+    nodes = np.zeros((T, M), dtype=NODE_DTYPE)
+    for t in range(T):
+        st = nodes["status"][t]
+        st[0] = 2 if t % 7 else 3  # some single-leaf trees
+        for i in range(M):
+            if st[i] == 2:
+                for c in (2 * i + 1, 2 * i + 2):
+                    lvl = int(np.log2(c + 1))
+                    st[c] = 2 if (lvl < D and rng.random() < 0.7) else 3
+    for f, dt in (("feat", np.int32), ("default_left", np.int32)):
+        nodes[f] = rng.integers(0, 2 if f == "default_left" else 30, (T, M)).astype(dt)
+    for f in ("split_cond", "loss_chg", "leaf_value", "sum_hess", "base_weight"):
+        nodes[f] = rng.standard_normal((T, M)).astype(np.float32)
+    a = trees_from_heap_nodes(nodes, D, native=True)
+    b = trees_from_heap_nodes(nodes, D, native=False)
+    assert len(a) == len(b) == T
+    for ta, tb in zip(a, b):
+        for k in ("left_children", "right_children", "parents", "split_indices", "split_conditions",
+                  "default_left", "base_weights", "loss_changes", "sum_hessian"):
+            x, y = getattr(ta, k), getattr(tb, k)
+            assert x.dtype == y.dtype and np.array_equal(x, y), k
