@@ -46,6 +46,7 @@ _SIGS: dict[str, tuple] = {
     "cobalt_gbdt_max_nodes": (c_int, [c_void_p]),
     "cobalt_gbdt_set_start": (c_int, [c_void_p, c_int]),
     "cobalt_gbdt_destroy": (c_int, [c_void_p]),
+    "cobalt_gbdt_reuse": (c_int, [c_void_p, c_void_p]),
     "cobalt_gbdt_grow_sampled": (c_int, [c_void_p, c_int, c_void_p]),
     "cobalt_gbdt_set_rows": (c_int, [c_void_p, c_int64]),
     "cobalt_gbdt_tree_ptr": (c_void_p, [c_void_p, c_int]),

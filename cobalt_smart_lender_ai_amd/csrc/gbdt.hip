@@ -3074,6 +3074,39 @@ COBALT_API int cobalt_gbdt_set_start(void* h, int t0) {
   return 0;
 }
 
+// Re-arm a trainer context for a new fit with the same shapes (rows, features, record pitch, depth,
+// tree capacity, item size, tile, communicator): the per-fit scalars come from `cfg`, the tree count
+// restarts at 0, and the device buffers -- hundreds of MB at 10M rows -- are kept instead of freed and
+// reallocated (models/gbdt.py fits back to back: ~2.5 ms of hipFree + hipMalloc per fit). Returns 1 when
+// the shapes differ (the caller creates a new context).
+COBALT_API int cobalt_gbdt_reuse(void* h, const GbdtConfig* cfg) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  if (!c || !cfg) return -3;
+  const GbdtConfig& o = c->cfg;
+  if (o.n_rows != cfg->n_rows || o.n_feat != cfg->n_feat || o.row_stride != cfg->row_stride ||
+      o.max_depth != cfg->max_depth || o.max_trees != cfg->max_trees || o.chunk != cfg->chunk ||
+      o.feat_tile != cfg->feat_tile || o.world_size != cfg->world_size || o.comm != cfg->comm)
+    return 1;
+  c->cfg = *cfg;
+  GbdtDev& d = c->d;
+  d.n = cfg->n_rows;  // (the external-memory mode's set_rows may have lowered it)
+  d.row_offset = cfg->row_offset;
+  d.eta = cfg->eta;
+  d.lambda_ = cfg->lambda_;
+  d.alpha = cfg->alpha;
+  d.gamma = cfg->gamma;
+  d.mcw = cfg->min_child_weight;
+  d.subsample = cfg->subsample;
+  d.gscale = cfg->gscale;
+  d.hscale = cfg->hscale;
+  d.ginv = 1.0 / cfg->gscale;
+  d.hinv = 1.0 / cfg->hscale;
+  d.seed = cfg->seed;
+  c->grown = 0;
+  c->applied = 0;
+  return 0;
+}
+
 COBALT_API int cobalt_gbdt_destroy(void* h) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   if (!c) return 0;

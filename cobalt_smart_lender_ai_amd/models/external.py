@@ -359,4 +359,4 @@ class _GpuPasses:
         return self.tr.fetch(0, self.T)
 
     def close(self) -> None:
-        self.tr.close()
+        self.tr.close(park=False)

@@ -479,6 +479,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         tr.set_data(bd.records, bd.binsT, bd.cuts.contiguous(), bd.nbins.to(torch.int32).contiguous(),
                     yt.contiguous(), wt, margin, fm)
         tp = rep.mark("trainer_setup", tp, dev)
+        completed = False
         try:
             if T0:
                 tr.set_start(T0)
@@ -491,8 +492,11 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                 seg_nodes = tr.fetch(s0, s1 - s0)
                 tp = rep.mark("fetch", tp, dev)
                 segment_done(seg_nodes, s1)
+                tp = rep.mark("convert", tp, dev)
+            completed = True
         finally:
-            tr.close()
+            tr.close(park=completed)  # a completed fit's context is kept for the next fit of these shapes
+        tp = rep.mark("close", tp, dev)
         rep.extra["margin"] = margin  # training margins incl. every tree (device tensor)
     else:
         cuts_np = bd.cuts.cpu().numpy()
