@@ -35,8 +35,8 @@ def test_ipc_data_parallel_processes_equal_single_process():
         for g in got:
             assert g["ok"], g
             assert g["transport"] == "ipc"
-            # one exchange per level per tree, plus the connect self-test's two
-            assert g["ipc_epochs"] == 2 + 7 * ref["trees"]
+            # one exchange per level per tree, plus the connect self-test's four (each slot twice)
+            assert g["ipc_epochs"] == 4 + 7 * ref["trees"]
             assert g["model_sha256"] == ref["model_sha256"], (procs, g["rank"])
 
 
