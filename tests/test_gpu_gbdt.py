@@ -413,3 +413,22 @@ def test_dpp_wave_primitives():
         best = ob.cpu().numpy().reshape(64, 4)
         assert (best[:, 0] == win).all() and (best[:, 1] == v[win]).all() and (best[:, 2] == -v[win]).all()
         assert (best[:, 3] == win).all()
+
+
+def test_reused_trainer_context_equals_fresh():
+    """Back-to-back fits of one shape reuse the parked trainer context (cobalt_gbdt_reuse): a fit with
+    other hyper-parameters on a reused context grows the same trees as on a freshly created one."""
+    from cobalt_smart_lender_ai_amd.ops import gbdt_ops
+
+    X, y = _data(40_000, seed=11)
+    Xg, yg = X.cuda(), y.cuda()
+    p1 = gbdt.GBDTParams(n_estimators=12, max_depth=5, learning_rate=0.3, random_state=1)
+    p2 = gbdt.GBDTParams(n_estimators=12, max_depth=5, learning_rate=0.1, gamma=1.0, reg_lambda=3.0,
+                         subsample=0.8, random_state=9)
+    gbdt_ops.release_cached_trainers()
+    gbdt.train(Xg, yg, p1, device="cuda")          # parks its context
+    assert gbdt_ops._PARKED
+    reused = gbdt.train(Xg, yg, p2, device="cuda")  # same shapes: reuses it
+    gbdt_ops.release_cached_trainers()
+    fresh = gbdt.train(Xg, yg, p2, device="cuda")
+    assert reused.save_raw() == fresh.save_raw()
