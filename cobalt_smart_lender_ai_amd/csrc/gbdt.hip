@@ -874,8 +874,7 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // 32 B/row re-read) disappears. Block b = root work item b: rows [b*chunk, (b+1)*chunk).
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
 template <int U, int FT4>
-// (no waves-per-EU bound: capping it at 80 VGPRs spills, 276.5 vs 269.7 ms per 10M fit)
-__global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
+__device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int apply_tree, int chunk) {
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_dyn[];
   __shared__ int64_t s_tot[2][16];
@@ -979,6 +978,20 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   __syncthreads();
   stamp_.probe(2);
   hist_flush(d, s_hist, hl, item, 0, ft, tg, th, true, s_tot, s_fo, s_fs);
+}
+
+// U rows in flight per thread; 2 per CU of 512 threads at 95 VGPRs (no waves-per-EU bound: capping U = 2
+// at 80 VGPRs spills, 276.5 vs 269.7 ms per 10M fit)
+template <int U, int FT4>
+__global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
+  grad_hist_body<U, FT4>(d, tree, apply_tree, chunk);
+}
+
+// One row in flight per thread within 80 VGPRs (no spill): 3 blocks per CU, 24 waves instead of 16
+template <int FT4>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k_grad_hist_w6(GbdtDev d, int tree,
+                                                                                              int apply_tree, int chunk) {
+  grad_hist_body<1, FT4>(d, tree, apply_tree, chunk);
 }
 
 // Lane-pair record gathers for the deep histogram levels (16 < F <= 24 features): lanes 2p and 2p+1
@@ -2562,7 +2575,20 @@ static HistKernel hist_kernel(int ft4, bool pair) {
     default: return k_hist<0, false>;
   }
 }
+static bool grad_w6() {  // the 3-blocks-per-CU root pass (COBALT_GRAD_W6=1)
+  static const int v = getenv("COBALT_GRAD_W6") ? atoi(getenv("COBALT_GRAD_W6")) : 0;
+  return v != 0;
+}
 static GradHistKernel grad_hist_kernel(int ft4) {
+  if (grad_w6()) switch (ft4) {
+    case 4: return k_grad_hist_w6<4>;
+    case 8: return k_grad_hist_w6<8>;
+    case 12: return k_grad_hist_w6<12>;
+    case 16: return k_grad_hist_w6<16>;
+    case 20: return k_grad_hist_w6<20>;
+    case 24: return k_grad_hist_w6<24>;
+    default: return nullptr;
+  }
   switch (ft4) {
     case 4: return k_grad_hist<2, 4>;
     case 8: return k_grad_hist<2, 8>;
@@ -2881,7 +2907,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // 167.5 -> 158.3 us per tree in the stamps)
   int root_rule = std::min(chunk_hist(d, 0), 8192);
   if (fuse_root) {
-    const int64_t res = 2LL * device_cu_count();
+    const int64_t res = (grad_w6() ? 3LL : 2LL) * device_cu_count();
     const int64_t rounds = std::max<int64_t>(1, (d.n + res * 4096) / (res * 8192));  // nearest to n / (res * 8192)
     root_rule = (int)std::min<int64_t>(16384, std::max<int64_t>(1024, (ceil_div(d.n, rounds * res) + 63) / 64 * 64));
   }
