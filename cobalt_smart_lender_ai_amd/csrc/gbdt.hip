@@ -1485,6 +1485,33 @@ __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pa
   }
 }
 
+// 9-16 ranks (more than one 8-GPU node's worth of processes): two groups of 8 loads per cell, so no
+// instantiation holds more than 8 ranks' values in registers (the fused k_eval keeps the parent's
+// histogram loads in flight across the exchange and spilled with 16)
+__device__ __forceinline__ void ipc_sum_cells_wide(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int m,
+                                                   int ncells, longlong2* s_cells, longlong2* hbw, bool store,
+                                                   bool store_tot) {
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    const int cell = i < m - 1 ? cb + i : ncells;
+    const int64_t off = pair_bytes + (int64_t)cell * (int64_t)sizeof(longlong2);
+    longlong2 acc = make_longlong2(0, 0);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      longlong2 t[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        t[r] = 8 * g + r < nr ? *reinterpret_cast<const longlong2*>(iv->slot[8 * g + r] + off) : make_longlong2(0, 0);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        acc.x += t[r].x;
+        acc.y += t[r].y;
+      }
+    }
+    s_cells[i] = acc;
+    if (i < m - 1 ? store : store_tot) hbw[cell] = acc;
+  }
+}
+
 __device__ __forceinline__ void ipc_sum_cells_n(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int m,
                                                 int ncells, longlong2* s_cells, longlong2* hbw, bool store,
                                                 bool store_tot) {
@@ -1492,10 +1519,9 @@ __device__ __forceinline__ void ipc_sum_cells_n(int nr, const IpcFusedView* iv, 
 #define IPC_SUM_CASE(K) \
     case K: ipc_sum_cells<K>(iv, pair_bytes, cb, m, ncells, s_cells, hbw, store, store_tot); break;
     IPC_SUM_CASE(1) IPC_SUM_CASE(2) IPC_SUM_CASE(3) IPC_SUM_CASE(4) IPC_SUM_CASE(5) IPC_SUM_CASE(6)
-    IPC_SUM_CASE(7) IPC_SUM_CASE(8) IPC_SUM_CASE(9) IPC_SUM_CASE(10) IPC_SUM_CASE(11) IPC_SUM_CASE(12)
-    IPC_SUM_CASE(13) IPC_SUM_CASE(14) IPC_SUM_CASE(15) IPC_SUM_CASE(16)
+    IPC_SUM_CASE(7) IPC_SUM_CASE(8)
 #undef IPC_SUM_CASE
-    default: break;
+    default: ipc_sum_cells_wide(nr, iv, pair_bytes, cb, m, ncells, s_cells, hbw, store, store_tot); break;
   }
 }
 
@@ -1590,6 +1616,45 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
     }
   };
   load_meta(fbeg + wave_id());
+  // per-lane byte offsets of this wave's cells (from the kernel-argument metadata) and the load masks:
+  // only lanes holding a real bin of an evaluated feature load (exec-masked): the CU's address path
+  // costs per active lane, and unmasked, the 16 waves' 2 x 4 chunks (+ the parent's) were 256 full
+  // 1 KB load instructions per block for ~26 chunks of real bins -- ~2 us per level at 1M rows.
+  // (the colsample bit is applied after the loads: it is a global load of round trip 1 itself)
+  // (32-bit byte offsets from the uniform bases: the loads take the SGPR-base + VGPR-offset form
+  // instead of a 64-bit VGPR address pair each -- 32 VGPRs the kernel otherwise spilled)
+  uint32_t cofs[2][4];
+  bool ld[2][4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      cofs[s][c] = (uint32_t)(ef[s].off + min(c * kWave + lane, max(ef[s].nb - 1, 0))) * (uint32_t)sizeof(longlong2);
+      ld[s][c] = c * kWave + lane < ef[s].nb;
+    }
+  // the parent's full histogram (the previous level's k_eval stored every node's by position): its
+  // address depends on the block index only
+  const int64_t* parent = level > 0 ? d.hist_s[parity ^ 1] + (int64_t)(pos >> 1) * SE : hb;
+  const longlong2* pa2 = reinterpret_cast<const longlong2*>(readlane64((int64_t)parent, 0));  // uniform base
+  longlong2 pv[2][4];
+  auto load_parent = [&]() {
+    if (level > 0) {  // kernel argument: uniform, no wait on the node record (whose build flag selects)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          pv[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(pa2) + cofs[s][c])
+                              : make_longlong2(0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pv[s][c] = make_longlong2(0, 0);
+    }
+  };
+  // fused exchange: the parent's loads (local, independent of the peers) are in flight during the
+  // wait for the ranks, instead of one more round trip after it
+  if (kFused && !kGroups) load_parent();  // (the grouped form spilled holding them)
   // round trip 1 (uniform scalar loads); unconditional (in-bounds) loads selected after
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
@@ -1630,10 +1695,6 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
       if (ef[s].f < 32) s_nb[ef[s].f] = ef[s].nb;
   }
   const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
-  // the parent's full histogram (the previous level's k_eval stored every node's by position): its
-  // address depends on the block index only, so its loads go out with the node record's (unused when
-  // this child was built)
-  const int64_t* parent = level > 0 ? d.hist_s[parity ^ 1] + (int64_t)(pos >> 1) * SE : hb;
   // wave-uniform: kept in SGPRs (as a VALU result it held a VGPR pair the candidate loop spilled)
   const double parent_gain = __longlong_as_double(
       readlane64(__double_as_longlong(calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw)), 0));
@@ -1644,29 +1705,11 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
   best.hl = 0;
   float best_cut = -FLT_MAX;
   const longlong2* hb2 = reinterpret_cast<const longlong2*>(hb);
-  const longlong2* pa2 = reinterpret_cast<const longlong2*>(readlane64((int64_t)parent, 0));  // uniform base
   // one pass: a block covers at most 2 features per wave (the host keeps F <= 32 per block)
   {
   // round trip 2: the histogram bins (and the parent's, for the subtraction) of both features, all
   // issued before the first use (clamped cells: the loads need no per-load guard)
-  // (32-bit byte offsets from the uniform bases: the loads take the SGPR-base + VGPR-offset form
-  // instead of a 64-bit VGPR address pair each -- 32 VGPRs the kernel otherwise spilled)
-  longlong2 v[2][4], pv[2][4];
-  uint32_t cofs[2][4];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      cofs[s][c] = (uint32_t)(ef[s].off + min(c * kWave + lane, max(ef[s].nb - 1, 0))) * (uint32_t)sizeof(longlong2);
-  // Only lanes holding a real bin of an evaluated feature load (exec-masked): the CU's address path
-  // costs per active lane, and unmasked, the 16 waves' 2 x 4 chunks (+ the parent's) were 256 full
-  // 1 KB load instructions per block for ~26 chunks of real bins -- ~2 us per level at 1M rows.
-  // (the colsample bit is applied after the loads: it is a global load of round trip 1 itself)
-  bool ld[2][4];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) ld[s][c] = c * kWave + lane < ef[s].nb;
+  longlong2 v[2][4];
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1677,19 +1720,7 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
         v[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c])
                            : make_longlong2(0, 0);
     }
-  if (level > 0) {  // kernel argument: uniform, no wait on the node record (whose build flag selects)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        pv[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(pa2) + cofs[s][c])
-                            : make_longlong2(0, 0);
-  } else {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) pv[s][c] = make_longlong2(0, 0);
-  }
+  if (!kFused || kGroups) load_parent();
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     EvalFeat& e = ef[s];
