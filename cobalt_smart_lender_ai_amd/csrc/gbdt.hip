@@ -2574,18 +2574,24 @@ static int chunk_hist(const GbdtDev& d, int level) {
   if (level == 0) return env0 > 0 ? std::min(16384, std::max(512, env0)) : d.chunk;
   if (env1 > 0) return std::min(16384, std::max(512, env1));
   // <= 4096 rows: with the reduce at ~3 us per level, more, smaller items balance the CUs better
-  // (10M rows: 295.7 vs 304.8 ms per fit with 8192; 2048 is slower again: 311.8)
+  // (10M rows: 295.7 vs 304.8 ms per fit with 8192; 2048 is slower again: 311.8). Up to 1.5M rows
+  // 1024 (1M: k_hist 68.5 -> 62.7 us per tree, fit 74.6 -> 72.6 ms; 5M measured slower with it).
+  if (d.n <= 1500000) return 1024;
   return pow2_clamp((d.n / 2 + 383) / 384, 1024, 4096);
 }
 // Partition item size and block shape (see k_partition); COBALT_PART_CHUNK overrides the size.
 static bool part_wide(const GbdtDev& d) { return d.n < 4000000; }
+static int device_cu_count();
 static int chunk_part(const GbdtDev& d) {
   static const int env = getenv("COBALT_PART_CHUNK") ? atoi(getenv("COBALT_PART_CHUNK")) : 0;
   const int cap = (part_wide(d) ? 16 : 4) * kPartSteps * kWave;
   if (env > 0) return std::min(cap, std::max(1024, env / 1024 * 1024));
-  // wide (16-wave) blocks: 4096-row items spread the level over ~2x the CUs (1M rows: 104.7 vs
-  // 106.8 ms per fit); narrow blocks keep 8192 (10M rows: 4096 measured 318.6 vs 304.8 ms)
-  return part_wide(d) ? 4096 : 8192;
+  // wide (16-wave) blocks: 4096-row items while a level's items fit one block per CU (1M rows: 104.7
+  // vs 106.8 ms per fit with 8192 in round 1), else 8192 (1.25M: 4096-row items ran 306 blocks on 256
+  // CUs; 8192: 82.1 -> 79.5 ms, 2.5M 105.5 -> 104.1; 16384 slower at both); narrow blocks keep 8192
+  // (10M rows: 4096 measured 318.6 vs 304.8 ms)
+  if (!part_wide(d)) return 8192;
+  return (d.n + 4095) / 4096 <= device_cu_count() ? 4096 : 8192;
 }
 
 // Histogram kernels by record shape: FT4 = F rounded up to 4 for 32-byte records with one feature tile
