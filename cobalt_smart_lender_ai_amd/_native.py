@@ -45,6 +45,7 @@ _SIGS: dict[str, tuple] = {
     "cobalt_gbdt_fetch_trees": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "cobalt_gbdt_max_nodes": (c_int, [c_void_p]),
     "cobalt_gbdt_set_start": (c_int, [c_void_p, c_int]),
+    "cobalt_gbdt_set_binary_labels": (c_int, [c_void_p, c_float, c_void_p]),
     "cobalt_gbdt_destroy": (c_int, [c_void_p]),
     "cobalt_gbdt_reuse": (c_int, [c_void_p, c_void_p]),
     "cobalt_gbdt_grow_sampled": (c_int, [c_void_p, c_int, c_void_p]),

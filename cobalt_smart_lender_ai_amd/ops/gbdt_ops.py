@@ -196,6 +196,17 @@ class GpuGbdtTrainer:
         rc = self.lib.cobalt_gbdt_set_data(self.h, *[t.data_ptr() for t in ts])
         _native.check(rc, "cobalt_gbdt_set_data")
 
+    def set_binary_labels(self, spw: float) -> bool:
+        """After :meth:`set_data`: hold the 0/1 labels in the row records (byte 23 of a 32-byte record,
+        F <= 20) and derive each row's weight from its label (``spw`` for positives, 1 otherwise), so
+        the gradient pass reads neither array. The caller guarantees binary labels and no sample
+        weights. False (nothing changed) when the record layout has no room."""
+        rc = self.lib.cobalt_gbdt_set_binary_labels(self.h, ctypes.c_float(spw), _native.stream_handle())
+        if rc == -13:
+            return False
+        _native.check(rc, "cobalt_gbdt_set_binary_labels")
+        return True
+
     def set_start(self, t0: int) -> None:
         """Continue boosting at global tree index ``t0`` (margins already hold trees < t0)."""
         _native.check(self.lib.cobalt_gbdt_set_start(self.h, t0), "cobalt_gbdt_set_start")

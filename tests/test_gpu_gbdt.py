@@ -432,3 +432,26 @@ def test_reused_trainer_context_equals_fresh():
     gbdt_ops.release_cached_trainers()
     fresh = gbdt.train(Xg, yg, p2, device="cuda")
     assert reused.save_raw() == fresh.save_raw()
+
+
+def test_labels_in_records_equal_label_arrays(monkeypatch):
+    """0/1 labels without sample weights ride in the row records' padding (byte 23, weights derived
+    from the label and scale_pos_weight): the trees equal the label/weight-array path and the oracle.
+    A weighted fit keeps the arrays (and still equals the oracle)."""
+    from cobalt_smart_lender_ai_amd.ops import gbdt_ops
+
+    X, y = _data(50_000, seed=21)
+    p = gbdt.GBDTParams(n_estimators=6, max_depth=6, learning_rate=0.3, gamma=0.5, scale_pos_weight=6.7,
+                        subsample=0.9, random_state=5)
+    gbdt_ops.release_cached_trainers()
+    packed = gbdt.train(X, y, p, device="cuda")
+    monkeypatch.setenv("COBALT_LABEL_IN_RECORD", "0")
+    arrays = gbdt.train(X, y, p, device="cuda")
+    monkeypatch.delenv("COBALT_LABEL_IN_RECORD")
+    assert packed.save_raw("ubj") == arrays.save_raw("ubj")
+    assert packed.save_raw("ubj") == gbdt.train(X, y, p, device="cpu").save_raw("ubj")
+    w = torch.rand(X.shape[0], generator=torch.Generator().manual_seed(3)) + 0.5
+    wg = gbdt.train(X, y, p, sample_weight=w, device="cuda")
+    wc = gbdt.train(X, y, p, sample_weight=w, device="cpu")
+    assert wg.save_raw("ubj") == wc.save_raw("ubj")
+    assert wg.save_raw("ubj") != packed.save_raw("ubj")
