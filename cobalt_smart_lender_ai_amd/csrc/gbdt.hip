@@ -2594,7 +2594,10 @@ static int chunk_hist(const GbdtDev& d, int level) {
   return pow2_clamp((d.n / 2 + 383) / 384, 1024, 4096);
 }
 // Partition item size and block shape (see k_partition); COBALT_PART_CHUNK overrides the size.
-static bool part_wide(const GbdtDev& d) { return d.n < 4000000; }
+static bool part_wide(const GbdtDev& d) {
+  static const int env = getenv("COBALT_PART_WIDE") ? atoi(getenv("COBALT_PART_WIDE")) : -1;
+  return env >= 0 ? env != 0 : d.n < 4000000;
+}
 static int device_cu_count();
 static int chunk_part(const GbdtDev& d) {
   static const int env = getenv("COBALT_PART_CHUNK") ? atoi(getenv("COBALT_PART_CHUNK")) : 0;
