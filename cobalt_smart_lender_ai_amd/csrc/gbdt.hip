@@ -195,6 +195,7 @@ struct GbdtDev {
   // so the gradient pass reads neither the label nor the weight array
   int32_t ylab;
   float spw;
+  int32_t pwide;  // host-side: 16-wave partition blocks (see part_wide)
 };
 
 // Store of a value the next launch reads: plain, or write-through (agent-scope relaxed atomic store =
@@ -2588,16 +2589,18 @@ static int chunk_hist(const GbdtDev& d, int level) {
   if (level == 0) return env0 > 0 ? std::min(16384, std::max(512, env0)) : d.chunk;
   if (env1 > 0) return std::min(16384, std::max(512, env1));
   // <= 4096 rows: with the reduce at ~3 us per level, more, smaller items balance the CUs better
-  // (10M rows: 295.7 vs 304.8 ms per fit with 8192; 2048 is slower again: 311.8). Up to 1.5M rows
-  // 1024 (1M: k_hist 68.5 -> 62.7 us per tree, fit 74.6 -> 72.6 ms; 5M measured slower with it).
-  if (d.n <= 1500000) return 1024;
-  return pow2_clamp((d.n / 2 + 383) / 384, 1024, 4096);
+  // (10M rows: 295.7 vs 304.8 ms per fit with 8192; 2048 is slower again: 311.8); ~768 items of a
+  // level's half of the rows: 1024 up to ~1.57M rows (1M: k_hist 68.5 -> 62.7 us per tree, fit 74.6 ->
+  // 72.6 ms), 2048 up to ~3.1M (2.5M: 102.8 -> 100.4 ms vs 4096), 4096 above (5M: 1024 / 2048 slower)
+  return pow2_clamp((d.n / 2 + 767) / 768, 1024, 4096);
 }
 // Partition item size and block shape (see k_partition); COBALT_PART_CHUNK overrides the size.
-static bool part_wide(const GbdtDev& d) {
-  static const int env = getenv("COBALT_PART_WIDE") ? atoi(getenv("COBALT_PART_WIDE")) : -1;
-  return env >= 0 ? env != 0 : d.n < 4000000;
-}
+// 16-wave blocks at every size (COBALT_PART_WIDE=0: 4-wave blocks, read when a context is created):
+// 10M rows 234.7 -> 230.6 ms, 7.5M 191.8 -> 188.6, 5M 150.2 -> 147.3 against 4-wave blocks above 4M
+// rows (profiles/round3/ab/ab_part_wide.txt); 4-wave blocks won at 10M in round 2, before the
+// partition passes went to integer arithmetic
+static int env_part_wide() { return getenv("COBALT_PART_WIDE") ? (atoi(getenv("COBALT_PART_WIDE")) != 0) : 1; }
+static bool part_wide(const GbdtDev& d) { return d.pwide != 0; }
 static int device_cu_count();
 static int chunk_part(const GbdtDev& d) {
   static const int env = getenv("COBALT_PART_CHUNK") ? atoi(getenv("COBALT_PART_CHUNK")) : 0;
@@ -2688,6 +2691,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
     GbdtDev tmp{};
     tmp.n = N;
     tmp.chunk = cfg->chunk;
+    tmp.pwide = env_part_wide();
     const int ch = std::min(chunk_hist(tmp, 0), chunk_hist(tmp, 1));
     c->items_cap = std::max(ceil_div(N, ch), ceil_div(N, chunk_part(tmp))) + (1 << cfg->max_depth) + 8;
   }
@@ -2715,6 +2719,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.hinv = 1.0 / cfg->hscale;
   d.seed = cfg->seed;
   d.ablate = getenv("COBALT_HIST_ABLATE") ? atoi(getenv("COBALT_HIST_ABLATE")) : 0;
+  d.pwide = env_part_wide();
   // write-through slabs always (10M rows: reduce gaps 14.2 -> 12.0 us per tree, fit 243.7 -> 243.2 ms); write-through
   // row ids below 4M rows only (1M: 240.2 -> 237.4 us per tree with both; at 10M the partition itself
   // slows 210 -> 228 us per tree for 10 us of shorter histogram gaps). COBALT_WT overrides.

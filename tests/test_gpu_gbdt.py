@@ -81,11 +81,12 @@ def test_gpu_trees_identical_to_host_oracle(kw):
 
 
 @pytest.mark.parametrize("env", [{"COBALT_HIST_PAIR": "0"}, {"COBALT_MAX_COPY_SHIFT": "6"},
-                                 {"COBALT_MAX_COPY_SHIFT": "0", "COBALT_HIST_PAIR": "0"}])
+                                 {"COBALT_MAX_COPY_SHIFT": "0", "COBALT_HIST_PAIR": "0"},
+                                 {"COBALT_PART_WIDE": "0"}])
 def test_gpu_histogram_variants_identical_to_host_oracle(env, monkeypatch):
     """The histogram variants behind switches (one lane per row instead of the default lane-pair record
-    gathers; 64 or 1 per-lane copies of a low-cardinality feature instead of 32) grow the oracle's
-    trees (the switches are read when a trainer context is created)."""
+    gathers; 64 or 1 per-lane copies of a low-cardinality feature instead of 32; 4-wave partition
+    blocks) grow the oracle's trees (the switches are read when a trainer context is created)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     X, y = _data(60_000, seed=4)
@@ -98,8 +99,8 @@ def test_gpu_histogram_variants_identical_to_host_oracle(env, monkeypatch):
 
 @pytest.mark.timeout(600)
 def test_gpu_large_n_kernel_shapes_identical_to_host_oracle():
-    """Above 4M rows the trainer switches kernel shapes (k_partition<4>, 8192-row root items,
-    16384-row work chunks -- the headline 10M-row configuration). Two depth-7 trees on 4.3M rows
+    """Above 4M rows the trainer switches kernel shapes (8192-row partition items in k_partition<16, 8>,
+    8192-row root items, 16384-row work chunks -- the headline 10M-row configuration). Two depth-7 trees on 4.3M rows
     must equal the NumPy oracle's byte for byte, and the training margins must equal the predictor's."""
     n = 4_300_000
     X, y = synth.make_lendingclub(n, seed=31)
