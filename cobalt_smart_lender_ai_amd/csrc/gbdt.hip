@@ -191,7 +191,7 @@ struct GbdtDev {
   // instead of at the kernel-end write-back that the dependent launch waits for
   int32_t wt;
   // binary labels held in the row records (cobalt_gbdt_set_binary_labels): byte 23 of a 32-byte record
-  // (F <= 20) is the 0/1 label and the weight is `spw` for positives, 1 otherwise (no sample weights),
+  // (F <= 23) is the 0/1 label and the weight is `spw` for positives, 1 otherwise (no sample weights),
   // so the gradient pass reads neither the label nor the weight array
   int32_t ylab;
   float spw;
@@ -3154,7 +3154,8 @@ COBALT_API int cobalt_gbdt_max_nodes(void* h) { return static_cast<GbdtCtx*>(h)-
 // keyed by the global tree index -- follow the uninterrupted run exactly.
 // Binary labels into the row records (see GbdtDev::ylab): after set_data, for a fit whose labels are
 // all 0 or 1 and whose weights are 1 (negatives) or `spw` (positives) -- the caller checks both. Writes
-// byte 23 of every record (padding: bins occupy bytes 0..F-1, F <= 20, and the gradient pass rewrites
+// byte 23 of every record (padding: bins occupy bytes 0..F-1, F <= 23 -- for F > 20 the histogram reads
+// byte 23 as a padding feature's bin, which goes to the trash cell -- and the gradient pass rewrites
 // bytes 16..31 from the record it read). Saves 8 of the ~80 bytes per row the gradient pass moves.
 __global__ __launch_bounds__(256) void k_put_label(uint8_t* bins, const float* label, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -3164,7 +3165,7 @@ __global__ __launch_bounds__(256) void k_put_label(uint8_t* bins, const float* l
 COBALT_API int cobalt_gbdt_set_binary_labels(void* h, float spw, hipStream_t stream) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   GbdtDev& d = c->d;
-  if (!d.bins || !d.label || d.stride != 32 || d.F > 20) return -13;
+  if (!d.bins || !d.label || d.stride != 32 || d.F > 23) return -13;
   if (d.n > 0) {
     const int grid = std::min(ceil_div(d.n, 256), 4096);
     hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);

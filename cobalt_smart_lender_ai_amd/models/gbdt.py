@@ -481,7 +481,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         # 0/1 labels and no sample weights: the labels ride in the row records' padding and the weights
         # follow from them (8 fewer bytes per row in every gradient pass); COBALT_LABEL_IN_RECORD=0 off
         if (sample_weight is None and os.environ.get("COBALT_LABEL_IN_RECORD", "1") != "0"
-                and bd.records.shape[1] == 32 and F <= 20 and bool(((yt == 0) | (yt == 1)).all())):
+                and bd.records.shape[1] == 32 and F <= 23 and bool(((yt == 0) | (yt == 1)).all())):
             tr.set_binary_labels(float(np.float32(spw)))
         tp = rep.mark("trainer_setup", tp, dev)
         completed = False

@@ -198,7 +198,7 @@ class GpuGbdtTrainer:
 
     def set_binary_labels(self, spw: float) -> bool:
         """After :meth:`set_data`: hold the 0/1 labels in the row records (byte 23 of a 32-byte record,
-        F <= 20) and derive each row's weight from its label (``spw`` for positives, 1 otherwise), so
+        F <= 23) and derive each row's weight from its label (``spw`` for positives, 1 otherwise), so
         the gradient pass reads neither array. The caller guarantees binary labels and no sample
         weights. False (nothing changed) when the record layout has no room."""
         rc = self.lib.cobalt_gbdt_set_binary_labels(self.h, ctypes.c_float(spw), _native.stream_handle())

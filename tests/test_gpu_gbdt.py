@@ -250,10 +250,11 @@ def _wide(n, F, seed):
     return X, y
 
 
-@pytest.mark.parametrize("F", [7, 13, 16, 17, 24, 37, 106])
+@pytest.mark.parametrize("F", [7, 13, 16, 17, 21, 23, 24, 37, 106])
 def test_gpu_trees_identical_to_host_oracle_other_widths(F):
     """Generic record layouts and multi-tile histograms (F=106 is the RFE stage's width); 13..24 cover
-    the 32-byte-record kernels of every lane-pair split (FT4 = 16, 20, 24; padding features)."""
+    the 32-byte-record kernels of every lane-pair split (FT4 = 16, 20, 24; padding features; 21 and
+    23: the label byte 23 read as a padding feature's bin)."""
     X, y = _wide(20_000, F, seed=F)
     p = gbdt.GBDTParams(n_estimators=4, max_depth=6, learning_rate=0.3, gamma=0.5, colsample_bytree=0.8,
                         subsample=0.9, random_state=3)
