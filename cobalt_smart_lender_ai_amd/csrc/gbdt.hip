@@ -2105,9 +2105,10 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
 // row list stays sorted in 8192-row runs (the root level reads rows in identity order).
 // Block size is a template parameter: the per-item cursor claim is a pair of same-address
 // device-scope atomics, whose latency/serialisation across the 8 XCDs dominates a level when items
-// are many and small (measured: removing the claims took a 10M-row level from 58 to 24 us). Small
-// row counts therefore use 1024-thread blocks (fewer, bigger items: ~150 at 1.25M rows); large ones
-// 256-thread blocks with 8192-row items, which keep more independent blocks in flight per CU.
+// are many and small (measured: removing the claims took a 10M-row level from 58 to 24 us). The
+// default is 1024-thread blocks (16 waves x 8 steps per 8192-row item, 4096-row items while they fit
+// one per CU; see part_wide / chunk_part); 256-thread blocks (COBALT_PART_WIDE=0) were the large-row
+// shape until round 3.
 constexpr int kPartSteps = 32;  // 64-row steps per wave (maximum; see k_partition's kSteps)
 
 // kSteps: 64-row steps per wave, sized by the host to the item (chunk <= kPartWaves * kSteps * 64):
@@ -2226,7 +2227,7 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
 }
 
 // ------------------------------------------------------------------------------------------
-// Split evaluation fused with the row partition (one GPU, < 4M rows, levels 0 .. max_depth - 2).
+// Split evaluation fused with the row partition (one GPU, a level's items <= CUs, levels 0 .. max_depth - 2).
 // At small row counts a level is a chain of short launches whose fixed costs dominate (1M rows:
 // k_eval ~6.6 us + a ~1.5 us boundary per level), so every block of the partition pass evaluates its
 // OWN node (the same eval_core, redundantly: ~2 us of fp64 work per block on its own CU, with the
@@ -2608,7 +2609,8 @@ static int chunk_part(const GbdtDev& d) {
   if (env > 0) return std::min(cap, std::max(1024, env / 1024 * 1024));
   // wide (16-wave) blocks: 4096-row items while a level's items fit one block per CU (1M rows: 104.7
   // vs 106.8 ms per fit with 8192 in round 1), else 8192 (1.25M: 4096-row items ran 306 blocks on 256
-  // CUs; 8192: 82.1 -> 79.5 ms, 2.5M 105.5 -> 104.1; 16384 slower at both); narrow blocks keep 8192
+  // CUs; 8192: 82.1 -> 79.5 ms, 2.5M 105.5 -> 104.1; 16384 slower at both; at 10M 4096 / 6144 / 12288 /
+  // 16384 243.0 / 234.8 / 256.0 / 250.6 vs 231.4 ms); narrow blocks keep 8192
   // (10M rows: 4096 measured 318.6 vs 304.8 ms)
   if (!part_wide(d)) return 8192;
   return (d.n + 4095) / 4096 <= device_cu_count() ? 4096 : 8192;
