@@ -2837,11 +2837,12 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   CK(hipMemcpy(nb.data(), nbins, F * sizeof(int32_t), hipMemcpyDeviceToHost));
   std::vector<int2> lay(F);
   std::vector<int32_t> ent(ntiles, 0);
-  // At most 32 per-lane copies of a low-cardinality feature: lanes l and l + 32 share a copy but sit in
-  // different LDS lane groups of a wave64 access, so the atomics stay conflict-free while the flush
-  // sums half as many copies (10M: 253.4 -> 250.3 ms per fit, 1M: 87.1 -> 85.7; 16 copies measured
-  // the same within noise). COBALT_MAX_COPY_SHIFT overrides the log2 (0..6).
-  const int max_sh = getenv("COBALT_MAX_COPY_SHIFT") ? std::min(6, std::max(0, atoi(getenv("COBALT_MAX_COPY_SHIFT")))) : 5;
+  // Per-lane copies of a low-cardinality feature, capped: with 32, lanes l and l + 32 share a copy but
+  // sit in different LDS lane groups of a wave64 access, so the atomics stay conflict-free while the
+  // flush sums half as many copies as 64 (10M: 253.4 -> 250.3 ms per fit, 1M: 87.1 -> 85.7). At most
+  // 16 since round 3 -- same-address collisions of 4 lanes traded for a quarter of the flush work (two same-box rounds at 1 / 1.25 / 2.5 / 10M rows: 0.3-0.8 ms per fit faster each,
+  // profiles/round3/ab/ab_copy_shift4.txt). COBALT_MAX_COPY_SHIFT overrides the log2 (0..6).
+  const int max_sh = getenv("COBALT_MAX_COPY_SHIFT") ? std::min(6, std::max(0, atoi(getenv("COBALT_MAX_COPY_SHIFT")))) : 4;
   int max_ent = 0;
   for (int t = 0; t < ntiles; ++t) {
     int off = 0;

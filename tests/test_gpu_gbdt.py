@@ -80,12 +80,12 @@ def test_gpu_trees_identical_to_host_oracle(kw):
         assert np.array_equal(tg.sum_hessian, tc.sum_hessian)
 
 
-@pytest.mark.parametrize("env", [{"COBALT_HIST_PAIR": "0"}, {"COBALT_MAX_COPY_SHIFT": "6"},
+@pytest.mark.parametrize("env", [{"COBALT_HIST_PAIR": "0"}, {"COBALT_MAX_COPY_SHIFT": "6"}, {"COBALT_MAX_COPY_SHIFT": "5"},
                                  {"COBALT_MAX_COPY_SHIFT": "0", "COBALT_HIST_PAIR": "0"},
                                  {"COBALT_PART_WIDE": "0"}])
 def test_gpu_histogram_variants_identical_to_host_oracle(env, monkeypatch):
     """The histogram variants behind switches (one lane per row instead of the default lane-pair record
-    gathers; 64 or 1 per-lane copies of a low-cardinality feature instead of 32; 4-wave partition
+    gathers; 64, 32 or 1 per-lane copies of a low-cardinality feature instead of 16; 4-wave partition
     blocks) grow the oracle's trees (the switches are read when a trainer context is created)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
