@@ -53,12 +53,22 @@ def main() -> None:
     from cobalt_smart_lender_ai_amd.models import gbdt
     from cobalt_smart_lender_ai_amd.parallel import dist as pdist
 
+    # COBALT_BENCH_SHARED_DEVICE=1: every rank on cuda:0 (the 1-GPU multi-process rehearsal); each rank
+    # then launches on its own CU-masked share of the device (parallel/cumask.py)
+    shared = os.environ.get("COBALT_BENCH_SHARED_DEVICE") == "1"
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if shared and torch.cuda.is_available():
+        from cobalt_smart_lender_ai_amd.parallel import cumask
+
+        torch.cuda.set_device(0)
+        if cumask.want_shared_mask(env_world):
+            torch.cuda.set_stream(cumask.shared_device_stream(int(os.environ.get("RANK", "0")), env_world,
+                                                              torch.device("cuda", 0)))
     ctx = pdist.init_from_env()
     world, rank = ctx.world, ctx.rank
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    # COBALT_BENCH_SHARED_DEVICE=1: every rank on cuda:0 (the 1-GPU multi-process rehearsal)
-    dev_index = 0 if os.environ.get("COBALT_BENCH_SHARED_DEVICE") == "1" else ctx.local_rank
+    dev_index = 0 if shared else ctx.local_rank
     dev = torch.device("cuda", dev_index) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
@@ -79,8 +89,20 @@ def main() -> None:
                        feature_types=synth.FEATURE_TYPES)
         return b, rep
 
+    fallback = None
     for _ in range(a.warmup):
-        fit()
+        diverged = False
+        try:
+            fit()
+        except gbdt.ReplicaDivergence as e:  # raised on every rank of the same fit (in-flight digest check)
+            print(f"[bench] rank {rank}: {e}", file=sys.stderr)
+            diverged = True
+        # every rank agrees before acting on it, so the ranks' collectives stay in step
+        if world > 1 and ctx.allreduce_scalar(1.0 if diverged else 0.0, "max", dev) > 0.5:
+            if ctx.transport != "ipc":
+                raise RuntimeError("data-parallel replicas diverged on the RCCL transport")
+            fallback = "ipc replicas diverged in warm-up; RCCL"
+            pdist.switch_transport(ctx, "rccl")
     ctx.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -149,6 +171,8 @@ def main() -> None:
             "rows_global": n_global,
             "sketch_rows": a.sketch_rows or "all",
             "dp_transport": ctx.transport if world > 1 else None,
+            "dp_transport_fallback": fallback,
+            "replica_check": "in-flight per-tree digest of every rank's split decisions" if world > 1 else None,
             "replicas_agree": replicas_agree,
             "auc": None if auc is None else round(auc, 5),
             "test_rows": a.test_rows,

@@ -50,6 +50,8 @@ _SIGS: dict[str, tuple] = {
     "cobalt_gbdt_reuse": (c_int, [c_void_p, c_void_p]),
     "cobalt_gbdt_grow_sampled": (c_int, [c_void_p, c_int, c_void_p]),
     "cobalt_gbdt_set_rows": (c_int, [c_void_p, c_int64]),
+    "cobalt_gbdt_error": (c_int, [c_void_p]),
+    "cobalt_gbdt_set_fault": (c_int, [c_void_p, c_int]),
     "cobalt_gbdt_tree_ptr": (c_void_p, [c_void_p, c_int]),
     "cobalt_ooc_page": (c_int, [c_void_p, c_int, c_int64, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                 ctypes.c_uint64, c_int64, ctypes.c_double, ctypes.c_double, ctypes.c_double,

@@ -196,7 +196,41 @@ struct GbdtDev {
   int32_t ylab;
   float spw;
   int32_t pwide;  // host-side: 16-wave partition blocks (see part_wide)
+  // In-flight replica check (data parallel only; dig == nullptr on one GPU). Every node decision a
+  // tree finalises adds a 32-bit hash to dig[tree & 1] (eval_finalize). At level 0 of the next tree
+  // the reduce writes the previous tree's sum into an extra int64 cell right after the root slot
+  // (element slot_elems), the level's collective sums it over the ranks with the histograms, and the
+  // evaluation checks sum == world x own: a rank that grew a different tree (a stale peer read, a
+  // corrupted exchange) makes the check fail on EVERY rank within one tree. The failure goes to the
+  // mapped host word err_host (2 = replica divergence), which the host polls while a segment runs.
+  int64_t* dig;
+  int32_t dig_slot;   // tree & 1 of the tree being grown
+  int32_t dig_check;  // the previous tree was grown by this context (its digest is comparable)
+  int32_t world;
+  int32_t corrupt;    // fault injection (COBALT_FAULT_CORRUPT_RANK): perturb this tree's root totals
+  unsigned* err_host;
+  uint64_t* dec;      // [max_nodes] k_eval_part<mode 2>: a node's decision granule {tag, decision}
 };
+
+// 32-bit hash of one finalised node decision (position, status, split feature / bin / default
+// direction, threshold or leaf value): summed over a tree's nodes into GbdtDev::dig.
+__device__ __forceinline__ uint32_t node_hash(int n, int status, int feat, int bin, int dl, float cond) {
+  uint64_t x = ((uint64_t)(uint32_t)n << 32) ^ ((uint64_t)(uint32_t)status << 40) ^ ((uint64_t)(uint32_t)feat << 44) ^
+               ((uint64_t)(uint32_t)(bin & 0x3FF) << 52) ^ ((uint64_t)(uint32_t)dl << 62) ^ __float_as_uint(cond);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+// Level 0 of a tree, after the collective: `sum` is the digest cell summed over the ranks.
+__device__ __forceinline__ void digest_check(const GbdtDev& d, int64_t sum) {
+  if (!d.dig) return;
+  const int64_t own = d.dig_check ? d.dig[d.dig_slot ^ 1] : 0;
+  if (sum != (int64_t)d.world * own) __hip_atomic_store(d.err_host, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Store of a value the next launch reads: plain, or write-through (agent-scope relaxed atomic store =
 // global_store ... sc1) when `wt`.
@@ -624,7 +658,10 @@ struct PlanOut {
   int node, slot, begin, end, total;
 };
 
-template <class EntryFn>
+// kZeroItem: an entry with no rows still gets one (empty) item -- the data-parallel evaluation +
+// partition pass must finalise every active node on every rank, also where this rank holds none of
+// its rows.
+template <bool kZeroItem = false, class EntryFn>
 __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int* s_out) {
   if (wave_id() == 0) {
     const int lane = lane_id();
@@ -634,7 +671,8 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
       const int e = base + lane;
       PlanEntry en{-1, 0, 0, 0};
       if (e < n_ent) en = entry(e);
-      const int nch = (en.node >= 0 && en.count > 0) ? (en.count + chunk - 1) / chunk : 0;
+      const int nch = en.node < 0 ? 0
+                      : (en.count > 0 ? (en.count + chunk - 1) / chunk : (kZeroItem ? 1 : 0));
       const int incl = wave_incl_scan(nch) + carry;
       const int excl = incl - nch;
       if (nch > 0 && item >= excl && item < incl) {
@@ -1266,10 +1304,18 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
 // global atomic per non-zero cell per (run, slot) -- coalesced, 30-100x fewer than per-block flushes.
 constexpr int kRedItems = 16;
 
-__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int publish, int n_grid) {
+__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int publish, int n_grid, int level) {
   BlockStamp stamp_(d);
   // fused partition path: block (0, 0) publishes the level's node ranges from the finished claims
   if (publish > 0 && blockIdx.x == 0 && blockIdx.y == 0) publish_level(d, publish, -1, true);
+  // replica check (data parallel): the previous tree's digest goes into the cell after the root slot
+  // (all-reduced with it); this tree's accumulator restarts (no eval of this tree has run yet)
+  if (level == 0 && d.dig && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    int64_t* const red = d.hist_red ? d.hist_red : d.hist_b[parity];
+    red[d.slot_elems] = d.dig_check ? d.dig[d.dig_slot ^ 1] : 0;
+    red[d.slot_elems + 1] = 0;
+    d.dig[d.dig_slot] = 0;
+  }
   const int i0 = blockIdx.x * kRedItems;
   const int ncell = d.ncells;
   const int cell = blockIdx.y * blockDim.x + threadIdx.x;
@@ -1472,20 +1518,29 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
     nd.leaf_value = (float)(wgt * d.eta);
     nd.split_cond = nd.leaf_value;
   }
+  if (d.dig) {  // replica digest (data parallel): this node's decision (+ its max-depth leaf children)
+    uint32_t hsum = node_hash(n, nd.status, ok ? nd.feat : -1, ok ? nd.bin : -1, ok ? nd.default_left : 0, nd.split_cond);
+    if (ok && level + 1 == d.max_depth) {
+      hsum += node_hash(2 * n + 1, kLeaf, -1, -1, 0, nodes[2 * n + 1].split_cond);
+      hsum += node_hash(2 * n + 2, kLeaf, -1, -1, 0, nodes[2 * n + 2].split_cond);
+    }
+    atomicAdd(reinterpret_cast<unsigned long long*>(d.dig + d.dig_slot), (unsigned long long)hsum);
+  }
 }
 
-// Fused exchange, phase A: the block's histogram cells [cb, cb + m - 1) and the totals cell (LDS slot
-// m - 1), summed over the NR ranks' send slots into LDS. Every cell's NR loads are in flight together
+// Fused exchange, phase A: the block's histogram cells [cb, cb + mt) and, after them, the totals cell
+// (LDS slot mt) and at level 0 the replica-digest cell (slot mt + 1), m cells in all, summed over the
+// NR ranks' send slots into LDS. Every cell's NR loads are in flight together
 // (one remote round trip per block instead of one per rank); `store`: the sums also go to hist_b
 // (the built child's global histogram, for the next level's subtraction), `store_tot`: the totals too.
 template <int NR>
-__device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pair_bytes, int cb, int m, int ncells,
+__device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m, int ncells,
                                               longlong2* s_cells, longlong2* hbw, bool store, bool store_tot) {
   const char* sp[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r) sp[r] = iv->slot[r] + pair_bytes;
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    const int cell = i < m - 1 ? cb + i : ncells;
+    const int cell = i < mt ? cb + i : ncells + (i - mt);
     longlong2 t[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) t[r] = *reinterpret_cast<const longlong2*>(sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2));
@@ -1496,18 +1551,18 @@ __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pa
       acc.y += t[r].y;
     }
     s_cells[i] = acc;
-    if (i < m - 1 ? store : store_tot) hbw[cell] = acc;
+    if (i < mt ? store : store_tot) hbw[cell] = acc;
   }
 }
 
 // 9-16 ranks (more than one 8-GPU node's worth of processes): two groups of 8 loads per cell, so no
 // instantiation holds more than 8 ranks' values in registers (the fused k_eval keeps the parent's
 // histogram loads in flight across the exchange and spilled with 16)
-__device__ __forceinline__ void ipc_sum_cells_wide(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int m,
+__device__ __forceinline__ void ipc_sum_cells_wide(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m,
                                                    int ncells, longlong2* s_cells, longlong2* hbw, bool store,
                                                    bool store_tot) {
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    const int cell = i < m - 1 ? cb + i : ncells;
+    const int cell = i < mt ? cb + i : ncells + (i - mt);
     const int64_t off = pair_bytes + (int64_t)cell * (int64_t)sizeof(longlong2);
     longlong2 acc = make_longlong2(0, 0);
 #pragma unroll
@@ -1523,20 +1578,20 @@ __device__ __forceinline__ void ipc_sum_cells_wide(int nr, const IpcFusedView* i
       }
     }
     s_cells[i] = acc;
-    if (i < m - 1 ? store : store_tot) hbw[cell] = acc;
+    if (i < mt ? store : store_tot) hbw[cell] = acc;
   }
 }
 
-__device__ __forceinline__ void ipc_sum_cells_n(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int m,
+__device__ __forceinline__ void ipc_sum_cells_n(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m,
                                                 int ncells, longlong2* s_cells, longlong2* hbw, bool store,
                                                 bool store_tot) {
   switch (nr) {
 #define IPC_SUM_CASE(K) \
-    case K: ipc_sum_cells<K>(iv, pair_bytes, cb, m, ncells, s_cells, hbw, store, store_tot); break;
+    case K: ipc_sum_cells<K>(iv, pair_bytes, cb, mt, m, ncells, s_cells, hbw, store, store_tot); break;
     IPC_SUM_CASE(1) IPC_SUM_CASE(2) IPC_SUM_CASE(3) IPC_SUM_CASE(4) IPC_SUM_CASE(5) IPC_SUM_CASE(6)
     IPC_SUM_CASE(7) IPC_SUM_CASE(8)
 #undef IPC_SUM_CASE
-    default: ipc_sum_cells_wide(nr, iv, pair_bytes, cb, m, ncells, s_cells, hbw, store, store_tot); break;
+    default: ipc_sum_cells_wide(nr, iv, pair_bytes, cb, mt, m, ncells, s_cells, hbw, store, store_tot); break;
   }
 }
 
@@ -1684,19 +1739,24 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
     const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
     cb = kGroups ? d.hoff[fbeg] : 0;
     const int ce = kGroups ? d.hoff[fend] : d.ncells;
-    if (blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
+    // (k_eval_part publishes before its plan: its block 0 is not always an evaluating block)
+    if (!kMerged && blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
     if (!ipc_wait(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout)) return false;
     // the global root totals are stored at level 0 (k_eval_finish reads them)
+    // (+ the replica-digest cell at level 0)
     ipc_sum_cells_n(__builtin_amdgcn_readfirstlane(iv->n), iv, (int64_t)pair * SE * (int64_t)sizeof(int64_t), cb,
-                    ce - cb + 1, d.ncells, s_cells, reinterpret_cast<longlong2*>(d.hist_b[parity] + pair * SE),
-                    built && status == kActive, level == 0 && blockIdx.y == 0);
+                    ce - cb, ce - cb + 1 + (level == 0 && d.dig ? 1 : 0), d.ncells, s_cells,
+                    reinterpret_cast<longlong2*>(d.hist_b[parity] + pair * SE), built && status == kActive,
+                    level == 0 && blockIdx.y == 0);
     __syncthreads();
     const longlong2 tot = s_cells[ce - cb];
     rg = tot.x;
     rh = tot.y;
   }
   // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
-  const int64_t G = readlane64(level == 0 ? rg : ng, 0), H = readlane64(level == 0 ? rh : nh, 0);
+  int64_t G = readlane64(level == 0 ? rg : ng, 0);
+  const int64_t H = readlane64(level == 0 ? rh : nh, 0);
+  if (level == 0 && d.corrupt) G += (int64_t)1 << 24;  // fault injection: this rank grows a different tree
   // No early return for an inactive node: a branch here let hipcc sink the feature metadata loads
   // below it (a third dependent round trip). Its block computes on valid buffers and stores nothing.
   const bool active = kMerged ? status != kNone : status == kActive;
@@ -1852,6 +1912,17 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
       s_out->nb = (!kGroups && best.key != 0x7fffffff) ? s_nb[(best.key >> 10) & 31] : 0;
       s_out->G = G;
       s_out->H = H;
+      // replica check of the previous tree (data parallel; off the evaluation's critical path)
+      if (level == 0 && d.dig && blockIdx.x == 0 && blockIdx.y == 0) {
+        int64_t dsum;
+        if (kFused) {
+          const int nc = kGroups ? d.hoff[fend] - d.hoff[fbeg] : d.ncells;
+          dsum = s_cells[nc + 1].x;
+        } else {
+          dsum = hb[SE];
+        }
+        digest_check(d, dsum);
+      }
     }
   }
   return true;
@@ -2089,6 +2160,7 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
   wave_best(best, best_cut);
   if (t != 0) return;
   const int wf = best.key != 0x7fffffff ? (best.key >> 10) : 0;
+  if (level == 0) digest_check(d, hb[SE]);
   eval_finalize(d, level, n, G, H, best, best_cut, s_nb[wf]);
   stamp_.probe(4);
 }
@@ -2248,27 +2320,51 @@ __device__ __forceinline__ bool split_decision(const GbdtDev& d, const Cand& bes
   return ok;
 }
 
-template <int kSteps>
+// Data-parallel form (kDP, the fused IPC exchange): only the node's FIRST block (its lead) evaluates:
+// it waits for the ranks, sums their cells (eval_core<kFused>), finalises the node and publishes the
+// decision {tag, ok, default direction, feature, bin} as ONE 8-byte write-through granule; the node's
+// other blocks poll that granule (their row ids are loaded meanwhile). Reading every rank's cells in
+// every block would multiply the xGMI traffic by the node's item count. Forward progress: a waiting
+// block only waits for a lower-indexed block of the same launch, and the host launches this form only
+// while the whole grid is resident at once (items + nodes <= CUs, one 1024-thread block per CU), so
+// the lead is running or done. Every active node gets at least one (possibly empty) item, so each
+// rank finalises every node of the level, also those it holds no rows of. Block 0 publishes this
+// rank's slot before its plan (every epoch, whatever the level holds).
+typedef __attribute__((address_space(1))) unsigned long long gu64;  // global (not flat) accesses
+
+__device__ __forceinline__ uint64_t part_decision_word(uint32_t tag, bool ok, bool fail, int f, int j, bool dl) {
+  const uint32_t v = (ok ? 1u : 0u) | (fail ? 2u : 0u) | (dl ? 4u : 0u) | ((uint32_t)f & 0xFFu) << 8 |
+                     ((uint32_t)(j + 1) & 0x3FFu) << 16;
+  return ((uint64_t)tag << 32) | v;
+}
+
+// kMode: 0 = one GPU; 1 = data parallel with the level's global histograms already in hist_b (RCCL /
+// separate IPC exchange): every block evaluates, every active node gets an item; 2 = data parallel
+// over the fused IPC exchange: the lead-decides form above.
+template <int kSteps, int kMode>
 __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64_t zero_next, int level, int chunk,
-                                                    int tree, EvalSlots es) {
+                                                    int tree, EvalSlots es, uint32_t tag) {
   constexpr int kPW = 16;  // waves
   BlockStamp stamp_(d);
   __shared__ int32_t s_cnt[2][kPW];
   __shared__ int32_t s_base[2];
   __shared__ int s_plan[5];
   __shared__ EvalOut s_out;
-  {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
-    int4* zp = reinterpret_cast<int4*>(d.hist_b[parity ^ 1]);
+  __shared__ uint32_t s_dec;
+  {  // zero the next level's reduce destination (hist_b of the other parity, or the next IPC send slot)
+    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
     const int64_t nz = zero_next / 2;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
   }
+  constexpr bool kDP = kMode == 2;
+  if (kDP && blockIdx.x == 0) ipc_publish(d.ipcv[d.ipc_epoch & 1u].myflag, d.ipc_epoch);
   const int item = blockIdx.x;
   const int first = (1 << level) - 1;
-  const PlanOut pl = block_plan(1 << level, chunk, item, [&](int e) {
+  const PlanOut pl = block_plan<kMode != 0>(1 << level, chunk, item, [&](int e) {
     const Node& n = d.nodes[first + e];
     const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
-    return (st != kNone && cnt > 0) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
+    return (st != kNone && (kMode != 0 || cnt > 0)) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
   }, s_plan);
   if (pl.node < 0) return;
   const int node = pl.node;
@@ -2281,24 +2377,73 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   const int per = ((len + kPW - 1) / kPW + kWave - 1) / kWave * kWave;
   const int wb = min(pl.end, pl.begin + wv * per), we = min(pl.end, wb + per);
   int r[kSteps];
+  auto load_rows = [&]() {
 #pragma unroll
-  for (int k = 0; k < kSteps; ++k) {
-    const int i = wb + k * kWave + lane;
-    const int ic = min(i, pl.end - 1);
-    const int rv = identity ? ic : cur[ic];
-    r[k] = i < we ? rv : -1;
-  }
+    for (int k = 0; k < kSteps; ++k) {
+      const int i = wb + k * kWave + lane;
+      const int ic = max(min(i, pl.end - 1), 0);
+      const int rv = identity ? ic : cur[ic];
+      r[k] = i < we ? rv : -1;
+    }
+  };
   const int nstart = d.nodes[node].start, ncount = d.nodes[node].count;
   const bool lead = pl.begin == nstart;  // the node's first item
-  eval_core<false, false, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, lead);
-  __syncthreads();
-  const Cand best = s_out.best;
   int f, j;
-  bool dlb;
-  const bool ok = split_decision(d, best, s_out.nb, f, j, dlb);
-  if (lead && threadIdx.x == 0) eval_finalize(d, level, node, s_out.G, s_out.H, best, s_out.cut, s_out.nb);
+  bool dlb, ok;
+  if (!kDP) {  // every block evaluates its node itself (local histograms: L2-hot, no waiting)
+    load_rows();
+    eval_core<false, false, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, lead);
+    __syncthreads();
+    const Cand best = s_out.best;
+    ok = split_decision(d, best, s_out.nb, f, j, dlb);
+    if (lead && threadIdx.x == 0) eval_finalize(d, level, node, s_out.G, s_out.H, best, s_out.cut, s_out.nb);
+  } else {
+    uint64_t* dec = reinterpret_cast<uint64_t*>(d.dec) + node;
+    if (lead) {
+      const bool good = eval_core<false, true, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, true);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int ff = 0, jj = -1;
+        bool dd = false, oo = false;
+        if (good) {
+          oo = split_decision(d, s_out.best, s_out.nb, ff, jj, dd);
+          eval_finalize(d, level, node, s_out.G, s_out.H, s_out.best, s_out.cut, s_out.nb);
+        }
+        const uint64_t w = part_decision_word(tag, oo, !good, ff, jj, dd);
+        __hip_atomic_store((gu64*)dec, (unsigned long long)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_dec = (uint32_t)w;
+      }
+    } else {
+      load_rows();
+    }
+    if (!lead && threadIdx.x == 0) {  // poll the lead's granule (one lane), bounded by the group's deadline
+      const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t v = 2u;  // failed unless the lead's word arrives
+      for (;;) {
+        const uint64_t w = __hip_atomic_load((gu64*)dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(w >> 32) == tag) { v = (uint32_t)w; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > iv->timeout) {
+          __hip_atomic_store(iv->myflag + kIpcStickyWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(iv->err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_dec = v;
+    }
+    __syncthreads();
+    const uint32_t v = s_dec;
+    if (v & 2u) return;  // the exchange failed (the host watchdog reports it)
+    // the lead loads its row ids after its evaluation: held across it, they spilled
+    if (lead) load_rows();
+    ok = (v & 1u) != 0;
+    dlb = (v & 4u) != 0;
+    f = (int)((v >> 8) & 0xFFu);
+    j = (int)((v >> 16) & 0x3FFu) - 1;
+  }
   stamp_.probe(4);
-  if (!ok) return;  // a leaf: its rows are not routed (block-uniform)
+  if (!ok || len == 0) return;  // a leaf (its rows are not routed) or an empty item (block-uniform)
   const uint8_t* col = d.binsT + (int64_t)f * d.ldt;
   uint8_t bv[kSteps];
 #pragma unroll
@@ -2513,6 +2658,10 @@ struct GbdtCtx {
   uint64_t eval_asg[4] = {~0ull, ~0ull, ~0ull, ~0ull};
   EvalSlots eval_slots{};  // the table with each slot's bin count and compact offset (k_eval<false> arguments)
   std::vector<int32_t> hoff_h;  // host copy of d.hoff (sizes k_eval's fused-exchange LDS)
+  int fit_first = 0;            // first tree this context grows in the current fit (no replica check)
+  uint32_t dec_tag = 0;         // k_eval_part<mode 2> decision-granule tag (one per launch)
+  int fault_tree = -1;          // fault injection: tree whose root totals are perturbed on this rank
+  unsigned* err_pinned = nullptr;  // mapped host word behind d.err_host
   // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
   const char* stamp_path = nullptr;
   int stamp_cap = 0;
@@ -2659,7 +2808,9 @@ static GradHistKernel grad_hist_kernel(int ft4) {
   }
 }
 
-// Compute units of the current device (256 on MI355X), cached per process.
+// Compute units of the current device (256 on MI355X), cached per process. COBALT_CU_BUDGET caps it
+// for a rank whose stream owns a CU-masked share of a device shared with other ranks
+// (parallel/cumask.py): the launch heuristics then size grids for the CUs the rank really has.
 static int device_cu_count() {
   static int n = 0;
   if (n <= 0) {
@@ -2667,6 +2818,8 @@ static int device_cu_count() {
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
       n = v;
     if (n <= 0) n = 256;
+    const char* b = getenv("COBALT_CU_BUDGET");
+    if (b && atoi(b) > 0) n = std::min(n, atoi(b));
   }
   return n;
 }
@@ -2740,7 +2893,8 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.ridx[0], N * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.ridx[1], N * sizeof(int32_t)))) return rc;
   for (int k = 0; k < 2; ++k) {
-    if ((rc = dev_alloc(c, (void**)&d.hist_b[k], hist_bytes))) return rc;
+    // + one int64 pair: the level-0 replica-digest cell after the root slot (data parallel)
+    if ((rc = dev_alloc(c, (void**)&d.hist_b[k], hist_bytes + 2 * sizeof(int64_t)))) return rc;
     if ((rc = dev_alloc(c, (void**)&d.hist_s[k], 2 * hist_bytes))) return rc;  // node-indexed
   }
   if ((rc = dev_alloc(c, (void**)&d.nodes_buf[0], c->max_nodes * sizeof(Node)))) return rc;
@@ -2752,9 +2906,18 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.counters, 16 * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cand, (size_t)c->pairs_max * 64 * sizeof(CandRec)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.dec, c->max_nodes * sizeof(uint64_t)))) return rc;
+  CK(hipMemset(d.dec, 0, c->max_nodes * sizeof(uint64_t)));
   if (cfg->comm) {  // local histograms of every node of a level (positions 0 .. 2^(max_depth-1))
     for (int k = 0; k < 2; ++k)
       if ((rc = dev_alloc(c, (void**)&d.hist_loc[k], 2 * hist_bytes))) return rc;
+    // replica check: per-tree-parity digest accumulators and the mapped host error word
+    if ((rc = dev_alloc(c, (void**)&d.dig, 4 * sizeof(int64_t)))) return rc;
+    CK(hipMemset(d.dig, 0, 4 * sizeof(int64_t)));
+    CK(hipHostMalloc((void**)&c->err_pinned, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->err_pinned, 0, 64);
+    CK(hipHostGetDevicePointer((void**)&d.err_host, c->err_pinned, 0));
+    d.world = cfg->world_size;
   }
   if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
@@ -2889,6 +3052,18 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   return 0;
 }
 
+static void launch_eval_part(int steps, int mode, dim3 grid, size_t lds, hipStream_t stream, const GbdtDev& d, int parity,
+                             int64_t zero_next, int level, int chunk, int tree, const EvalSlots& es, uint32_t tag) {
+#define EP_LAUNCH(S, M) \
+  hipLaunchKernelGGL((k_eval_part<S, M>), grid, dim3(1024), lds, stream, d, parity, zero_next, level, chunk, tree, es, tag)
+  if (steps <= 4) {
+    if (mode == 0) EP_LAUNCH(4, 0); else if (mode == 1) EP_LAUNCH(4, 1); else EP_LAUNCH(4, 2);
+  } else {
+    if (mode == 0) EP_LAUNCH(8, 0); else if (mode == 1) EP_LAUNCH(8, 1); else EP_LAUNCH(8, 2);
+  }
+#undef EP_LAUNCH
+}
+
 // Enqueue `n_trees` boosting rounds starting at tree index `t0`. No host synchronisation.
 // `sampled`: the row records already hold the (reweighted) gradient pairs of this tree's rows --
 // the external-memory path, where k_ooc_page wrote a fresh sample -- so the tree starts with a
@@ -2910,7 +3085,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const bool ipc = dp && cc->kind == 2;
   d.hist_red = nullptr;
   if (ipc) {
-    if (ipc_capacity(cc) < (int64_t)c->pairs_max * d.slot_elems * (int64_t)sizeof(int64_t)) {
+    if (ipc_capacity(cc) < ((int64_t)c->pairs_max * d.slot_elems + 2) * (int64_t)sizeof(int64_t)) {
       comm_set_error("ipc: slot capacity below one level of histograms (raise COBALT_IPC_SLOT_MB)");
       return -14;
     }
@@ -2946,7 +3121,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     for (int f0 = 0; f0 < d.F; f0 += eval_fg)
       fused_cells = std::max(fused_cells, c->hoff_h[std::min(d.F, f0 + eval_fg)] - c->hoff_h[f0]);
   }
-  const size_t fused_lds = (size_t)(fused_cells + 1) * 16;
+  const size_t fused_lds = (size_t)(fused_cells + 2) * 16;  // + the totals and the level-0 digest cells
   const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part && fused_lds <= 65536;
   d.ipc_epoch = 0;
   d.ipcv = ipc_fused ? ipc_device_views(cc) : nullptr;
@@ -2956,9 +3131,24 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // two evaluations per CU). COBALT_EVAL_PART=0 / 2 disables / forces it.
   static const int env_ep = getenv("COBALT_EVAL_PART") ? atoi(getenv("COBALT_EVAL_PART")) : 1;
   const int ep_steps = ceil_div(chunk_part(d), 16 * kWave);
-  const bool eval_part = env_ep != 0 && !dp && eval_fg == 0 && !eval_compact && !fuse_part && part_wide(d) &&
-                         ep_steps <= 8 && d.F <= 32 &&
-                         (env_ep == 2 || ceil_div(d.n, chunk_part(d)) <= device_cu_count());
+  // data parallel: the lead-decides form over the fused IPC exchange (mode 2), or every block evaluating
+  // from the all-reduced hist_b (mode 1: RCCL / separate exchange)
+  const int ep_mode = !dp ? 0 : (ipc_fused ? 2 : 1);
+  const bool eval_part = env_ep != 0 && eval_fg == 0 && !eval_compact && !fuse_part && part_wide(d) &&
+                         ep_steps <= 8 && d.F <= 32 && (ep_mode != 2 || fused_lds <= 65536);
+  // Item size of a level's fused pass: the grid (items + one partial item per node) must fit one
+  // 1024-thread block per CU -- beyond that a second round of blocks doubles the level (1M rows with
+  // 4096-row items: levels 4-5 launched 261 / 277 blocks on 256 CUs), and the data-parallel form
+  // relies on the whole grid being resident at once. The partition item size while it fits, else
+  // 8192 rows, else the level runs the separate evaluation + partition (0). COBALT_EVAL_PART=2 forces
+  // the fusion on one GPU (8192-row items when none fits).
+  auto ep_chunk = [&](int level) -> int {
+    if (!eval_part) return 0;
+    const int cus = device_cu_count();
+    for (int ch = chunk_part(d); ch <= 8192; ch *= 2)
+      if (ceil_div(d.n, ch) + (1 << level) <= cus) return ch;
+    return (env_ep == 2 && ep_mode == 0) ? 8192 : 0;
+  };
   d.zero_red = nullptr;
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
@@ -2984,6 +3174,9 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     if (t >= c->cfg.max_trees) return -10;
     d.nodes = d.nodes_buf[t & 1];
     d.prev_nodes = d.nodes_buf[(t + 1) & 1];
+    d.dig_slot = t & 1;
+    d.dig_check = t > c->fit_first ? 1 : 0;
+    d.corrupt = t == c->fault_tree ? 1 : 0;
     d.stamps = stamp_tree(c, t) ? c->stamp_buf : nullptr;
     const int apply = (t >= 1 && c->applied == t - 1) ? t - 1 : -1;  // prediction-cache update
     // the root pass zeroes the root's reduce destination (under the fused exchange: the next send slot)
@@ -3019,9 +3212,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
                   stream, d, parity, t, level, chh);
       }
+      // this level's evaluation runs in the partition pass (k_eval_part), with items of ep_ch rows
+      const int ep_ch = level + 1 < D ? ep_chunk(level) : 0;
+      const bool ep_level = ep_ch > 0;
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
-              dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap));
+              dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap), level);
       CK_LAUNCH();
       if (dp) {
         // row-count choice: ranks built their locally smaller child -> turn it into the local LEFT
@@ -3033,19 +3229,20 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           CK_LAUNCH();
         }
         int rc;
+        // level 0 carries the replica-digest cell after the root slot (see GbdtDev::dig)
+        const int64_t count = (int64_t)slots * d.slot_elems + (level == 0 ? 2 : 0);
         if (ipc_fused) {  // k_eval exchanges this epoch itself
           d.ipc_epoch = ipc_next_epoch(cc);
           rc = 0;
         } else if (ipc) {  // the exchange also zeroes the next level's send slot (next tree's root after the last)
           const int64_t next_slots = level + 1 < D ? (1 << level) : 1;
-          rc = ipc_exchange(cc, d.hist_b[parity], (int64_t)slots * d.slot_elems, 0, 0,
-                            next_slots * d.slot_elems * (int64_t)sizeof(int64_t), stream);
+          rc = ipc_exchange(cc, d.hist_b[parity], count, 0, 0, next_slots * d.slot_elems * (int64_t)sizeof(int64_t),
+                            stream);
         } else {
-          rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], (int64_t)slots * d.slot_elems, stream);
+          rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.hist_b[parity], count, stream);
         }
         if (rc) return rc;
       }
-      const bool ep_level = eval_part && level + 1 < D;  // this level's evaluation runs in k_eval_part
       if (ep_level) {
       } else if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
         const int ng = ceil_div(d.F, eval_fg);
@@ -3066,9 +3263,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           GLAUNCH("k_eval", (k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F,
                   c->eval_slots);
       }
-      d.ipc_epoch = 0;
       if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
-        const int chp = chunk_part(d);
+        const int chp = ep_level ? ep_ch : chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
         // (under the separate IPC exchange it overwrites the next level's hist_b slots whole: nothing to
         // zero; under the fused one the next level's send slot is the reduce destination to zero)
@@ -3076,13 +3272,13 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         d.zero_red = ipc_fused ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
         const int pw = part_wide(d) ? 16 : 4;
         const int steps = ceil_div(chp, pw * kWave);  // <= kPartSteps (chunk_part's cap)
-        if (ep_level && steps <= 4)
-          GLAUNCH("k_eval_part", k_eval_part<4>, dim3(ubp), dim3(1024), 0, stream, d, parity, zero_next, level, chp, t,
-                  c->eval_slots);
-        else if (ep_level)
-          GLAUNCH("k_eval_part", k_eval_part<8>, dim3(ubp), dim3(1024), 0, stream, d, parity, zero_next, level, chp, t,
-                  c->eval_slots);
-        else if (pw == 16 && steps <= 4)
+        if (ep_level) {
+          const uint32_t tag = ++c->dec_tag;  // unique per launch: the decision granules need no reset
+          const size_t lds = ep_mode == 2 ? fused_lds : 0;
+          c->d.seq = stamp_next(c, "k_eval_part");
+          launch_eval_part(steps <= 4 ? 4 : 8, ep_mode, dim3(ubp), lds, stream, d, parity, zero_next, level, chp, t,
+                           c->eval_slots, tag);
+        } else if (pw == 16 && steps <= 4)
           GLAUNCH("k_partition", (k_partition<16, 4>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
                   level, chp);
         else if (pw == 16 && steps <= 8)
@@ -3095,6 +3291,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           GLAUNCH("k_partition", (k_partition<4, kPartSteps>), dim3(ubp), dim3(4 * kWave), 0, stream, d, parity,
                   zero_next, level, chp);
       }
+      d.ipc_epoch = 0;
       CK_LAUNCH();
     }
     c->grown = t + 1;
@@ -3184,6 +3381,20 @@ COBALT_API int cobalt_gbdt_set_start(void* h, int t0) {
   if (t0 < 0 || t0 > c->cfg.max_trees || c->grown != 0) return -12;
   c->grown = t0;
   c->applied = t0;
+  c->fit_first = t0;
+  return 0;
+}
+
+// Data-parallel replica check: 0 = healthy, 2 = this rank's trees diverged from its peers' (see
+// GbdtDev::dig). Read by the host after / while a segment of trees runs.
+COBALT_API int cobalt_gbdt_error(void* h) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  return c && c->err_pinned ? (int)__atomic_load_n(c->err_pinned, __ATOMIC_ACQUIRE) : 0;
+}
+
+// Fault injection (tests): perturb tree `t`'s root totals on this rank, so its replica diverges.
+COBALT_API int cobalt_gbdt_set_fault(void* h, int t) {
+  static_cast<GbdtCtx*>(h)->fault_tree = t;
   return 0;
 }
 
@@ -3217,6 +3428,9 @@ COBALT_API int cobalt_gbdt_reuse(void* h, const GbdtConfig* cfg) {
   d.seed = cfg->seed;
   c->grown = 0;
   c->applied = 0;
+  c->fit_first = 0;
+  c->fault_tree = -1;
+  if (c->err_pinned) memset(c->err_pinned, 0, 64);
   return 0;
 }
 
@@ -3224,6 +3438,7 @@ COBALT_API int cobalt_gbdt_destroy(void* h) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   if (!c) return 0;
   for (void* p : c->allocs) (void)hipFree(p);
+  if (c->err_pinned) (void)hipHostFree(c->err_pinned);
   delete c;
   return 0;
 }

@@ -488,13 +488,22 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         try:
             if T0:
                 tr.set_start(T0)
+            if world > 1:
+                # COBALT_FAULT_CORRUPT_RANK=r [COBALT_FAULT_CORRUPT_TREE=t]: rank r grows a different tree t
+                # (its root totals perturbed), which the in-flight replica check must catch on every rank
+                cr = int(os.environ.get("COBALT_FAULT_CORRUPT_RANK", "-1") or -1)
+                if cr == dist.rank:
+                    tr.set_fault(int(os.environ.get("COBALT_FAULT_CORRUPT_TREE", "1") or 1))
             for s0 in range(T0, T, seg):
                 s1 = min(T, s0 + seg)
                 tr.grow(s0, s1 - s0)
                 if world > 1:  # fail fast (abort the communicator) if a peer rank dies mid-segment
-                    _watch_segment(dist, dev, s0, s1)
+                    _watch_segment(dist, dev, s0, s1, tr)
                 tp = rep.mark("grow", tp, dev)
                 seg_nodes = tr.fetch(s0, s1 - s0)
+                if world > 1 and tr.replica_error():
+                    raise ReplicaDivergence(f"data-parallel replicas diverged before tree {s1} (rank {dist.rank}): "
+                                            "the ranks' split decisions differ (in-flight digest check)")
                 tp = rep.mark("fetch", tp, dev)
                 segment_done(seg_nodes, s1)
                 tp = rep.mark("convert", tp, dev)
@@ -537,7 +546,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     return bst
 
 
-def _watch_segment(dist, dev, s0: int, s1: int) -> None:
+def _watch_segment(dist, dev, s0: int, s1: int, tr=None) -> None:
     from .. import _native
     from ..parallel import dist as pdist
 
@@ -545,13 +554,23 @@ def _watch_segment(dist, dev, s0: int, s1: int) -> None:
     ev.record()
     comm = dist.native_comm
     lib = _native.lib()
-    pdist.wait_with_watchdog(ev.query, timeout_s=pdist.collective_timeout_s(),
-                             comm_error=(lambda: lib.cobalt_comm_async_error(ctypes.c_void_p(comm))) if comm else None,
+
+    def comm_error():
+        e = lib.cobalt_comm_async_error(ctypes.c_void_p(comm)) if comm else 0
+        return e
+    # a replica divergence does not stop the stream (every rank keeps exchanging in step): the segment
+    # finishes and the caller raises ReplicaDivergence after it, on every rank
+    pdist.wait_with_watchdog(ev.query, timeout_s=pdist.collective_timeout_s(), comm_error=comm_error if comm else None,
                              abort=lambda: pdist.abort_native_comm(dist), what=f"trees {s0}..{s1 - 1}")
 
 
 class InjectedFault(RuntimeError):
     """Raised by the fault-injection hook (``COBALT_FAULT_AFTER_TREES`` [+ ``COBALT_FAULT_RANK``])."""
+
+
+class ReplicaDivergence(RuntimeError):
+    """Data-parallel ranks grew different trees (a stale or corrupted exchange on some rank). Raised on
+    every rank of the fit: each one's digest check compares the ranks' summed digests with its own."""
 
 
 class Checkpointer:

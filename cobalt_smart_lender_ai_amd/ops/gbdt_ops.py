@@ -207,6 +207,15 @@ class GpuGbdtTrainer:
         _native.check(rc, "cobalt_gbdt_set_binary_labels")
         return True
 
+    def replica_error(self) -> int:
+        """Data-parallel replica check (csrc/gbdt.hip GbdtDev::dig): 0 = healthy, 2 = this rank's trees
+        diverged from its peers' (detected at level 0 of the tree after the divergent one)."""
+        return int(self.lib.cobalt_gbdt_error(self.h)) if self.h else 0
+
+    def set_fault(self, tree: int) -> None:
+        """Fault injection (tests): perturb tree ``tree``'s root totals on this rank only."""
+        _native.check(self.lib.cobalt_gbdt_set_fault(self.h, int(tree)), "cobalt_gbdt_set_fault")
+
     def set_start(self, t0: int) -> None:
         """Continue boosting at global tree index ``t0`` (margins already hold trees < t0)."""
         _native.check(self.lib.cobalt_gbdt_set_start(self.h, t0), "cobalt_gbdt_set_start")

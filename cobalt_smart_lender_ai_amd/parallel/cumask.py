@@ -1,0 +1,63 @@
+"""CU partitioning for several ranks that share ONE GPU (the 1-GPU rehearsal of multi-GPU data
+parallelism).
+
+On an 8-GPU node every rank owns a whole device. When N rank processes share one device instead,
+their kernels compete for the same compute units, and the data-parallel exchange waits inside
+kernels (the fused IPC exchange of ``csrc/gbdt.hip``): with 8 ranks the blocks of 7 ranks that are
+already waiting can occupy every CU while the 8th rank's publishing block never gets one -- observed
+as a 120 s group deadline at 8 processes (round 4), while 2-4 processes ran. A GPU does not preempt a
+running wave for another process's queue, so the fix is the hardware's own partitioning: each rank
+launches on a stream whose CU mask (``hipExtStreamCreateWithCUMask``) holds a disjoint 1/N of the
+CUs, like a small GPU of its own. The mask interleaves the ranks (CU ``rank + k * N``), so every rank
+has CUs in every XCD whichever way the runtime maps mask bits onto the XCDs. ``COBALT_CU_BUDGET``
+tells the trainer's launch heuristics how many CUs it has (e.g. the fused evaluation + partition
+pass only runs while its whole grid is resident).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_HIP = None
+
+
+def _hip() -> ctypes.CDLL:
+    global _HIP
+    if _HIP is None:
+        p = Path(torch.__file__).parent / "lib" / "libamdhip64.so"
+        _HIP = ctypes.CDLL(str(p) if p.exists() else "libamdhip64.so")
+        _HIP.hipExtStreamCreateWithCUMask.restype = ctypes.c_int
+        _HIP.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                      ctypes.POINTER(ctypes.c_uint32)]
+    return _HIP
+
+
+def interleaved_mask(rank: int, world: int, n_cu: int) -> list[int]:
+    """32-bit mask words selecting CUs ``rank, rank + world, rank + 2 world, ...`` of ``n_cu``."""
+    words = [0] * ((n_cu + 31) // 32)
+    for cu in range(rank, n_cu, world):
+        words[cu // 32] |= 1 << (cu % 32)
+    return words
+
+
+def shared_device_stream(rank: int, world: int, device: torch.device) -> torch.cuda.ExternalStream:
+    """A stream of ``device`` restricted to this rank's 1/world of the CUs; sets ``COBALT_CU_BUDGET``
+    (call before the first fit: the trainer reads it once)."""
+    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = interleaved_mask(rank, world, n_cu)
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    h = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = _hip().hipExtStreamCreateWithCUMask(ctypes.byref(h), len(words), arr)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    os.environ["COBALT_CU_BUDGET"] = str(sum(bin(w).count("1") for w in words))
+    return torch.cuda.ExternalStream(h.value, device=device)
+
+
+def want_shared_mask(world: int) -> bool:
+    """Partition the CUs when ranks share a device (``COBALT_SHARED_CU_MASK``, default on for >= 2)."""
+    return world > 1 and os.environ.get("COBALT_SHARED_CU_MASK", "1") != "0"

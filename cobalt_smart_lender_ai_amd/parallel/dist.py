@@ -159,12 +159,14 @@ def _pick_transport(ctx: DistContext, transport: str | None) -> str:
 
 def create_native_comm(ctx: DistContext, transport: str | None = None) -> tuple[int, str]:
     """The trainer's native communicator and its transport name (see the module docstring). An
-    automatically chosen IPC group that fails its self-test falls back to RCCL with a warning."""
+    automatically chosen IPC group that fails on ANY rank (create, connect or self-test) falls back to
+    RCCL on EVERY rank: :func:`create_ipc_comm` agrees on the outcome over the torch group, so the
+    ranks always make the same choice and their torch collectives stay matched."""
     t = _pick_transport(ctx, transport)
     if t == "ipc":
         try:
             return create_ipc_comm(ctx), "ipc"
-        except Exception as e:  # noqa: BLE001
+        except IpcGroupFailed as e:
             if transport == "ipc" or os.environ.get("COBALT_DP_TRANSPORT", "auto").lower() == "ipc" \
                     or ctx.backend != "nccl":
                 raise
@@ -172,6 +174,10 @@ def create_native_comm(ctx: DistContext, transport: str | None = None) -> tuple[
 
             warnings.warn(f"IPC all-reduce group unavailable ({e}); using RCCL")
     return create_rccl_comm(ctx), "rccl"
+
+
+class IpcGroupFailed(RuntimeError):
+    """The IPC group could not be set up on at least one rank (raised on every rank together)."""
 
 
 def ipc_slot_bytes() -> int:
@@ -185,9 +191,22 @@ def ipc_timeout_s() -> float:
     return float(os.environ.get("COBALT_IPC_TIMEOUT_S", "120"))
 
 
+def _agree(ctx: DistContext, ok: bool) -> bool:
+    """True iff ``ok`` on every rank (a MIN all-reduce over the torch group; every rank must call)."""
+    if ctx.world <= 1:
+        return ok
+    return ctx.allreduce_scalar(1.0 if ok else 0.0, "min", ctx._coll_device("cpu")) > 0.5
+
+
 def create_ipc_comm(ctx: DistContext) -> int:
     """IPC one-shot group over the ranks of this node: export, all-gather the handles over the torch
-    group, map every peer, then a self-test all-reduce of a known pattern on both send slots."""
+    group, map every peer, then a self-test all-reduce of a known pattern on both send slots.
+
+    Every stage ends in an agreement (MIN of an ok flag over the torch group) that every rank reaches
+    whatever happened locally, so one rank's failure -- an export error, a mapping that does not open,
+    a self-test that times out or sums a stale peer copy -- fails the group on ALL ranks together
+    (:class:`IpcGroupFailed`). Nobody frees its exported slots before every rank has left the group's
+    kernels (device synchronise, then the agreement), so no peer can still be reading them."""
     from .. import _native
 
     lib = _native.lib()
@@ -197,29 +216,58 @@ def create_ipc_comm(ctx: DistContext) -> int:
     # the connect self-test runs under a short deadline (the ranks enter it together, right after the
     # handle all-gather): a group whose peer mappings do not work fails in seconds, not minutes
     connect_s = min(ipc_timeout_s(), float(os.environ.get("COBALT_IPC_CONNECT_TIMEOUT_S", "30")))
-    rc = lib.cobalt_ipc_create(ctx.rank, ctx.world, ipc_slot_bytes(), connect_s, ctypes.byref(h), mine)
-    if rc != 0:
-        raise RuntimeError(f"cobalt_ipc_create failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+    err = ""
+    created = False
     try:
-        if ctx.world > 1:
-            dev = ctx._coll_device("cpu")
-            t = torch.tensor(list(bytes(mine)), dtype=torch.uint8, device=dev)
-            outs = [torch.zeros_like(t) for _ in range(ctx.world)]
-            tdist.all_gather(outs, t)
-            blob = b"".join(bytes(o.cpu().tolist()) for o in outs)
-        else:  # a 1-rank group (exercises the protocol on one process)
-            blob = bytes(mine)
-        allh = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
-        rc = lib.cobalt_ipc_connect(h, allh)
+        rc = lib.cobalt_ipc_create(ctx.rank, ctx.world, ipc_slot_bytes(), connect_s, ctypes.byref(h), mine)
         if rc != 0:
-            raise RuntimeError(f"cobalt_ipc_connect failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
-        _ipc_selftest(ctx, int(h.value))
-        if lib.cobalt_ipc_set_timeout(h, ipc_timeout_s()) != 0:
-            raise RuntimeError(f"cobalt_ipc_set_timeout failed: {lib.cobalt_comm_last_error().decode()}")
-    except Exception:
-        lib.cobalt_comm_destroy(h, 1)
-        raise
+            raise RuntimeError(f"cobalt_ipc_create failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+        created = True
+    except Exception as e:  # noqa: BLE001 -- reported after the agreement
+        err = str(e)
+    # handle all-gather: every rank takes part, a failed rank contributes zeros
+    if ctx.world > 1:
+        dev = ctx._coll_device("cpu")
+        t = torch.tensor(list(bytes(mine)), dtype=torch.uint8, device=dev)
+        outs = [torch.zeros_like(t) for _ in range(ctx.world)]
+        tdist.all_gather(outs, t)
+        blob = b"".join(bytes(o.cpu().tolist()) for o in outs)
+    else:  # a 1-rank group (exercises the protocol on one process)
+        blob = bytes(mine)
+    ok = _agree(ctx, created)
+    if ok:
+        try:
+            allh = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
+            rc = lib.cobalt_ipc_connect(h, allh)
+            if rc != 0:
+                raise RuntimeError(f"cobalt_ipc_connect failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, str(e)
+        ok = _agree(ctx, ok)
+    if ok:
+        try:
+            _ipc_selftest(ctx, int(h.value))
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, str(e)
+        _quiesce()
+        ok = _agree(ctx, ok)
+    if ok:
+        if lib.cobalt_ipc_set_timeout(h, ipc_timeout_s()) != 0:  # host-side only: cannot fail on one rank
+            ok, err = False, f"cobalt_ipc_set_timeout failed: {lib.cobalt_comm_last_error().decode()}"
+    if not ok:
+        if created:
+            lib.cobalt_comm_destroy(h, 1)
+        raise IpcGroupFailed(err or "a peer rank could not join the IPC group")
     return int(h.value)
+
+
+def _quiesce() -> None:
+    """Wait until this rank's GPU work (the group's kernels) has finished, ignoring errors."""
+    try:
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001
+        pass
 
 
 def _ipc_selftest(ctx: DistContext, comm: int) -> None:
@@ -312,6 +360,25 @@ def abort_native_comm(ctx: DistContext) -> None:
 
         _native.lib().cobalt_comm_destroy(ctypes.c_void_p(ctx.native_comm), 1)
         ctx.native_comm = None
+
+
+def switch_transport(ctx: DistContext, transport: str) -> None:
+    """Replace the native communicator by one of ``transport`` on every rank (all ranks call it
+    together: e.g. after an agreed replica divergence on the IPC transport). Trainer contexts parked
+    for the old communicator are released first (they are keyed by it)."""
+    from ..ops import gbdt_ops
+
+    gbdt_ops.release_cached_trainers()
+    _quiesce()
+    ctx.barrier()
+    if ctx.native_comm:
+        from .. import _native
+
+        _native.lib().cobalt_comm_destroy(ctypes.c_void_p(ctx.native_comm), 0)
+        ctx.native_comm = None
+    ctx.barrier()
+    ctx.native_comm, ctx.transport = (create_rccl_comm(ctx), "rccl") if transport == "rccl" else \
+        (create_ipc_comm(ctx), "ipc")
 
 
 def get_context() -> DistContext:

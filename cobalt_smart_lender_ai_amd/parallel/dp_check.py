@@ -53,19 +53,28 @@ def rank_main(rank: int, world: int, port: int, out_dir: str, rows: int, params:
         from ..models import gbdt
         from . import dist as pdist
 
+        from . import cumask
+
         dev = torch.device("cuda", rank if one_gpu_per_rank else 0)
         torch.cuda.set_device(dev)
-        if world > 1:
-            backend = "nccl" if (one_gpu_per_rank and transport == "rccl") else "gloo"
-            ctx = pdist.init_from_env(backend=backend, native=True, transport=transport)
-            res["transport"] = ctx.transport
-        s, e = pdist.shard_range(rows, rank, world)
-        X, y = synth.make_lendingclub(e - s, seed=seed, row_offset=s, device=dev)
-        ck = str(Path(out_dir) / "ckpt.ubj") if checkpoint_every else None
-        t1 = time.monotonic()
-        b = gbdt.train(X, y, params, device=dev, dist=ctx, n_rows_global=rows, row_offset=s,
-                       checkpoint_path=ck, checkpoint_every=checkpoint_every, resume=False)
-        res["fit_s"] = time.monotonic() - t1
+        stream = None
+        if not one_gpu_per_rank and cumask.want_shared_mask(world):
+            # ranks sharing the device each get their own 1/world of the CUs (see parallel/cumask.py)
+            stream = cumask.shared_device_stream(rank, world, dev)
+            res["cu_budget"] = int(os.environ["COBALT_CU_BUDGET"])
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            if world > 1:
+                backend = "nccl" if (one_gpu_per_rank and transport == "rccl") else "gloo"
+                ctx = pdist.init_from_env(backend=backend, native=True, transport=transport)
+                res["transport"] = ctx.transport
+            s, e = pdist.shard_range(rows, rank, world)
+            X, y = synth.make_lendingclub(e - s, seed=seed, row_offset=s, device=dev)
+            ck = str(Path(out_dir) / "ckpt.ubj") if checkpoint_every else None
+            t1 = time.monotonic()
+            b = gbdt.train(X, y, params, device=dev, dist=ctx, n_rows_global=rows, row_offset=s,
+                           checkpoint_path=ck, checkpoint_every=checkpoint_every, resume=False)
+            torch.cuda.synchronize(dev)
+            res["fit_s"] = time.monotonic() - t1
         raw = b.save_raw("ubj")
         res["model_sha256"] = hashlib.sha256(raw).hexdigest()
         res["trees"] = b.num_trees
@@ -95,6 +104,14 @@ def rank_main(rank: int, world: int, port: int, out_dir: str, rows: int, params:
     except Exception:  # noqa: BLE001
         pass
     os._exit(0 if res["ok"] else 1)
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 def run(procs: int, rows: int = 300_000, params: dict | None = None, *, transport: str = "ipc",

@@ -28,16 +28,42 @@ def test_ipc_data_parallel_processes_equal_single_process():
     _check_clean(torch.cuda.is_initialized())
     ref = dp_check.run(1, ROWS)[0]
     assert ref["ok"], ref
-    # the exchange fused into the split evaluation (default) with 2 and 3 ranks, and the separate
-    # exchange kernel (COBALT_IPC_FUSED=0)
-    for procs, env in ((2, None), (3, None), (2, {"COBALT_IPC_FUSED": "0"})):
+    # the exchange fused into the split evaluation (default: the lead-decides evaluation + partition
+    # pass, k_eval_part mode 2, while a level's grid fits the rank's CUs, else k_eval) with 2, 3, 4 and 8
+    # ranks -- ipc_sum_cells<4> / <8> are what an 8-GPU node runs; the ranks share the device through
+    # disjoint CU masks (parallel/cumask.py) --, the fused k_eval alone (COBALT_EVAL_PART=0), and the
+    # separate exchange kernel (COBALT_IPC_FUSED=0: k_eval_part mode 1 over the all-reduced histograms)
+    for procs, env in ((2, None), (3, None), (4, None), (8, None), (2, {"COBALT_EVAL_PART": "0"}),
+                       (2, {"COBALT_IPC_FUSED": "0"})):
         got = dp_check.run(procs, ROWS, timeout_s=400, env=env)
         for g in got:
-            assert g["ok"], g
+            assert g["ok"], (procs, env, g)
             assert g["transport"] == "ipc"
             # one exchange per level per tree, plus the connect self-test's four (each slot twice)
             assert g["ipc_epochs"] == 4 + 7 * ref["trees"]
-            assert g["model_sha256"] == ref["model_sha256"], (procs, g["rank"])
+            assert g["model_sha256"] == ref["model_sha256"], (procs, env, g["rank"])
+
+
+@pytest.mark.timeout(600)
+def test_ipc_replica_divergence_fails_every_rank():
+    """Fault injection: rank 1 grows a different tree 1 (its root totals perturbed after the exchange,
+    as a stale peer read would). The in-flight digest check (csrc/gbdt.hip GbdtDev::dig) sees it at
+    level 0 of tree 2, on EVERY rank, and each raises ReplicaDivergence after that tree's segment --
+    not a silently divergent model at the end of the fit."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=8)
+    for procs in (2, 3):
+        got = dp_check.run(procs, 200_000, params, checkpoint_every=1, timeout_s=300,
+                           env={"COBALT_FAULT_CORRUPT_RANK": "1", "COBALT_FAULT_CORRUPT_TREE": "1"})
+        for g in got:
+            assert not g["ok"], g
+            assert g.get("error") == "ReplicaDivergence", g
+            assert "before tree 3" in g.get("message", ""), g  # detected within one tree
+    # the same fit without the fault: the check stays quiet
+    got = dp_check.run(2, 200_000, params, checkpoint_every=1, timeout_s=300)
+    assert all(g["ok"] for g in got), got
 
 
 @pytest.mark.timeout(600)
