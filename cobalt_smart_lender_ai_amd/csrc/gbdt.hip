@@ -3131,10 +3131,14 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // two evaluations per CU). COBALT_EVAL_PART=0 / 2 disables / forces it.
   static const int env_ep = getenv("COBALT_EVAL_PART") ? atoi(getenv("COBALT_EVAL_PART")) : 1;
   const int ep_steps = ceil_div(chunk_part(d), 16 * kWave);
-  // data parallel: the lead-decides form over the fused IPC exchange (mode 2), or every block evaluating
-  // from the all-reduced hist_b (mode 1: RCCL / separate exchange)
-  const int ep_mode = !dp ? 0 : (ipc_fused ? 2 : 1);
-  const bool eval_part = env_ep != 0 && eval_fg == 0 && !eval_compact && !fuse_part && part_wide(d) &&
+  // data parallel: every block evaluating from the all-reduced hist_b (mode 1: RCCL / the separate
+  // IPC exchange: +0.9 us per level over one GPU at 1.25M rows with a 1-rank RCCL group), or the
+  // lead-decides form over the fused IPC exchange (mode 2, COBALT_DP_EVAL_PART=1: with a 1-rank IPC
+  // group 88.5 ms per 1.25M-row fit against 86.2 for k_eval + k_partition -- the lead's evaluation, its
+  // hand-off and the late row / bin loads cost more than the launch they save -- so off by default)
+  static const int env_dp_ep = getenv("COBALT_DP_EVAL_PART") ? atoi(getenv("COBALT_DP_EVAL_PART")) : 0;
+  const int ep_mode = !dp ? 0 : (ipc_fused ? (env_dp_ep ? 2 : -1) : 1);
+  const bool eval_part = env_ep != 0 && ep_mode >= 0 && eval_fg == 0 && !eval_compact && !fuse_part && part_wide(d) &&
                          ep_steps <= 8 && d.F <= 32 && (ep_mode != 2 || fused_lds <= 65536);
   // Item size of a level's fused pass: the grid (items + one partial item per node) must fit one
   // 1024-thread block per CU -- beyond that a second round of blocks doubles the level (1M rows with

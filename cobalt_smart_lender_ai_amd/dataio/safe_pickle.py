@@ -197,7 +197,9 @@ class _Writer:
     def commit(self, force: bool = False) -> None:
         n = self.frame.tell()
         if n and (force or n >= _FRAME_TARGET):
-            self.out.write(b"\x95" + struct.pack("<Q", n) + self.frame.getvalue())  # FRAME
+            # pickle._Framer.commit_frame: frames shorter than _FRAME_SIZE_MIN (4) go out without a header
+            head = b"\x95" + struct.pack("<Q", n) if n >= 4 else b""
+            self.out.write(head + self.frame.getvalue())  # FRAME
             self.frame = io.BytesIO()
 
     def large(self, header: bytes, payload: bytes) -> None:

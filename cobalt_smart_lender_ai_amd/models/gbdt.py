@@ -223,6 +223,22 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = 1 << 18, dev
     if world > 1:
         has_missing = _allreduce_max_flags(has_missing, dist, dev)
     full = not sketch_rows
+    if full and dev.type == "cuda" and sketch_mode != "summary":
+        # every row, exactly (csrc/sketch.hip: bucket histograms + per-bucket selection, no row sort;
+        # under data parallelism the histograms are all-reduced, so the cuts are the full data's)
+        sw = _to_tensor(sketch_weights, dev).reshape(-1) if sketch_weights is not None else None
+        cuts, nbins = sketch.device_exact_cuts(Xt, max_bin, sw, has_missing, dist=dist if world > 1 else None,
+                                               row_offset=row_offset, n_rows_global=n_glob)
+        torch.cuda.synchronize(dev)
+        t_sketch = time.perf_counter() - ts
+        tb = time.perf_counter()
+        bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
+        from ..ops import gbdt_ops
+
+        bd.records, bd.binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
+        torch.cuda.synchronize(dev)
+        bd.t_bin = time.perf_counter() - tb
+        return bd
     stride = 1 if full else sketch.sample_stride(n_glob, sketch_rows)
     samp = sketch.local_sample(Xt, row_offset, stride)
     wsamp = None

@@ -364,3 +364,273 @@ def bin_matrix_host(X: np.ndarray, cuts: np.ndarray, nbins: np.ndarray) -> np.nd
 def full_bin_mask(nbins) -> np.ndarray:
     """Features whose uint8 code 255 is a real bin (256 bins, no missing values)."""
     return np.asarray(nbins) >= MAX_BINS
+
+
+def _sk_lib():
+    from .. import _native
+
+    lib = _native.lib()
+    if not getattr(lib, "_sk_declared", False):
+        import ctypes
+
+        V, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        lib.cobalt_sk_hist.restype = I
+        lib.cobalt_sk_hist.argtypes = [V, I64, I64, I, V, V, V, I, V, V, V, V]
+        lib.cobalt_sk_gather.restype = I
+        lib.cobalt_sk_gather.argtypes = [V, I64, I64, I, V, V, V, V, V, V, V, V, I, V]
+        lib.cobalt_sk_select.restype = I
+        lib.cobalt_sk_select.argtypes = [V, V, V, I, V, V, V, V, V, V]
+        for name in ("cobalt_sk_bounds", "cobalt_sk_buckets", "cobalt_sk_sort_cap"):
+            getattr(lib, name).restype = I
+            getattr(lib, name).argtypes = []
+        lib._sk_declared = True
+    return lib
+
+
+def _ptr(t):
+    return None if t is None else int(t.data_ptr())
+
+
+def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor | None = None,
+                      has_missing: torch.Tensor | None = None, *, dist=None, row_offset: int = 0,
+                      n_rows_global: int | None = None, w_max: float | None = None,
+                      sample_rows: int = 1 << 16) -> tuple[torch.Tensor, torch.Tensor]:
+    """:func:`compute_cuts` over EVERY row of ``X`` [N, F] (a CUDA tensor), bit for bit, without sorting
+    the rows (csrc/sketch.hip): sample boundaries split each feature's value axis into buckets, one
+    pass histograms the rows per bucket, the target ranks are located by prefix sums, and only the
+    rows of the few buckets that hold a target are gathered and sorted (in LDS, per bucket).
+
+    Under data parallelism (``dist``) every rank passes its shard: the sample is global (strided by
+    global row index), the bucket histograms are all-reduced and the candidates all-gathered, so all
+    ranks compute the cuts of the full data. ``w_max`` scales the weights (default: the global max)."""
+    from .. import _native
+
+    lib = _sk_lib()
+    N, F = X.shape
+    dev = X.device
+    world = dist.world if dist is not None else 1
+    n_glob = n_rows_global if n_rows_global is not None else N
+    NBND, NB, CAP = lib.cobalt_sk_bounds(), lib.cobalt_sk_buckets(), lib.cobalt_sk_sort_cap()
+    stream = _native.stream_handle()
+    X = X.to(torch.float32)
+    if has_missing is None:
+        has_missing = torch.isnan(X).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
+        if world > 1:
+            t = has_missing.to(torch.float32).to(dist._coll_device(dev))
+            dist.allreduce(t, "max")
+            has_missing = t.to(dev) > 0
+    maxb = feature_max_bins(max_bin, has_missing.to(dev))                            # [F] int64
+    XT = X.t().contiguous()                                                          # [F, N]
+    wq = None
+    if weights is not None:
+        wd = weights.to(device=dev, dtype=torch.float64).reshape(-1)
+        if w_max is None:
+            w_max = float(wd.max()) if wd.numel() else 0.0
+            if world > 1:
+                w_max = dist.allreduce_scalar(w_max, "max", dev)
+        if bool((wd < 0).any()) or not bool(torch.isfinite(wd).all()):
+            raise ValueError("sketch weights must be finite and >= 0")
+        scale = WEIGHT_SCALE / w_max if w_max and w_max > 0 else 0.0
+        wq = (torch.round(wd * scale) if scale else torch.ones_like(wd)).to(torch.int32).contiguous()
+
+    # 1. boundaries: <= NBND - 1 distinct values of the global strided sample
+    samp = local_sample(X, row_offset, sample_stride(n_glob, sample_rows))
+    if world > 1:
+        samp = dist.allgather_rows(samp)
+    sv = torch.sort((samp.t() + 0.0).contiguous(), dim=1).values                     # [F, S], NaN last
+    S = sv.shape[1]
+    K = NBND - 1
+    cnt = (~torch.isnan(sv)).sum(1)
+    bounds = torch.full((F, NBND + 1), float("inf"), dtype=torch.float32, device=dev)
+    if S:
+        pos = (torch.arange(K, device=dev)[None, :] * cnt[:, None]) // K
+        u = sv.gather(1, pos.clamp(max=S - 1))
+        ok = pos < cnt[:, None]
+        newv = ok.clone()
+        newv[:, 1:] &= u[:, 1:] != u[:, :-1]
+        slotp = torch.where(newv, torch.cumsum(newv.to(torch.int64), 1) - 1, NBND)
+        bounds.scatter_(1, slotp, u)
+        m = newv.sum(1).to(torch.int32)
+    else:
+        m = torch.zeros(F, dtype=torch.int32, device=dev)
+    bounds = bounds[:, :NBND].contiguous()
+
+    # 2. bucket histograms (row counts; weight sums when weighted) + min / max valid value
+    nblk = max(1, min(64, -(-N // 65536)))
+    cnt_slab = torch.zeros((nblk, F, NB), dtype=torch.int32, device=dev)
+    w_slab = torch.zeros((nblk, F, NB), dtype=torch.int64, device=dev) if wq is not None else None
+    bmm = torch.empty((nblk, F, 2), dtype=torch.float32, device=dev)
+    bmm[:, :, 0] = float("inf")
+    bmm[:, :, 1] = float("-inf")
+    if N:
+        rc = lib.cobalt_sk_hist(XT.data_ptr(), N, N, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), nblk,
+                                cnt_slab.data_ptr(), _ptr(w_slab), bmm.data_ptr(), stream)
+        _native.check(rc, "cobalt_sk_hist")
+    cnt_loc = cnt_slab.sum(0, dtype=torch.int64)                                      # [F, NB]
+    w_h = w_slab.sum(0) if w_slab is not None else None
+    vmin, vmax = bmm[:, :, 0].amin(0), bmm[:, :, 1].amax(0)
+    cnt_h = cnt_loc
+    if world > 1:
+        cd = dist._coll_device(dev)
+        cnt_h = cnt_loc.to(cd).clone()
+        dist.allreduce(cnt_h, "sum")
+        cnt_h = cnt_h.to(dev)
+        if w_h is not None:
+            t = w_h.to(cd)
+            dist.allreduce(t, "sum")
+            w_h = t.to(dev)
+        t = vmin.to(cd)
+        dist.allreduce(t, "min")
+        vmin = t.to(dev)
+        t = vmax.to(cd)
+        dist.allreduce(t, "max")
+        vmax = t.to(dev)
+    if w_h is None:
+        w_h = cnt_h
+
+    # 3. targets: bucket of every rank j * W / maxb; equal buckets ARE their value
+    C = torch.cumsum(w_h, 1)
+    W = C[:, -1]
+    jj = torch.arange(1, MAX_BINS, device=dev, dtype=torch.int64)                      # j = 1..255
+    thr = jj[None, :] * W[:, None]
+    b = torch.searchsorted((C * maxb[:, None]).contiguous(), thr.contiguous(), right=True).clamp(max=NB - 1)
+    inb = jj[None, :] < maxb[:, None]
+    eq_t = (b % 2) == 1
+    q = bounds.gather(1, ((b - 1) // 2).clamp(0, NBND - 1))
+    q = torch.where(W[:, None] > 0, q, vmax[:, None])                                  # W == 0: compute_cuts' clamp
+    nz = cnt_h > 0
+    E = nz[:, 1::2].sum(1)
+    O = nz[:, 0::2].sum(1)
+    many = (E + O) > maxb
+    exact_known = (O == 0) & (E <= maxb)
+    uncertain = (~many) & (O > 0)
+    need_t = inb & ~eq_t & (W[:, None] > 0) & ~exact_known[:, None]
+    sel = torch.zeros((F, NB), dtype=torch.bool, device=dev)
+    sel.scatter_(1, torch.where(need_t, b, NB - 1), True)
+    sel[:, NB - 1] = False  # (never a used bucket: m <= NBND - 1, so buckets end at 2m <= NB - 3)
+    even = (torch.arange(NB, device=dev) % 2) == 0
+    sel |= uncertain[:, None] & nz & even[None, :]
+    sel_f = sel.reshape(-1)
+    seg_of = torch.cumsum(sel_f.to(torch.int64), 0) - 1
+    slot = torch.where(sel_f, seg_of, -1).to(torch.int32).contiguous()
+    loc_sizes = cnt_loc.reshape(-1)[sel_f]                                             # this rank's rows per segment
+    glob_sizes = cnt_h.reshape(-1)[sel_f]
+    nseg = int(loc_sizes.numel())
+    loc_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
+    if nseg:
+        loc_off[1:] = torch.cumsum(loc_sizes, 0)
+    glob_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
+    if nseg:
+        glob_off[1:] = torch.cumsum(glob_sizes, 0)
+    tot_loc = int(loc_off[-1])
+
+    # 4. candidates: the rows of the selected buckets, per segment
+    cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)
+    cw = torch.empty(max(tot_loc, 1), dtype=torch.int32, device=dev) if wq is not None else None
+    if nseg and N:
+        cursor = torch.zeros(nseg, dtype=torch.int64, device=dev)
+        rc = lib.cobalt_sk_gather(XT.data_ptr(), N, N, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), slot.data_ptr(),
+                                  loc_off.data_ptr(), cursor.data_ptr(), cval.data_ptr(), _ptr(cw), nblk, stream)
+        _native.check(rc, "cobalt_sk_gather")
+    if world > 1 and nseg:  # every rank's candidates, re-packed segment by segment
+        cval, cw = _merge_candidates(dist, dev, cval[:tot_loc], None if cw is None else cw[:tot_loc], loc_sizes,
+                                     glob_off)
+
+    # 5. select the open targets from their bucket's sorted candidates
+    tf, tj = torch.nonzero(need_t, as_tuple=True)
+    T = int(tf.numel())
+    if T:
+        tb = b[tf, tj]
+        tseg = slot.reshape(F, NB)[tf, tb].to(torch.int64)
+        tgt_off = torch.zeros(nseg + 1, dtype=torch.int32, device=dev)
+        tgt_off[1:] = torch.cumsum(torch.bincount(tseg, minlength=nseg), 0).to(torch.int32)
+        prefix = torch.where(tb > 0, C[tf, (tb - 1).clamp(min=0)], torch.zeros_like(tb)).contiguous()
+        tthr = thr[tf, tj].contiguous()
+        tmaxb = maxb[tf].contiguous()
+        out = torch.empty(T, dtype=torch.float32, device=dev)
+        rc = lib.cobalt_sk_select(cval.data_ptr(), _ptr(cw), glob_off.data_ptr(), nseg, tgt_off.data_ptr(),
+                                  prefix.data_ptr(), tthr.data_ptr(), tmaxb.data_ptr(), out.data_ptr(), stream)
+        _native.check(rc, "cobalt_sk_select")
+        big = torch.nonzero(glob_sizes > CAP).reshape(-1).tolist()  # rare: segments beyond the LDS sort
+        for s in big:
+            t0, t1 = int(tgt_off[s]), int(tgt_off[s + 1])
+            if t0 == t1:
+                continue
+            o0, o1 = int(glob_off[s]), int(glob_off[s + 1])
+            vs, order = torch.sort(cval[o0:o1])
+            ws = (cw[o0:o1][order].to(torch.int64) if cw is not None else torch.ones_like(order))
+            cum = torch.cumsum(ws, 0)
+            key = ((prefix[t0:t1, None] + cum[None, :]) * tmaxb[t0:t1, None]).contiguous()
+            i = torch.searchsorted(key, tthr[t0:t1, None].contiguous(), right=True)[:, 0].clamp(max=o1 - o0 - 1)
+            out[t0:t1] = vs[i]
+        q[tf, tj] = out
+
+    # 6. the cut tables, as compute_cuts assembles them
+    trash = torch.full((F, 257), FLT_MAX, dtype=torch.float32, device=dev)
+    keep = inb & (q > vmin[:, None])
+    keep[:, 1:] &= q[:, 1:] != q[:, :-1]
+    qpos = torch.cumsum(keep.to(torch.int64), 1) - 1
+    cuts_q = trash.clone().scatter_(1, torch.where(keep, qpos, 256), q)
+    nbq = keep.sum(1) + 1
+    # exact path: one bin per distinct value (the sample's values that occur, + for the uncertain
+    # features the distinct values of their open buckets)
+    eqnz = nz[:, 1::2][:, :NBND]
+    nd = E.clone()
+    dv_rank = torch.cumsum(eqnz.to(torch.int64), 1) - 1
+    ex_ok = eqnz & (dv_rank >= 1)
+    cuts_ex = trash.clone().scatter_(1, torch.where(ex_ok, (dv_rank - 1).clamp(max=256), 256), bounds)
+    exact = exact_known.clone()
+    for f in torch.nonzero(uncertain).reshape(-1).tolist():
+        segs = torch.nonzero(slot.reshape(F, NB)[f] >= 0).reshape(-1)
+        parts = [bounds[f][eqnz[f]]]
+        for bb in segs.tolist():
+            s = int(slot.reshape(F, NB)[f, bb])
+            parts.append(cval[int(glob_off[s]):int(glob_off[s + 1])])
+        dv = torch.unique(torch.cat(parts))                                            # sorted
+        nd[f] = dv.numel()
+        if dv.numel() <= int(maxb[f]):
+            exact[f] = True
+            row = torch.full((257,), FLT_MAX, dtype=torch.float32, device=dev)
+            row[: dv.numel() - 1] = dv[1:]
+            cuts_ex[f] = row
+    nb_ex = torch.where(nd > 0, nd, torch.ones_like(nd))
+    cuts = torch.where(exact[:, None], cuts_ex[:, :256], cuts_q[:, :256]).contiguous()
+    nbv = torch.where(exact, nb_ex, nbq)
+    cuts.scatter_(1, (nbv - 1).clamp(min=0)[:, None], FLT_MAX)
+    return cuts + 0.0, nbv.to(torch.int32)
+
+
+def _merge_candidates(dist, dev, cval, cw, loc_sizes, glob_off):
+    """All ranks' candidate values (and weights) re-packed into the global segment layout: segment s
+    holds rank 0's values of s, then rank 1's, ... (the order inside a segment does not matter)."""
+    world = dist.world
+    cd = dist._coll_device(dev)
+    sizes = loc_sizes.to(cd)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    import torch.distributed as tdist
+
+    tdist.all_gather(all_sizes, sizes)
+    all_sizes = torch.stack(all_sizes).to(dev)                                         # [world, nseg]
+    vals = dist.allgather_rows(cval.reshape(-1, 1).to(cd), pad_value=0.0).to(dev)[:, 0]
+    per = vals.numel() // world
+    wts = None
+    if cw is not None:
+        wts = dist.allgather_rows(cw.to(torch.float64).reshape(-1, 1).to(cd), pad_value=0.0).to(dev)[:, 0]
+    nseg = all_sizes.shape[1]
+    before = torch.cumsum(all_sizes, 0) - all_sizes                                     # rows of lower ranks per segment
+    total = int(glob_off[-1])
+    out_v = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
+    out_w = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if cw is not None else None
+    for r in range(world):
+        sz = all_sizes[r]
+        n_r = int(sz.sum())
+        if n_r == 0:
+            continue
+        seg = torch.repeat_interleave(torch.arange(nseg, device=dev), sz)
+        loff = torch.cumsum(sz, 0) - sz
+        k = torch.arange(n_r, device=dev) - loff[seg]
+        dest = glob_off[:-1][seg] + before[r][seg] + k
+        out_v[dest] = vals[r * per:r * per + n_r]
+        if out_w is not None:
+            out_w[dest] = wts[r * per:r * per + n_r].to(torch.int32)
+    return out_v, out_w

@@ -163,13 +163,20 @@ def _bulk_inputs(data: bytes, feats: list, state: dict):
     return pd.read_csv(io.BytesIO(data)), None
 
 
-def _score_device(booster: Booster, Xd) -> np.ndarray:
+def _score_device(booster: Booster, Xd, lock=None) -> np.ndarray:
+    """Probabilities of a device-parsed bulk upload. Serialised with the scoring engine (its lock): the
+    MicroBatcher thread replays the engine's hipGraphs on the engine stream, and a bulk request must
+    neither capture a graph (global capture mode forbids other threads' stream syncs and allocator
+    calls meanwhile) nor run concurrently with another bulk capture. Per-request buffers are never
+    captured (``capture=False``): a one-off matrix gains nothing from a graph."""
+    import contextlib
+
     import torch
 
     from .batch_score import score_device_matrix
 
-    with torch.cuda.device(Xd.device):
-        return score_device_matrix(booster, Xd).cpu().numpy()
+    with (lock if lock is not None else contextlib.nullcontext()), torch.cuda.device(Xd.device):
+        return score_device_matrix(booster, Xd, capture=False).cpu().numpy()
 
 
 def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -> FastAPI:
@@ -254,7 +261,8 @@ def create_app(cfg: ServeConfig | None = None, booster: Booster | None = None) -
             # scored on a worker thread: the reference runs this blocking call on the event loop
             # (SURVEY App. B.8), which stalls every concurrent /predict request behind a bulk file
             if Xd is not None:
-                df["prob_default"] = await loop.run_in_executor(None, _score_device, state["booster"], Xd)
+                df["prob_default"] = await loop.run_in_executor(None, _score_device, state["booster"], Xd,
+                                                                getattr(state.get("engine"), "_lock", None))
             elif "remote" in state:
                 X = df.to_numpy(dtype=np.float32, na_value=np.nan)
                 df["prob_default"] = (await state["remote"].score_many(X, False))[0]

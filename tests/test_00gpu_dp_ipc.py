@@ -28,13 +28,13 @@ def test_ipc_data_parallel_processes_equal_single_process():
     _check_clean(torch.cuda.is_initialized())
     ref = dp_check.run(1, ROWS)[0]
     assert ref["ok"], ref
-    # the exchange fused into the split evaluation (default: the lead-decides evaluation + partition
-    # pass, k_eval_part mode 2, while a level's grid fits the rank's CUs, else k_eval) with 2, 3, 4 and 8
-    # ranks -- ipc_sum_cells<4> / <8> are what an 8-GPU node runs; the ranks share the device through
-    # disjoint CU masks (parallel/cumask.py) --, the fused k_eval alone (COBALT_EVAL_PART=0), and the
-    # separate exchange kernel (COBALT_IPC_FUSED=0: k_eval_part mode 1 over the all-reduced histograms)
-    for procs, env in ((2, None), (3, None), (4, None), (8, None), (2, {"COBALT_EVAL_PART": "0"}),
-                       (2, {"COBALT_IPC_FUSED": "0"})):
+    # the exchange fused into the split evaluation (default: k_eval + k_partition) with 2, 3 and 4 ranks
+    # -- ipc_sum_cells<4> --, the lead-decides evaluation + partition pass (k_eval_part mode 2,
+    # COBALT_DP_EVAL_PART=1), and the separate exchange kernel (COBALT_IPC_FUSED=0: k_eval_part mode 1
+    # over the all-reduced histograms). The ranks share the device through disjoint CU masks
+    # (parallel/cumask.py); 8 ranks: test_ipc_eight_ranks_share_one_gpu
+    for procs, env in ((2, None), (3, None), (4, None), (2, {"COBALT_DP_EVAL_PART": "1"}),
+                       (4, {"COBALT_DP_EVAL_PART": "1"}), (2, {"COBALT_IPC_FUSED": "0"})):
         got = dp_check.run(procs, ROWS, timeout_s=400, env=env)
         for g in got:
             assert g["ok"], (procs, env, g)

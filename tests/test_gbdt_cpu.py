@@ -265,3 +265,28 @@ def test_native_tree_conversion_equals_numpy():
                   "default_left", "base_weights", "loss_changes", "sum_hessian"):
             x, y = getattr(ta, k), getattr(tb, k)
             assert x.dtype == y.dtype and np.array_equal(x, y), k
+
+
+def test_pickle_writer_frames_like_cpython():
+    """The checkpoint encoder's framing is pickle._Framer's byte for byte, including a trailing frame
+    shorter than 4 bytes after an out-of-frame large payload (no FRAME header then)."""
+    import io
+    import pickle
+
+    from cobalt_smart_lender_ai_amd.dataio.safe_pickle import _Writer
+
+    for tail in range(0, 7):
+        ops = bytes([0x85 + (i % 3) for i in range(tail)])
+        w = _Writer()
+        w.op(b"\x8c\x01a")
+        w.large(b"B" + (70000).to_bytes(4, "little"), b"x" * 70000)
+        w.op(ops)
+        ours = w.getvalue()
+        buf = io.BytesIO()
+        f = pickle._Framer(buf.write)
+        f.start_framing()
+        f.write(b"\x8c\x01a")
+        f.write_large_bytes(b"B" + (70000).to_bytes(4, "little"), b"x" * 70000)
+        f.write(ops)
+        f.end_framing()
+        assert ours == buf.getvalue(), tail

@@ -235,7 +235,8 @@ def test_bulk_csv_device_parse_equals_pandas_path(reference_booster, monkeypatch
         monkeypatch.setattr(app_mod, "GPU_CSV_MIN_BYTES", 0)
         calls = []
         real = app_mod._score_device
-        monkeypatch.setattr(app_mod, "_score_device", lambda b, Xd: calls.append(Xd.shape) or real(b, Xd))
+        monkeypatch.setattr(app_mod, "_score_device",
+                            lambda b, Xd, lock=None: calls.append(Xd.shape) or real(b, Xd, lock))
         dev = c.post("/predict_bulk_csv", files=files)
     assert host.status_code == 200 and dev.status_code == 200, (host.text[:200], dev.text[:200])
     assert calls == [(n, len(DEPLOYED_FEATURES))]  # the device path ran
@@ -244,3 +245,43 @@ def test_bulk_csv_device_parse_equals_pandas_path(reference_booster, monkeypatch
     diff = [(i, k, hp[i][k], dp[i].get(k)) for i in range(n) for k in hp[i] if hp[i][k] != dp[i].get(k)]
     assert not diff, (len(diff), diff[:8])
     assert dev.json() == host.json()
+
+
+def test_concurrent_predict_and_repeated_bulk_device_requests(reference_booster, monkeypatch):
+    """Same-size device-parsed bulk uploads (the caching allocator hands them the same addresses) next
+    to concurrent /predict requests whose micro-batcher replays the engine's hipGraphs: every request
+    succeeds and every bulk answer is the same (advisor finding: the bulk scorer captured a graph on a
+    worker thread outside the engine lock; it is now serialised with the engine and never captures)."""
+    import concurrent.futures as cf
+    import io
+
+    import pandas as pd
+    from fastapi.testclient import TestClient
+
+    from cobalt_smart_lender_ai_amd.config import DEPLOYED_FEATURES, ServeConfig
+    from cobalt_smart_lender_ai_amd.serve import app as app_mod
+
+    n = 12_000
+    X = _rows(n, len(DEPLOYED_FEATURES), seed=5)
+    buf = io.StringIO()
+    pd.DataFrame(X.astype(np.float64), columns=DEPLOYED_FEATURES).to_csv(buf, index=False)
+    files = {"file": ("x.csv", buf.getvalue().encode(), "text/csv")}
+    monkeypatch.setattr(app_mod, "GPU_CSV_MIN_BYTES", 0)
+    row = {f: float(v) for f, v in zip(DEPLOYED_FEATURES, np.nan_to_num(X[0]))}
+    row["application_type_Joint App"] = row.pop("application_type_Joint App")
+    app = app_mod.create_app(ServeConfig(device="cuda:0", use_graphs=True), booster=reference_booster)
+    with TestClient(app) as c:
+        def bulk(_):
+            r = c.post("/predict_bulk_csv", files=files)
+            return r.status_code, [p["prob_default"] for p in r.json()["predictions"]] if r.status_code == 200 else r.text
+
+        def single(_):
+            return c.post("/predict", json=row).status_code, None
+
+        with cf.ThreadPoolExecutor(8) as ex:
+            futs = [ex.submit(bulk if k % 2 == 0 else single, k) for k in range(24)]
+            res = [f.result() for f in futs]
+    codes = [r[0] for r in res]
+    assert codes == [200] * len(codes), res[:3]
+    outs = [r[1] for k, r in enumerate(res) if k % 2 == 0]
+    assert all(o == outs[0] for o in outs)

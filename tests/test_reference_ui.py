@@ -7,7 +7,8 @@ that host to FastAPI's TestClient over ``serve.app.create_app`` (the reference m
 static decoder). ``streamlit`` and ``shap`` are not installed here, so recording stand-ins replace
 them: the UI's widget calls return their defaults, and ``shap.Explanation`` /
 ``shap.plots.waterfall`` record what the UI hands them (reference:
-src/streamlit_ui/cobalt_streamlit.py:10,85,102-110,140,159)."""
+src/streamlit_ui/cobalt_streamlit.py:10,85,102-110,140,159). Both tests run against the host engine and,
+under ``-m gpu``, against the hipGraph GPU engine.""" 
 import io
 import math
 import os
@@ -79,15 +80,19 @@ def _shap():
     return shap
 
 
-@pytest.fixture()
-def routed_api(reference_booster, monkeypatch):
+@pytest.fixture(params=["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def routed_api(request, reference_booster, monkeypatch):
+    """The API behind the UI: the host engine, and (``-m gpu``) the MI355X engine the north star names
+    -- hipGraph-captured predictor + TreeSHAP buckets behind the micro-batcher, device CSV parsing for
+    the bulk upload (ServeConfig(device="cuda", use_graphs=True))."""
     import requests
     from fastapi.testclient import TestClient
 
     from cobalt_smart_lender_ai_amd.config import ServeConfig
     from cobalt_smart_lender_ai_amd.serve.app import create_app
 
-    with TestClient(create_app(ServeConfig(device="cpu"), booster=reference_booster)) as client:
+    cfg = ServeConfig(device="cpu") if request.param == "cpu" else ServeConfig(device="cuda", use_graphs=True)
+    with TestClient(create_app(cfg, booster=reference_booster)) as client:
         sent = []
 
         def post(url, **kw):

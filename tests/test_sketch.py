@@ -213,3 +213,54 @@ def test_full_data_sketch_single_rank_is_exact_and_ranks_agree():
     assert torch.equal(c[2:], one.cuts[2:]) and torch.equal(nb[2:], one.nbins[2:])
     for f in (0, 1):
         assert _rank_error_ok(X, w, c, nb, f, 0.004)
+
+
+def _adversarial_frames(n, dev, seed=0):
+    """Feature columns that stress the bucketed exact sketch: continuous, heavy duplicates, rare
+    values the strided sample misses, low cardinality with a few unsampled extra values (the
+    'uncertain' distinct-count path), NaNs, -0.0 / +0.0, a constant and an all-NaN column, and a column
+    whose sampled rows hold a single value (one huge open bucket: the host fallback sort)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    cols = []
+    cols.append(torch.randn(n, generator=g) * 1000)
+    cols.append(torch.round(torch.randn(n, generator=g) * 3))                       # heavy duplicates
+    x = torch.randint(0, 40, (n,), generator=g).float()
+    rare = torch.rand(n, generator=g) < 5e-5
+    cols.append(torch.where(rare, 1000.0 + torch.arange(n).float(), x))              # rare unsampled values
+    x = torch.randint(0, 100, (n,), generator=g).float()
+    cols.append(torch.where(torch.arange(n) % 7919 == 3, 100.5 + (torch.arange(n) % 5).float(), x))  # uncertain
+    x = torch.randn(n, generator=g)
+    cols.append(torch.where(torch.rand(n, generator=g) < 0.3, torch.tensor(float("nan")), x))
+    x = torch.where(torch.rand(n, generator=g) < 0.5, torch.tensor(-0.0), torch.tensor(0.0))
+    cols.append(torch.where(torch.rand(n, generator=g) < 0.5, x, torch.randn(n, generator=g)))
+    cols.append(torch.full((n,), 3.25))
+    cols.append(torch.full((n,), float("nan")))
+    stride = sketch.sample_stride(n, 1 << 16)
+    cols.append(torch.where(torch.arange(n) % stride == 0, torch.tensor(0.0), 1.0 + torch.rand(n, generator=g)))
+    return torch.stack(cols, 1).to(dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("weighted", [False, True])
+def test_device_exact_cuts_equal_the_full_sort(weighted):
+    """The bucketed full-data sketch (csrc/sketch.hip) returns compute_cuts' cuts over EVERY row, bit
+    for bit: the LendingClub-shaped features at 2M rows and the adversarial columns at 600k rows, with
+    unit weights and with hessian-style weights (including zero-weight rows)."""
+    from cobalt_smart_lender_ai_amd.dataio import synth
+
+    dev = torch.device("cuda", 0)
+    X1, y1 = synth.make_lendingclub(2_000_000, seed=4, device=dev)
+    X2 = _adversarial_frames(600_000, dev)
+    for X, y in ((X1, y1), (X2, None)):
+        w = None
+        if weighted:
+            if y is not None:
+                w = torch.where(y == 1, 6.5, 1.0).to(dev)
+            else:
+                w = (torch.arange(X.shape[0], device=dev) % 11).float()  # zero weights on every 11th row
+        want_c, want_n = sketch.compute_cuts(X, 256, w)
+        got_c, got_n = sketch.device_exact_cuts(X, 256, w)
+        assert torch.equal(got_n, want_n), (got_n, want_n)
+        for f in range(X.shape[1]):
+            nb = int(want_n[f])
+            assert torch.equal(got_c[f, :nb].view(torch.int32), want_c[f, :nb].view(torch.int32)), f
