@@ -51,6 +51,11 @@ _SIGS: dict[str, tuple] = {
     "cobalt_gbdt_grow_sampled": (c_int, [c_void_p, c_int, c_void_p]),
     "cobalt_gbdt_set_rows": (c_int, [c_void_p, c_int64]),
     "cobalt_gbdt_error": (c_int, [c_void_p]),
+    "cobalt_gbdt_ox_init": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "cobalt_gbdt_ox_begin": (c_int, [c_void_p, c_int, c_void_p]),
+    "cobalt_gbdt_ox_page": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int, c_int, c_void_p]),
+    "cobalt_gbdt_ox_level": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "cobalt_gbdt_ox_end": (c_int, [c_void_p, c_int, c_void_p]),
     "cobalt_gbdt_set_fault": (c_int, [c_void_p, c_int]),
     "cobalt_gbdt_tree_ptr": (c_void_p, [c_void_p, c_int]),
     "cobalt_ooc_page": (c_int, [c_void_p, c_int, c_int64, c_int64, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,

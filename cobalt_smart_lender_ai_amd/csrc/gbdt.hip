@@ -210,7 +210,14 @@ struct GbdtDev {
   int32_t corrupt;    // fault injection (COBALT_FAULT_CORRUPT_RANK): perturb this tree's root totals
   unsigned* err_host;
   uint64_t* dec;      // [max_nodes] k_eval_part<mode 2>: a node's decision granule {tag, decision}
+  // k_eval_part work items of the level, laid out by the histogram pass's block (0, 0) (ep_plan):
+  // {node, begin, end} per item, the count in counters[1]; ep_chunk = the level's item size (0: the
+  // level has no fused pass), ep_zero = active nodes without local rows get an empty item (DP)
+  int4* ep_items;
+  int32_t ep_chunk, ep_zero;
+  int32_t ep_plan;    // 1: items from ep_plan (COBALT_EP_PLAN, default), 0: every block plans (block_plan)
 };
+
 
 // 32-bit hash of one finalised node decision (position, status, split feature / bin / default
 // direction, threshold or leaf value): summed over a tree's nodes into GbdtDev::dig.
@@ -747,6 +754,43 @@ __device__ void publish_level(const GbdtDev& d, int level, int total, bool keep_
   }
 }
 
+// Block (0, 0) of the histogram pass of level L > 0 also lays out the level's fused evaluation +
+// partition items (k_eval_part then loads its item -- one load -- instead of planning: the node-table
+// loads + wave scan + barrier were ~2.5 us at the head of every block). A node's row range is its
+// parent's partition split, as publish_level computes it; wave 0 of the block.
+__device__ void ep_plan(const GbdtDev& d, int level) {
+  if (wave_id() != 0) return;
+  const int lane = lane_id();
+  const int n_ent = 1 << level, first = n_ent - 1;
+  const int chunk = d.ep_chunk;
+  int carry = 0;
+  for (int base = 0; base < n_ent; base += kWave) {
+    const int e = base + lane;
+    int node = -1, start = 0, cnt = 0;
+    if (e < n_ent) {
+      const int n = first + e, q = (n - 1) >> 1;
+      const Node& par = d.nodes[q];
+      const int st = par.status, pstart = par.start, pcount = par.count;  // loaded together
+      const int lc = d.cursors[2 * q];
+      const bool left = (n & 1) == 1;
+      if (st == kSplit) {
+        node = n;
+        start = left ? pstart : pstart + lc;
+        cnt = left ? lc : pcount - lc;
+      }
+    }
+    const int nch = node < 0 ? 0 : (cnt > 0 ? (cnt + chunk - 1) / chunk : (d.ep_zero ? 1 : 0));
+    const int incl = wave_incl_scan(nch) + carry;
+    const int excl = incl - nch;
+    for (int k = 0; k < nch; ++k) {
+      const int b = start + k * chunk;
+      d.ep_items[excl + k] = make_int4(node, b, min(start + cnt, b + chunk), 0);
+    }
+    carry = readlane32(incl, kWave - 1);
+  }
+  if (lane == 0) d.counters[1] = carry;
+}
+
 // LDS histogram helpers shared by k_hist and k_grad_hist (32-byte record fast path).
 struct HistLanes {
   uint64_t fbits;                 // colsample mask of the tile's features
@@ -1162,7 +1206,10 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
   // barrier after the row loop publishes it to the flush
   flush_meta_store(fmeta, ft, s_fo, s_fs);
   stamp_.probe(1);
-  if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total, d.by_hess != 0);
+  if (item == 0 && blockIdx.y == 0) {
+    publish_level(d, level, pl.total, d.by_hess != 0);
+    if (level > 0 && d.ep_chunk > 0 && d.ep_plan) ep_plan(d, level);
+  }
   if (pl.node < 0) return;
   WorkItem w;
   w.node = pl.node;
@@ -2348,7 +2395,6 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   BlockStamp stamp_(d);
   __shared__ int32_t s_cnt[2][kPW];
   __shared__ int32_t s_base[2];
-  __shared__ int s_plan[5];
   __shared__ EvalOut s_out;
   __shared__ uint32_t s_dec;
   {  // zero the next level's reduce destination (hist_b of the other parity, or the next IPC send slot)
@@ -2361,11 +2407,25 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   if (kDP && blockIdx.x == 0) ipc_publish(d.ipcv[d.ipc_epoch & 1u].myflag, d.ipc_epoch);
   const int item = blockIdx.x;
   const int first = (1 << level) - 1;
-  const PlanOut pl = block_plan<kMode != 0>(1 << level, chunk, item, [&](int e) {
-    const Node& n = d.nodes[first + e];
-    const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
-    return (st != kNone && (kMode != 0 || cnt > 0)) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
-  }, s_plan);
+  // this block's item: the root's rows are fixed slices; deeper levels' items were laid out by the
+  // histogram pass (ep_plan) -- both loads in one round trip
+  PlanOut pl;
+  __shared__ int s_plan[5];
+  if (level == 0) {
+    const int n = (int)d.n, b = item * chunk;
+    const int items = max((n + chunk - 1) / chunk, kMode != 0 ? 1 : 0);
+    pl = PlanOut{item < items ? 0 : -1, 0, min(b, n), min(n, b + chunk), items};
+  } else if (!d.ep_plan) {
+    pl = block_plan<kMode != 0>(1 << level, chunk, item, [&](int e) {
+      const Node& n = d.nodes[first + e];
+      const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
+      return (st != kNone && (kMode != 0 || cnt > 0)) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
+    }, s_plan);
+  } else {
+    const int4 it = d.ep_items[item];
+    const int tot = d.counters[1];
+    pl = PlanOut{item < tot ? it.x : -1, 0, it.y, it.z, tot};
+  }
   if (pl.node < 0) return;
   const int node = pl.node;
   // the item's row ids and the node's range: independent of the split, in flight during the evaluation
@@ -2667,6 +2727,14 @@ struct GbdtCtx {
   int stamp_cap = 0;
   uint64_t* stamp_buf = nullptr;
   std::vector<const char*> stamp_names;
+  // exact external-memory mode (cobalt_gbdt_ox_*): per-row state of the streamed data set
+  int64_t ox_n = 0;
+  uint16_t* ox_pos = nullptr;   // [ox_n] the row's node (heap index) in the tree being grown
+  uint64_t* ox_gh = nullptr;    // [ox_n] packed quantised (g, h) of the tree being grown
+  int64_t* ox_slab = nullptr;   // [kOxSlab][pairs_max][slot_elems] per-block partial histograms
+  float* ox_margin = nullptr;
+  const float* ox_label = nullptr;
+  const float* ox_weight = nullptr;
 };
 
 // Next launch's stamp slot (0 when stamping is off or the tree is not sampled: d.stamps == nullptr).
@@ -2875,6 +2943,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.seed = cfg->seed;
   d.ablate = getenv("COBALT_HIST_ABLATE") ? atoi(getenv("COBALT_HIST_ABLATE")) : 0;
   d.pwide = env_part_wide();
+  d.ep_plan = getenv("COBALT_EP_PLAN") ? atoi(getenv("COBALT_EP_PLAN")) : 1;
   // write-through slabs always (10M rows: reduce gaps 14.2 -> 12.0 us per tree, fit 243.7 -> 243.2 ms); write-through
   // row ids below 4M rows only (1M: 240.2 -> 237.4 us per tree with both; at 10M the partition itself
   // slows 210 -> 228 us per tree for 10 us of shorter histogram gaps). COBALT_WT overrides.
@@ -2907,6 +2976,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cand, (size_t)c->pairs_max * 64 * sizeof(CandRec)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.dec, c->max_nodes * sizeof(uint64_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.ep_items, c->items_cap * sizeof(int4)))) return rc;
   CK(hipMemset(d.dec, 0, c->max_nodes * sizeof(uint64_t)));
   if (cfg->comm) {  // local histograms of every node of a level (positions 0 .. 2^(max_depth-1))
     for (int k = 0; k < 2; ++k)
@@ -3197,6 +3267,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     CK_LAUNCH();
     for (int level = 0; level < D; ++level) {
       const int parity = level & 1;
+      // this level's evaluation runs in the partition pass (k_eval_part), with items of ep_ch rows laid
+      // out by the level's histogram pass (ep_plan)
+      const int ep_ch = level + 1 < D ? ep_chunk(level) : 0;
+      const bool ep_level = ep_ch > 0;
+      d.ep_chunk = ep_ch;
+      d.ep_zero = ep_mode != 0 ? 1 : 0;
       const int slots = level == 0 ? 1 : (1 << (level - 1));
       int ub;  // upper bound on the level's histogram work items
       if (fuse_part && level > 0) {  // partition of level - 1 and this level's histogram in one pass
@@ -3216,9 +3292,6 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
                   stream, d, parity, t, level, chh);
       }
-      // this level's evaluation runs in the partition pass (k_eval_part), with items of ep_ch rows
-      const int ep_ch = level + 1 < D ? ep_chunk(level) : 0;
-      const bool ep_level = ep_ch > 0;
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
               dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap), level);
@@ -3320,6 +3393,247 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
 
 COBALT_API int cobalt_gbdt_grow(void* h, int t0, int n_trees, hipStream_t stream) {
   return grow_impl(static_cast<GbdtCtx*>(h), t0, n_trees, stream, false);
+}
+
+// ------------------------------------------------------------------------------------------
+// Exact external-memory training (histograms over page-resident chunks, the analog of
+// XGBoost's external-memory `hist` without sampling). The quantised pages stay in host DRAM (or HBM
+// under a budget); on the device every row keeps only its margin, label, weight, packed (g, h) and its
+// current node (2 B): ~22 B per row instead of the in-core ~72 B. A tree is grown level by level, and
+// every level streams every page once:
+//   * level -1 (k_ox_page, mode grad): the previous tree's leaf (found through the row's node) is added
+//     to its margin, g / h are computed and quantised exactly as the in-core root pass does (same
+//     dither key: per tree and GLOBAL row), every row moves to the root, the root histogram is built;
+//   * level L >= 0: a row of a node split at level L moves to its child (the split feature's bin from
+//     the page), and a row entering the child the evaluation chose to build (smaller hessian) adds its
+//     (g, h) to that child pair's histogram;
+//   * after each pass: the per-block partial histograms are reduced into the in-core trainer's level
+//     slots (k_ox_reduce) and the in-core split evaluation (k_eval) runs on them unchanged -- same
+//     node table, same subtraction trick, same finalisation.
+// Every histogram is an exact integer sum, so the trees are byte-identical to the in-core fit of the
+// same rows (tests/test_external.py). Histograms: each block privatises the pair slots of its group
+// (gridDim.y groups) in LDS as packed u64 cells -- flushed to its own int64 slab rows every 16384 rows
+// (the packed halves cannot carry within that) -- so the page data is read once per slot group.
+// ------------------------------------------------------------------------------------------
+constexpr int kOxSlab = 128;           // blocks per page pass (= slab rows per pair slot)
+constexpr int kOxFlushRows = 16384;    // rows per LDS flush (packed u64 bound, as the in-core blocks)
+constexpr size_t kOxLdsBudget = 150 * 1024;
+
+static int ox_group_slots(const GbdtDev& d) {
+  return std::max<int>(1, (int)(kOxLdsBudget / ((size_t)(d.ncells + 1) * sizeof(uint64_t))));
+}
+
+// mode: -1 = gradient pass (+ root histogram), L >= 0 = route level L + histogram of level L + 1.
+__global__ __launch_bounds__(1024) void k_ox_page(GbdtDev d, const uint8_t* __restrict__ page, int ps, int64_t n,
+                                                  int64_t r0, int mode, int tree, int apply, uint16_t* __restrict__ pos,
+                                                  uint64_t* __restrict__ gh, int64_t* __restrict__ slab,
+                                                  float* __restrict__ margin, const float* __restrict__ label,
+                                                  const float* __restrict__ weight, int gslots) {
+  extern __shared__ uint64_t s_h[];  // [gslots][ncells + 1] packed (g, h); cell ncells = the slot's totals
+  __shared__ uint32_t s_meta[256];
+  __shared__ float s_leaf[256];
+  __shared__ uint8_t s_build[256];
+  __shared__ int s_hoff[kMaxFeatTile + 1];
+  __shared__ int s_nb[kMaxFeatTile];  // bin count, 0 for a feature colsample masked out of this tree
+  const int F = d.F, nc = d.ncells, cells = nc + 1;
+  const int g0 = blockIdx.y * gslots;                                  // first slot of this block's group
+  const int nslots = mode < 0 ? 1 : (1 << mode);                       // pairs of level mode + 1
+  const int gs = min(gslots, nslots - g0);
+  if (gs <= 0) return;
+  const Node* tab = (mode < 0) ? d.prev_nodes : d.nodes;              // tree staged for this pass
+  for (int i = threadIdx.x; i < d.max_nodes && i < 256; i += blockDim.x) {
+    const Node nd = tab[i];
+    s_meta[i] = (uint32_t)(nd.feat & 0xFFFF) | ((uint32_t)(nd.bin & 0xFF) << 16) |
+                ((uint32_t)(nd.default_left & 1) << 24) | ((nd.status == kSplit ? 1u : 0u) << 25);
+    s_leaf[i] = nd.leaf_value;
+    s_build[i] = (uint8_t)(nd.build != 0);
+  }
+  for (int f = threadIdx.x; f <= F; f += blockDim.x) {
+    s_hoff[f] = d.hoff[f];
+    if (f < F) s_nb[f] = d.fmask[(int64_t)tree * F + f] ? d.nbins[f] : 0;
+  }
+  const uint64_t tree_key = tree_key_of(d.seed, tree);
+  const uint64_t dkey = splitmix64(tree_key ^ kDitherSalt);
+  const int first = mode < 0 ? 0 : (1 << mode) - 1;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t b0 = min(n, (int64_t)blockIdx.x * per), b1 = min(n, b0 + per);
+  int64_t* my = slab + (int64_t)blockIdx.x * d.slot_elems * (int64_t)(1 << (d.max_depth - 1));
+  for (int64_t c0 = b0; c0 < b1; c0 += kOxFlushRows) {
+    const int64_t c1 = min(b1, c0 + kOxFlushRows);
+    __syncthreads();  // (previous flush done with s_h; staged tables visible)
+    for (int i = threadIdx.x; i < gs * cells; i += blockDim.x) s_h[i] = 0ull;
+    __syncthreads();
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+      const int64_t r = r0 + i;
+      const uint8_t* row = page + i * ps;
+      int slot = -1;
+      uint64_t v = 0;
+      if (mode < 0) {  // gradients (+ the previous tree's leaf), every row builds the root
+        float mf = margin[r];
+        if (apply) {  // the previous tree's leaf: from the row's last routed node down (its last level
+                      // was evaluated but not routed), with the page's bins
+          int nd = pos[r];
+          uint32_t m = s_meta[nd];
+          while (m & (1u << 25)) {
+            const uint32_t b = row[m & 0xFFFF];
+            const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+            nd = 2 * nd + (left ? 1 : 2);
+            m = s_meta[nd];
+          }
+          mf += s_leaf[nd];
+          margin[r] = mf;
+        }
+        const double p = 1.0 / (1.0 + exp(-(double)mf));
+        const double y = (double)label[r], w = (double)weight[r];
+        double g = (p - y) * w;
+        double h = fmax(p * (1.0 - p), 1e-16) * w;
+        if (d.subsample < 1.0) {
+          const uint64_t hsh = splitmix64(tree_key ^ (uint64_t)(d.row_offset + r));
+          if (!(uniform01(hsh) < d.subsample)) { g = 0.0; h = 0.0; }
+        }
+        int64_t gq, hq;
+        quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + r, gq, hq);
+        v = ((uint64_t)(uint32_t)(int32_t)gq << 32) | (uint64_t)(uint32_t)hq;
+        gh[r] = v;
+        pos[r] = 0;
+        slot = 0;
+      } else {  // route a row of a split node of this level; it may build its child's pair histogram
+        const int nd = pos[r];
+        const uint32_t m = (nd >= first && nd < 2 * first + 1) ? s_meta[nd] : 0u;
+        if (m & (1u << 25)) {
+          const int f = m & 0xFFFF;
+          const uint32_t b = row[f];
+          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          const int ch = 2 * nd + (left ? 1 : 2);
+          pos[r] = (uint16_t)ch;
+          if (s_build[ch]) {
+            slot = nd - first;
+            v = gh[r];
+          }
+        }
+      }
+      const int ls = slot - g0;
+      if (slot >= 0 && ls >= 0 && ls < gs) {
+        unsigned long long* hs = reinterpret_cast<unsigned long long*>(s_h + (int64_t)ls * cells);
+        atomicAdd(hs + nc, (unsigned long long)v);  // the slot's (G, H)
+        for (int f = 0; f < F; ++f) {
+          const int b = row[f];
+          if (b < s_nb[f]) atomicAdd(hs + s_hoff[f] + b, (unsigned long long)v);
+        }
+      }
+    }
+    __syncthreads();
+    // flush: this block owns its slab rows (no atomics); only non-zero cells are written
+    for (int i = threadIdx.x; i < gs * cells; i += blockDim.x) {
+      const uint64_t pv = s_h[i];
+      if (!pv) continue;
+      const int ls = i / cells, c = i - ls * cells;
+      int64_t* dst = my + (int64_t)(g0 + ls) * d.slot_elems + 2 * c;
+      dst[0] += (int64_t)(int32_t)(uint32_t)(pv >> 32);
+      dst[1] += (int64_t)(uint32_t)pv;
+    }
+  }
+}
+
+// Level histograms: the kOxSlab per-block slab rows of each pair slot summed into hist_b[parity] (the
+// in-core evaluation's input, totals cell included), the slab zeroed behind the read.
+__global__ __launch_bounds__(256) void k_ox_reduce(GbdtDev d, int64_t* __restrict__ slab, int parity, int slots) {
+  const int s = blockIdx.x;
+  const int64_t e = ((int64_t)blockIdx.y * blockDim.x + threadIdx.x) * 2;
+  if (e >= d.slot_elems || s >= slots) return;
+  const int64_t rowstride = d.slot_elems * (int64_t)(1 << (d.max_depth - 1));
+  int64_t g = 0, h = 0;
+  for (int b = 0; b < kOxSlab; ++b) {
+    int64_t* p = slab + b * rowstride + (int64_t)s * d.slot_elems + e;
+    g += p[0];
+    h += p[1];
+    p[0] = 0;
+    p[1] = 0;
+  }
+  int64_t* o = d.hist_b[parity] + (int64_t)s * d.slot_elems + e;
+  o[0] = g;
+  o[1] = h;
+}
+
+COBALT_API int cobalt_gbdt_ox_init(void* h, int64_t n, float* margin, const float* label, const float* weight) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  if (c->d.F > kMaxFeatTile || c->max_nodes > 256 || c->d.F > 32) return -15;  // depth <= 7, <= 32 features
+  if (c->ox_pos) return -16;
+  c->ox_n = n;
+  int rc;
+  if ((rc = dev_alloc(c, (void**)&c->ox_pos, (size_t)std::max<int64_t>(n, 1) * sizeof(uint16_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&c->ox_gh, (size_t)std::max<int64_t>(n, 1) * sizeof(uint64_t)))) return rc;
+  const size_t sb = (size_t)kOxSlab * c->pairs_max * c->d.slot_elems * sizeof(int64_t);
+  if ((rc = dev_alloc(c, (void**)&c->ox_slab, sb))) return rc;
+  CK(hipMemset(c->ox_slab, 0, sb));
+  c->ox_margin = margin;
+  c->ox_label = label;
+  c->ox_weight = weight;
+  const size_t lds = (size_t)ox_group_slots(c->d) * (c->d.ncells + 1) * sizeof(uint64_t);
+  CK(hipFuncSetAttribute((const void*)k_ox_page, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return 0;
+}
+
+// Start tree t: node tables (the new one reset, the previous one kept for the margin update).
+COBALT_API int cobalt_gbdt_ox_begin(void* h, int t, hipStream_t stream) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  if (t != c->grown || t >= c->cfg.max_trees) return -11;
+  GbdtDev& d = c->d;
+  d.nodes = d.nodes_buf[t & 1];
+  d.prev_nodes = d.nodes_buf[(t + 1) & 1];
+  d.zero_red = nullptr;
+  d.stamps = nullptr;
+  hipLaunchKernelGGL(k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
+                     stream, d);
+  CK_LAUNCH();
+  return 0;
+}
+
+// One page of the current pass (mode -1 = gradients, L = route level L). Rows r0 .. r0 + n of the data
+// set, `ps` bytes per row (the F bins first).
+COBALT_API int cobalt_gbdt_ox_page(void* h, const uint8_t* page, int ps, int64_t n, int64_t r0, int mode, int t,
+                                   hipStream_t stream) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  const GbdtDev& d = c->d;
+  if (!c->ox_pos || r0 < 0 || r0 + n > c->ox_n || ps < d.F || mode >= d.max_depth - 1) return -3;
+  if (n <= 0) return 0;
+  const int gsl = ox_group_slots(d);
+  const int nslots = mode < 0 ? 1 : (1 << mode);
+  const dim3 grid(kOxSlab, ceil_div(nslots, gsl));
+  const int gs = std::min(gsl, nslots);
+  const size_t lds = (size_t)gs * (d.ncells + 1) * sizeof(uint64_t);
+  const int apply = (mode < 0 && t > c->fit_first) ? 1 : 0;
+  hipLaunchKernelGGL(k_ox_page, grid, dim3(1024), lds, stream, d, page, ps, n, r0, mode, t, apply, c->ox_pos, c->ox_gh,
+                     c->ox_slab, c->ox_margin, c->ox_label, c->ox_weight, gsl);
+  CK_LAUNCH();
+  return 0;
+}
+
+// After the pass that built level `level`'s histograms: reduce them and evaluate the level.
+COBALT_API int cobalt_gbdt_ox_level(void* h, int level, int t, hipStream_t stream) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  GbdtDev& d = c->d;
+  if (level < 0 || level >= d.max_depth) return -3;
+  const int parity = level & 1;
+  const int slots = level == 0 ? 1 : (1 << (level - 1));
+  hipLaunchKernelGGL(k_ox_reduce, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d, c->ox_slab,
+                     parity, slots);
+  CK_LAUNCH();
+  hipLaunchKernelGGL((k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F,
+                     c->eval_slots);
+  CK_LAUNCH();
+  return 0;
+}
+
+// Finish tree t: archive its node table.
+COBALT_API int cobalt_gbdt_ox_end(void* h, int t, hipStream_t stream) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  GbdtDev& d = c->d;
+  CK(hipMemcpyAsync(d.trees + (size_t)t * c->max_nodes, d.nodes_buf[t & 1], c->max_nodes * sizeof(Node),
+                    hipMemcpyDeviceToDevice, stream));
+  c->grown = t + 1;
+  c->applied = t;
+  return 0;
 }
 
 // External memory: grow tree t from the sample the last k_ooc_page passes wrote into the trainer's

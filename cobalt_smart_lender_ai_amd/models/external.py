@@ -131,6 +131,7 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
         params = GBDTParams.from_kwargs(**params)
     if not 0.0 < sample_rate <= 1.0:
         raise ValueError("sample_rate must be in (0, 1]")
+    exact = sample_rate >= 1.0  # every row every tree: level-wise page streaming (no sample)
     dev = _resolve_device(device, None)
     rep = report if report is not None else ExternalReport()
     t0 = time.perf_counter()
@@ -200,6 +201,22 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
                                   gscale=gscale, hscale=hscale)
     target = sample_rate * N
     cap = int(min(N, math.ceil(target * 1.25) + 4096))
+
+    if exact:
+        t0 = time.perf_counter()
+        nodes = _train_exact(pages, y, w, base_margin, F, dev, cuts, nbins, params, T, fmask, wmax)
+        rep.t_boost = time.perf_counter() - t0
+        rep.sample_rows = [N] * T
+        names = list(feature_names) if feature_names is not None else None
+        return Booster(trees=trees_from_heap_nodes(nodes, D), feature_names=names,
+                       feature_types=list(feature_types) if feature_types is not None else None,
+                       base_score=base_score, num_feature=F,
+                       train_params=dict(eta=float(params.learning_rate), gamma=float(params.gamma), max_depth=D,
+                                         min_child_weight=float(params.min_child_weight),
+                                         reg_lambda=float(params.reg_lambda), reg_alpha=float(params.reg_alpha),
+                                         subsample=float(params.subsample),
+                                         colsample_bytree=float(params.colsample_bytree),
+                                         max_bin=int(params.max_bin), scale_pos_weight=spw, seed=seed))
 
     t0 = time.perf_counter()
     runner = (_GpuPasses if dev.type == "cuda" else _HostPasses)(pages, y, w, base_margin, F, cap, gscale, hscale,
@@ -360,3 +377,86 @@ class _GpuPasses:
 
     def close(self) -> None:
         self.tr.close(park=False)
+
+
+def _train_exact(pages, y, w, base_margin, F, dev, cuts, nbins, params, T, fmask, wmax) -> np.ndarray:
+    """Every row every tree (``sample_rate=1``): the in-core fixed-point scales and dither, so the trees
+    equal the in-core fit's byte for byte. GPU: level-wise page streaming (``cobalt_gbdt_ox_*``, the
+    in-core split evaluation on histograms summed page by page; ~22 B per row on the device). CPU: the
+    host trainer on the concatenated pages (the oracle)."""
+    D = int(params.max_depth)
+    gscale, hscale = gbdt_host.quant_scales(wmax)
+    hp = gbdt_host.HostGbdtParams(max_depth=D, eta=float(params.learning_rate), reg_lambda=float(params.reg_lambda),
+                                  reg_alpha=float(params.reg_alpha), gamma=float(params.gamma),
+                                  min_child_weight=float(params.min_child_weight), subsample=float(params.subsample),
+                                  seed=int(params.random_state), gscale=gscale, hscale=hscale)
+    if dev.type != "cuda":
+        bins = np.concatenate([p for _, p in pages]) if pages else np.zeros((0, F), np.uint8)
+        bins = np.ascontiguousarray(bins[:, :F])
+        margin = np.full(len(bins), np.float32(base_margin), dtype=np.float32)
+        yn, wn = y.cpu().numpy(), w.cpu().numpy()
+        c_np, nb_np = cuts.cpu().numpy(), nbins.cpu().numpy()
+        recs = []
+        for t in range(T):
+            gq, hq = gbdt_host.gradients_host(margin, yn, wn, hp, t, 0)
+            recs.append(gbdt_host.grow_tree_host(bins, c_np, nb_np, gq, hq, margin, hp, fmask[t]))
+        return np.stack(recs) if recs else np.zeros((0, (1 << (D + 1)) - 1), NODE_DTYPE)
+    from .. import _native
+    from ..ops import gbdt_ops
+
+    lib, stream = _native.lib(), _native.stream_handle
+    N = len(y)
+    dummy = 4096
+    tr = gbdt_ops.GpuGbdtTrainer(n_rows=dummy, n_feat=F, max_depth=D, max_trees=T, eta=hp.eta, reg_lambda=hp.reg_lambda,
+                                 reg_alpha=hp.reg_alpha, gamma=hp.gamma, min_child_weight=hp.min_child_weight,
+                                 subsample=hp.subsample, gscale=gscale, hscale=hscale, base_margin=base_margin,
+                                 seed=hp.seed)
+    try:
+        fm = torch.as_tensor(fmask, device=dev).contiguous()
+        z = torch.zeros(dummy, device=dev)
+        tr.set_data(torch.zeros((dummy, gbdt_ops.row_stride(F)), dtype=torch.uint8, device=dev),
+                    torch.zeros((F, dummy), dtype=torch.uint8, device=dev), cuts.contiguous(),
+                    nbins.to(torch.int32).contiguous(), z, torch.ones(dummy, device=dev), z.clone(), fm)
+        margin = torch.full((N,), base_margin, dtype=torch.float32, device=dev)
+        yy, ww = y.to(dev, torch.float32).contiguous(), w.to(dev, torch.float32).contiguous()
+        _native.check(lib.cobalt_gbdt_ox_init(tr.h, N, margin.data_ptr(), yy.data_ptr(), ww.data_ptr()),
+                      "cobalt_gbdt_ox_init")
+        biggest = max((p.shape[0] for _, p in pages), default=1)
+        ps = pages[0][1].shape[1] if pages else page_stride(F)
+        stage = [torch.empty((biggest, ps), dtype=torch.uint8, device=dev) for _ in range(2)]
+        copy_stream = torch.cuda.Stream(dev)
+
+        def stream_pages(mode: int, t: int) -> None:
+            cur = torch.cuda.current_stream(dev)
+            done = [None, None]
+            for k, (r0, page) in enumerate(pages):
+                if page.is_cuda:
+                    ptr = page.data_ptr()
+                else:  # double-buffered H2D on the copy stream, overlapping the previous page's pass
+                    buf = stage[k & 1]
+                    with torch.cuda.stream(copy_stream):
+                        if done[k & 1] is not None:
+                            copy_stream.wait_event(done[k & 1])
+                        buf[: page.shape[0]].copy_(page, non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(copy_stream)
+                    cur.wait_event(ev)
+                    ptr = buf.data_ptr()
+                rc = lib.cobalt_gbdt_ox_page(tr.h, ptr, page.shape[1], page.shape[0], r0, mode, t, stream())
+                _native.check(rc, "cobalt_gbdt_ox_page")
+                if not page.is_cuda:
+                    e2 = torch.cuda.Event()
+                    e2.record(cur)
+                    done[k & 1] = e2
+
+        for t in range(T):
+            _native.check(lib.cobalt_gbdt_ox_begin(tr.h, t, stream()), "cobalt_gbdt_ox_begin")
+            stream_pages(-1, t)
+            _native.check(lib.cobalt_gbdt_ox_level(tr.h, 0, t, stream()), "cobalt_gbdt_ox_level")
+            for lv in range(D - 1):
+                stream_pages(lv, t)
+                _native.check(lib.cobalt_gbdt_ox_level(tr.h, lv + 1, t, stream()), "cobalt_gbdt_ox_level")
+            _native.check(lib.cobalt_gbdt_ox_end(tr.h, t, stream()), "cobalt_gbdt_ox_end")
+        return tr.fetch(0, T)
+    finally:
+        tr.close(park=False)

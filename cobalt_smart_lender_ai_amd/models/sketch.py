@@ -403,11 +403,21 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     Under data parallelism (``dist``) every rank passes its shard: the sample is global (strided by
     global row index), the bucket histograms are all-reduced and the candidates all-gathered, so all
     ranks compute the cuts of the full data. ``w_max`` scales the weights (default: the global max)."""
+    import os
+
     from .. import _native
 
     lib = _sk_lib()
     N, F = X.shape
     dev = X.device
+    timing = os.environ.get("COBALT_SK_TIMING") == "1"  # per-stage times (device-synchronised) to stderr
+    marks = []
+
+    def mark(name):
+        if timing:
+            torch.cuda.synchronize(dev)
+            marks.append((name, __import__("time").perf_counter()))
+    mark("start")
     world = dist.world if dist is not None else 1
     n_glob = n_rows_global if n_rows_global is not None else N
     NBND, NB, CAP = lib.cobalt_sk_bounds(), lib.cobalt_sk_buckets(), lib.cobalt_sk_sort_cap()
@@ -454,6 +464,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     else:
         m = torch.zeros(F, dtype=torch.int32, device=dev)
     bounds = bounds[:, :NBND].contiguous()
+    mark("bounds")
 
     # 2. bucket histograms (row counts; weight sums when weighted) + min / max valid value
     nblk = max(1, min(64, -(-N // 65536)))
@@ -487,6 +498,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
         vmax = t.to(dev)
     if w_h is None:
         w_h = cnt_h
+    mark("hist")
 
     # 3. targets: bucket of every rank j * W / maxb; equal buckets ARE their value
     C = torch.cumsum(w_h, 1)
@@ -523,6 +535,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     if nseg:
         glob_off[1:] = torch.cumsum(glob_sizes, 0)
     tot_loc = int(loc_off[-1])
+    mark("targets")
 
     # 4. candidates: the rows of the selected buckets, per segment
     cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)
@@ -536,6 +549,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
         cval, cw = _merge_candidates(dist, dev, cval[:tot_loc], None if cw is None else cw[:tot_loc], loc_sizes,
                                      glob_off)
 
+    mark("gather")
     # 5. select the open targets from their bucket's sorted candidates
     tf, tj = torch.nonzero(need_t, as_tuple=True)
     T = int(tf.numel())
@@ -565,6 +579,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
             out[t0:t1] = vs[i]
         q[tf, tj] = out
 
+    mark("select")
     # 6. the cut tables, as compute_cuts assembles them
     trash = torch.full((F, 257), FLT_MAX, dtype=torch.float32, device=dev)
     keep = inb & (q > vmin[:, None])
@@ -597,7 +612,15 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     cuts = torch.where(exact[:, None], cuts_ex[:, :256], cuts_q[:, :256]).contiguous()
     nbv = torch.where(exact, nb_ex, nbq)
     cuts.scatter_(1, (nbv - 1).clamp(min=0)[:, None], FLT_MAX)
-    return cuts + 0.0, nbv.to(torch.int32)
+    out = cuts + 0.0, nbv.to(torch.int32)
+    mark("assemble")
+    if timing:
+        import sys
+
+        print("[sketch] " + " ".join(f"{marks[i][0]}={1e3 * (marks[i][1] - marks[i - 1][1]):.3f}ms"
+                                     for i in range(1, len(marks))) + f" candidates={tot_loc} segments={nseg}",
+              file=sys.stderr)
+    return out
 
 
 def _merge_candidates(dist, dev, cval, cw, loc_sizes, glob_off):

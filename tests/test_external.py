@@ -49,12 +49,36 @@ def test_external_host_path_quality_matches_in_core():
     a_ref = roc_auc(yte, ref.predict_proba(Xte, device="cpu"))
     a_ext = roc_auc(yte, b.predict_proba(Xte, device="cpu"))
     assert abs(a_ref - a_ext) < 0.01, (a_ref, a_ext)
-    # a full-rate "sample" keeps every row with weight 1: the in-core trees (the hessian is quantised
-    # 4x coarser here, so leaf values agree to the quantisation step, splits exactly)
+    # sample_rate=1: exact streaming (every row every tree, the in-core fixed point): the in-core trees
     full = external.train_external(array_chunks(X, y, 9_000), PARAMS, device="cpu", sample_rate=1.0)
-    for a, b2 in zip(full.trees, ref.trees):
-        assert np.array_equal(a.split_indices, b2.split_indices) and np.array_equal(a.left_children, b2.left_children)
-    np.testing.assert_allclose(full.predict_margin(X, device="cpu"), ref.predict_margin(X, device="cpu"), atol=2e-3)
+    _same_trees(full, ref)
+
+
+def _same_trees(a, b):
+    assert a.num_trees == b.num_trees
+    for ta, tb in zip(a.trees, b.trees):
+        for k in ("left_children", "right_children", "split_indices", "split_conditions", "default_left",
+                  "base_weights", "loss_changes", "sum_hessian"):
+            assert np.array_equal(getattr(ta, k), getattr(tb, k)), k
+    assert a.base_score == b.base_score
+
+
+@pytest.mark.gpu
+def test_external_exact_streaming_gpu_equals_in_core():
+    """sample_rate=1 on the GPU: level-wise page streaming (csrc/gbdt.hip k_ox_page / k_ox_reduce + the
+    in-core k_eval), the trees of the in-core GPU fit byte for byte -- pages spilled to host DRAM, and
+    partly resident in HBM."""
+    import torch
+
+    X, y = _lc(90_000, 6)
+    params = {**PARAMS, "colsample_bytree": 0.8, "max_depth": 7, "n_estimators": 9}
+    ref = gbdt.train(torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda(), params, device="cuda")
+    src = array_chunks(X, y, 13_000)
+    ext = external.train_external(src, params, device="cuda", sample_rate=1.0)
+    _same_trees(ext, ref)
+    ps = external.page_stride(X.shape[1])
+    mixed = external.train_external(src, params, device="cuda", sample_rate=1.0, device_page_bytes=40_000 * ps)
+    _same_trees(mixed, ref)
 
 
 @pytest.mark.gpu
