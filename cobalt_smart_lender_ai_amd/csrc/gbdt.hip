@@ -215,7 +215,7 @@ struct GbdtDev {
   // level has no fused pass), ep_zero = active nodes without local rows get an empty item (DP)
   int4* ep_items;
   int32_t ep_chunk, ep_zero;
-  int32_t ep_plan;    // 1: items from ep_plan (COBALT_EP_PLAN, default), 0: every block plans (block_plan)
+  int32_t ep_plan;    // 1: items from ep_plan (COBALT_EP_PLAN=1), 0 (default): every block plans (block_plan)
 };
 
 
@@ -367,14 +367,22 @@ __device__ void init_tree_block(const GbdtDev& d) {
   }
 }
 
-// Stage tree `t` (heap-ordered node records) into LDS as {meta, leaf value}:
-// meta = feat | bin << 16 | default_left << 24 | is_split << 25.
+// Staged split word: feat | (bin + 1) << 16 (9 bits: the split bin j may be -1, a missing-only split
+// that sends every non-missing row right) | default_left << 25 | is_split << 26.
+constexpr uint32_t kMetaSplit = 1u << 26;
+__device__ __forceinline__ uint32_t node_meta(const Node& nd) {
+  return (uint32_t)(nd.feat & 0xFFFF) | ((uint32_t)((nd.bin + 1) & 0x1FF) << 16) |
+         ((uint32_t)(nd.default_left & 1) << 25) | (nd.status == kSplit ? kMetaSplit : 0u);
+}
+__device__ __forceinline__ bool meta_left(uint32_t m, uint32_t b) {
+  return (b == kMissingBin) ? ((m >> 25) & 1u) : (b < ((m >> 16) & 0x1FFu));
+}
+
+// Stage tree `t` (heap-ordered node records) into LDS as {meta, leaf value}.
 __device__ __forceinline__ void stage_tree(const GbdtDev& d, const Node* tr, uint32_t* s_meta, float* s_leaf) {
   for (int i = threadIdx.x; i < d.max_nodes; i += blockDim.x) {
     const Node nd = tr[i];
-    const uint32_t split = nd.status == kSplit ? 1u : 0u;
-    s_meta[i] = (uint32_t)(nd.feat & 0xFFFF) | ((uint32_t)(nd.bin & 0xFF) << 16) |
-                ((uint32_t)(nd.default_left & 1) << 24) | (split << 25);
+    s_meta[i] = node_meta(nd);
     s_leaf[i] = nd.leaf_value;
   }
 }
@@ -387,10 +395,10 @@ __device__ __forceinline__ float tree_leaf_T(const GbdtDev& d, int64_t i, const 
                                              const float* s_leaf) {
   int n = 0;
   uint32_t m = s_meta[0];
-  while (m & (1u << 25)) {
+  while (m & kMetaSplit) {
     const int f = m & 0xFFFF;
     const uint32_t b = d.binsT[(int64_t)f * d.ldt + i];
-    const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+    const bool left = meta_left(m, b);
     n = 2 * n + (left ? 1 : 2);
     m = s_meta[n];
   }
@@ -440,11 +448,11 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
         // walk the previous tree with the record held in registers
         int n = 0;
         uint32_t m = s_meta[0];
-        while (m & (1u << 25)) {
+        while (m & kMetaSplit) {
           const int f = m & 0xFFFF, q = f >> 2;
           const uint32_t word = q == 0 ? ra.x : q == 1 ? ra.y : q == 2 ? ra.z : q == 3 ? ra.w : q == 4 ? rb.x : rb.y;
           const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
-          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          const bool left = meta_left(m, b);
           n = 2 * n + (left ? 1 : 2);
           m = s_meta[n];
         }
@@ -545,8 +553,7 @@ __global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ pa
   if (prev != nullptr)
     for (int i = threadIdx.x; i < max_nodes; i += blockDim.x) {
       const Node nd = prev[i];
-      s_meta[i] = (uint32_t)(nd.feat & 0xFFFF) | ((uint32_t)(nd.bin & 0xFF) << 16) |
-                  ((uint32_t)(nd.default_left & 1) << 24) | ((nd.status == kSplit ? 1u : 0u) << 25);
+      s_meta[i] = node_meta(nd);
       s_leaf[i] = nd.leaf_value;
     }
   __syncthreads();
@@ -577,11 +584,11 @@ __global__ __launch_bounds__(256) void k_ooc_page(const uint8_t* __restrict__ pa
       if (prev != nullptr) {
         int nx = 0;
         uint32_t m = s_meta[0];
-        while (m & (1u << 25)) {
+        while (m & kMetaSplit) {
           const int f = m & 0xFFFF, q = f >> 2;
           const uint32_t word = q == 0 ? ra.x : q == 1 ? ra.y : q == 2 ? ra.z : q == 3 ? ra.w : q == 4 ? rb.x : rb.y;
           const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
-          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          const bool left = meta_left(m, b);
           nx = 2 * nx + (left ? 1 : 2);
           m = s_meta[nx];
         }
@@ -1036,12 +1043,12 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       if (apply_tree >= 0 && d.ablate != 22) {  // walk the previous tree with the record held in registers
         int nidx = 0;
         uint32_t m = s_meta[0];
-        while (m & (1u << 25)) {
+        while (m & kMetaSplit) {
           const int f = m & 0xFFFF, q = f >> 2;
           const uint32_t word = q == 0 ? ra[u].x : q == 1 ? ra[u].y : q == 2 ? ra[u].z : q == 3 ? ra[u].w
                               : q == 4 ? rb[u].x : rb[u].y;
           const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
-          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          const bool left = meta_left(m, b);
           nidx = 2 * nidx + (left ? 1 : 2);
           m = s_meta[nidx];
         }
@@ -1355,14 +1362,6 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
   BlockStamp stamp_(d);
   // fused partition path: block (0, 0) publishes the level's node ranges from the finished claims
   if (publish > 0 && blockIdx.x == 0 && blockIdx.y == 0) publish_level(d, publish, -1, true);
-  // replica check (data parallel): the previous tree's digest goes into the cell after the root slot
-  // (all-reduced with it); this tree's accumulator restarts (no eval of this tree has run yet)
-  if (level == 0 && d.dig && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    int64_t* const red = d.hist_red ? d.hist_red : d.hist_b[parity];
-    red[d.slot_elems] = d.dig_check ? d.dig[d.dig_slot ^ 1] : 0;
-    red[d.slot_elems + 1] = 0;
-    d.dig[d.dig_slot] = 0;
-  }
   const int i0 = blockIdx.x * kRedItems;
   const int ncell = d.ncells;
   const int cell = blockIdx.y * blockDim.x + threadIdx.x;
@@ -1400,6 +1399,15 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
   }
   const int n_items = d.counters[0];
   stamp_.probe(1);
+  // replica check (data parallel): the previous tree's digest goes into the cell after the root slot
+  // (all-reduced with it); this tree's accumulator restarts (no eval of this tree has run yet). After
+  // the loads above are issued: at the kernel's head its branch delayed them (+0.4 us per launch).
+  if (level == 0 && d.dig && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    int64_t* const red = d.hist_red ? d.hist_red : d.hist_b[parity];
+    red[d.slot_elems] = d.dig_check ? d.dig[d.dig_slot ^ 1] : 0;
+    red[d.slot_elems + 1] = 0;
+    d.dig[d.dig_slot] = 0;
+  }
   if (i0 >= n_items) return;
   const int cnt = min(n_items - i0, kRedItems);
 #pragma unroll
@@ -2943,7 +2951,9 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.seed = cfg->seed;
   d.ablate = getenv("COBALT_HIST_ABLATE") ? atoi(getenv("COBALT_HIST_ABLATE")) : 0;
   d.pwide = env_part_wide();
-  d.ep_plan = getenv("COBALT_EP_PLAN") ? atoi(getenv("COBALT_EP_PLAN")) : 1;
+  // one planner block in k_hist + the item list in memory measured slower than every k_eval_part block
+  // planning for itself (same box, 1M rows: 78.1 vs 73.9 ms per fit; 1.25M: 80.8 vs 78.0; 10M: 229.6 vs 229.3)
+  d.ep_plan = getenv("COBALT_EP_PLAN") ? atoi(getenv("COBALT_EP_PLAN")) : 0;
   // write-through slabs always (10M rows: reduce gaps 14.2 -> 12.0 us per tree, fit 243.7 -> 243.2 ms); write-through
   // row ids below 4M rows only (1M: 240.2 -> 237.4 us per tree with both; at 10M the partition itself
   // slows 210 -> 228 us per tree for 10 us of shorter histogram gaps). COBALT_WT overrides.
@@ -3443,8 +3453,7 @@ __global__ __launch_bounds__(1024) void k_ox_page(GbdtDev d, const uint8_t* __re
   const Node* tab = (mode < 0) ? d.prev_nodes : d.nodes;              // tree staged for this pass
   for (int i = threadIdx.x; i < d.max_nodes && i < 256; i += blockDim.x) {
     const Node nd = tab[i];
-    s_meta[i] = (uint32_t)(nd.feat & 0xFFFF) | ((uint32_t)(nd.bin & 0xFF) << 16) |
-                ((uint32_t)(nd.default_left & 1) << 24) | ((nd.status == kSplit ? 1u : 0u) << 25);
+    s_meta[i] = node_meta(nd);
     s_leaf[i] = nd.leaf_value;
     s_build[i] = (uint8_t)(nd.build != 0);
   }
@@ -3474,9 +3483,9 @@ __global__ __launch_bounds__(1024) void k_ox_page(GbdtDev d, const uint8_t* __re
                       // was evaluated but not routed), with the page's bins
           int nd = pos[r];
           uint32_t m = s_meta[nd];
-          while (m & (1u << 25)) {
-            const uint32_t b = row[m & 0xFFFF];
-            const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
+          while (m & kMetaSplit) {
+            const uint32_t b = row[m & 0xFFFFu];
+            const bool left = meta_left(m, b);
             nd = 2 * nd + (left ? 1 : 2);
             m = s_meta[nd];
           }
@@ -3498,18 +3507,26 @@ __global__ __launch_bounds__(1024) void k_ox_page(GbdtDev d, const uint8_t* __re
         pos[r] = 0;
         slot = 0;
       } else {  // route a row of a split node of this level; it may build its child's pair histogram
-        const int nd = pos[r];
-        const uint32_t m = (nd >= first && nd < 2 * first + 1) ? s_meta[nd] : 0u;
-        if (m & (1u << 25)) {
-          const int f = m & 0xFFFF;
-          const uint32_t b = row[f];
-          const bool left = (b == kMissingBin) ? ((m >> 24) & 1u) : (b <= ((m >> 16) & 0xFFu));
-          const int ch = 2 * nd + (left ? 1 : 2);
-          pos[r] = (uint16_t)ch;
-          if (s_build[ch]) {
-            slot = nd - first;
-            v = gh[r];
+        // (with several slot groups the y = 0 blocks store the routed position; another group's block
+        // can read the row before or after that store, so a position already on level mode + 1 counts
+        // as routed from its parent)
+        int nd = pos[r];
+        int ch = -1;
+        if (nd >= 2 * first + 1) {
+          ch = nd;
+          nd = (nd - 1) >> 1;
+        } else if (nd >= first) {
+          const uint32_t m = s_meta[nd];
+          if (m & kMetaSplit) {
+            const uint32_t b = row[m & 0xFFFFu];
+            const bool left = meta_left(m, b);
+            ch = 2 * nd + (left ? 1 : 2);
+            if (blockIdx.y == 0) pos[r] = (uint16_t)ch;
           }
+        }
+        if (ch >= 0 && s_build[ch]) {
+          slot = nd - first;
+          v = gh[r];
         }
       }
       const int ls = slot - g0;

@@ -425,10 +425,12 @@ def _train_exact(pages, y, w, base_margin, F, dev, cuts, nbins, params, T, fmask
         ps = pages[0][1].shape[1] if pages else page_stride(F)
         stage = [torch.empty((biggest, ps), dtype=torch.uint8, device=dev) for _ in range(2)]
         copy_stream = torch.cuda.Stream(dev)
+        # last pass reading each staging buffer: kept ACROSS passes (the next pass's first uploads
+        # overwrite the buffers the previous pass's last pages are still being read from)
+        done = [None, None]
 
         def stream_pages(mode: int, t: int) -> None:
             cur = torch.cuda.current_stream(dev)
-            done = [None, None]
             for k, (r0, page) in enumerate(pages):
                 if page.is_cuda:
                     ptr = page.data_ptr()

@@ -210,7 +210,8 @@ class GpuGbdtTrainer:
     def replica_error(self) -> int:
         """Data-parallel replica check (csrc/gbdt.hip GbdtDev::dig): 0 = healthy, 2 = this rank's trees
         diverged from its peers' (detected at level 0 of the tree after the divergent one)."""
-        return int(self.lib.cobalt_gbdt_error(self.h)) if self.h else 0
+        fn = getattr(self.lib, "cobalt_gbdt_error", None)  # absent from pre-check libraries (A/B runs)
+        return int(fn(self.h)) if (self.h and fn is not None) else 0
 
     def set_fault(self, tree: int) -> None:
         """Fault injection (tests): perturb tree ``tree``'s root totals on this rank only."""

@@ -4,8 +4,8 @@
 set -o pipefail
 S=scripts/gpu_step.sh
 REF=$PWD/abref/libcobalt_hip_ref.so
-bash $S r4e_ext_tests 600 python -u -m pytest tests/test_external.py -x -v -m gpu --timeout 500 --timeout-method thread || exit $?
-grep -q " failed" gpurun_out/r4e_ext_tests.log && { echo "external tests failed"; exit 1; }
+bash $S r4e_oxdbg 300 python -u scripts/ox_debug.py || exit $?
+bash $S r4e_ext_tests 600 python -u -m pytest tests/test_external.py -v -m gpu --timeout 500 --timeout-method thread || exit $?
 COBALT_SK_TIMING=1 bash $S r4e_sketch 200 python -u scripts/sketch_exact_probe.py --reps 3 || exit $?
 for rep in 1 2; do
   for rows in 1000000 1250000 10000000; do
