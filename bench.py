@@ -44,8 +44,9 @@ def main() -> None:
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--profile-fit", action="store_true", help="print per-phase timings to stderr")
-    ap.add_argument("--sketch-rows", type=int, default=1 << 18,
-                    help="rows of the quantile-sketch sample; 0 = every row (full-data sketch)")
+    ap.add_argument("--sketch-rows", type=int, default=0,
+                    help="rows of the quantile-sketch sample; 0 (default) = every row, the exact device sketch "
+                         "(XGBoost hist's all-row semantics; csrc/sketch.hip)")
     a = ap.parse_args()
 
     from cobalt_smart_lender_ai_amd.dataio import synth

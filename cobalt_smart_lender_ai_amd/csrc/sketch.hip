@@ -71,16 +71,45 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_hist(const float* __restrict_
   const int64_t r0 = (int64_t)blockIdx.x * per, r1 = min(n, r0 + per);
   const float* col = X + (int64_t)f * ldx;
   float mn = INFINITY, mx = -INFINITY;
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-    const float v = canon(col[r]);
-    if (v != v) continue;  // NaN: the missing bin, no weight
-    mn = fminf(mn, v);
-    mx = fmaxf(mx, v);
-    const int b = sk_bucket(s_u, m, v);
-    atomicAdd(&s_c[b], 1u);
-    if (kW) {
-      const int32_t wi = w[r];
-      if (wi) atomicAdd(&s_w[b], (unsigned long long)wi);
+  const int lane = lane_id();
+  // every lane runs every iteration (whole-wave ballots / sums below)
+  for (int64_t base = r0; base < r1; base += blockDim.x) {
+    const int64_t r = base + threadIdx.x;
+    const float v = r < r1 ? canon(col[r]) : __int_as_float(0x7fc00000);
+    int b = -1;
+    int64_t wi = 0;
+    if (v == v) {  // NaN: the missing bin, no weight
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+      b = sk_bucket(s_u, m, v);
+      wi = kW ? (int64_t)w[r] : 1;
+    }
+    // Low-cardinality features put most lanes of a wave on one or two buckets: 64 same-address LDS
+    // atomics serialise. Two leader rounds add the wave's most common buckets once (popcount /
+    // wave sum), the remaining lanes add their own.
+#pragma unroll
+    for (int round = 0; round < 2; ++round) {
+      const uint64_t act = __ballot(b >= 0);
+      if (!act) break;
+      const int lead = __builtin_ctzll(act);
+      const int bl = __builtin_amdgcn_readlane(b, lead);
+      const bool mine = b == bl;
+      const uint64_t same = __ballot(mine);
+      if (__popcll(same) < 8) break;  // a spread wave: per-lane atomics are cheaper than the sums
+      if (kW) {
+        const int64_t ws = wave_sum(mine ? wi : (int64_t)0);
+        if (lane == lead) {
+          atomicAdd(&s_c[bl], (uint32_t)__popcll(same));
+          if (ws) atomicAdd(&s_w[bl], (unsigned long long)ws);
+        }
+      } else if (lane == lead) {
+        atomicAdd(&s_c[bl], (uint32_t)__popcll(same));
+      }
+      if (mine) b = -1;
+    }
+    if (b >= 0) {
+      atomicAdd(&s_c[b], 1u);
+      if (kW && wi) atomicAdd(&s_w[b], (unsigned long long)wi);
     }
   }
   mn = wave_min(mn);
@@ -106,25 +135,27 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_hist(const float* __restrict_
   }
 }
 
-// Pass 2. slot [F][kSkBuckets]: the bucket's segment index (-1 = not selected); seg_off [nseg + 1]
-// (exclusive), cursor [nseg] (zeroed). Writes candidate values (and int32 weights) into their
-// bucket's segment. Per block: count per selected bucket in LDS, reserve one range per bucket with
-// a global atomic, then a second walk over the rows writes through LDS cursors.
+// Pass 2. slot [F][kSkBuckets]: the bucket's segment index (-1 = not selected); blk_off [gridDim.x][nseg]:
+// where this block's rows of each segment start (the exclusive prefix over the blocks of pass 1's
+// per-block bucket counts, plus the segment's offset -- the same row partition as k_sk_hist, so one
+// walk over the rows suffices). Writes candidate values (and int32 weights) into their segments
+// through LDS cursors.
 template <bool kW>
 __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restrict__ X, int64_t n, int64_t ldx,
                                                          const int32_t* __restrict__ w, const float* __restrict__ bounds,
                                                          const int32_t* __restrict__ nbound,
-                                                         const int32_t* __restrict__ slot, const int64_t* __restrict__ seg_off,
-                                                         unsigned long long* __restrict__ cursor, float* __restrict__ cval,
-                                                         int32_t* __restrict__ cw) {
+                                                         const int32_t* __restrict__ slot, const int64_t* __restrict__ blk_off,
+                                                         int nseg, float* __restrict__ cval, int32_t* __restrict__ cw) {
   __shared__ float s_u[kSkMaxBounds];
   __shared__ int32_t s_slot[kSkBuckets];
-  __shared__ uint32_t s_cnt[kSkBuckets];  // per bucket: rows of this block, then the write cursor
+  __shared__ uint32_t s_cur[kSkBuckets];  // per selected bucket: this block's write cursor
   const int f = blockIdx.y;
   sk_load_bounds(s_u, bounds, f);
+  const int64_t* bo = blk_off + (int64_t)blockIdx.x * nseg;
   for (int i = threadIdx.x; i < kSkBuckets; i += blockDim.x) {
-    s_slot[i] = slot[(int64_t)f * kSkBuckets + i];
-    s_cnt[i] = 0u;
+    const int sg = slot[(int64_t)f * kSkBuckets + i];
+    s_slot[i] = sg;
+    s_cur[i] = sg >= 0 ? (uint32_t)bo[sg] : 0u;
   }
   const int m = nbound[f];
   __syncthreads();
@@ -135,26 +166,31 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
     const float v = canon(col[r]);
     if (v != v) continue;
     const int b = sk_bucket(s_u, m, v);
-    if (s_slot[b] >= 0) atomicAdd(&s_cnt[b], 1u);
-  }
-  __syncthreads();
-  // reserve this block's range in every selected bucket it touches; s_cnt becomes the write cursor
-  for (int b = threadIdx.x; b < kSkBuckets; b += blockDim.x) {
-    const uint32_t c = s_cnt[b];
-    if (c) {
-      const int sg = s_slot[b];
-      s_cnt[b] = (uint32_t)(seg_off[sg] + (int64_t)atomicAdd(cursor + sg, (unsigned long long)c));
-    }
-  }
-  __syncthreads();
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-    const float v = canon(col[r]);
-    if (v != v) continue;
-    const int b = sk_bucket(s_u, m, v);
     if (s_slot[b] < 0) continue;
-    const uint32_t pos = atomicAdd(&s_cnt[b], 1u);
+    const uint32_t pos = atomicAdd(&s_cur[b], 1u);
     cval[pos] = v;
     if (kW) cw[pos] = w[r];
+  }
+}
+
+// Row-major X [n][F] -> feature-major XT [F][n] (F <= 32): a tile of 256 rows is read as one
+// contiguous run into LDS (rows padded to F + 1 words: conflict-free column reads), then written as
+// F runs of 256 values.
+constexpr int kTrRows = 256;
+__global__ __launch_bounds__(256) void k_sk_transpose(const float* __restrict__ X, int64_t n, int F,
+                                                      float* __restrict__ XT) {
+  __shared__ float s_t[kTrRows * 33];
+  const int64_t r0 = (int64_t)blockIdx.x * kTrRows;
+  const int rows = (int)min((int64_t)kTrRows, n - r0);
+  const float* src = X + r0 * F;
+  for (int j = threadIdx.x; j < rows * F; j += blockDim.x) {
+    const int i = j / F, f = j - i * F;
+    s_t[i * (F + 1) + f] = src[j];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < kTrRows * F; j += blockDim.x) {
+    const int f = j / kTrRows, i = j - f * kTrRows;
+    if (i < rows) XT[(int64_t)f * n + r0 + i] = s_t[i * (F + 1) + f];
   }
 }
 
@@ -178,13 +214,16 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_select(const float* __restric
                                                          const int64_t* __restrict__ seg_off,
                                                          const int32_t* __restrict__ tgt_off,
                                                          const int64_t* __restrict__ prefix, const int64_t* __restrict__ thr,
-                                                         const int64_t* __restrict__ maxb, float* __restrict__ out) {
+                                                         const int64_t* __restrict__ maxb, float* __restrict__ out,
+                                                         const uint8_t* __restrict__ want, float* __restrict__ dval,
+                                                         int32_t* __restrict__ ndist) {
   extern __shared__ uint32_t s_dyn[];
   const int s = blockIdx.x;
   const int64_t o0 = seg_off[s], o1 = seg_off[s + 1];
   const int len = (int)(o1 - o0);
   const int t0 = tgt_off[s], t1 = tgt_off[s + 1];
-  if (len <= 0 || len > kSkSortCap || t0 >= t1) return;
+  const bool wd = want != nullptr && want[s];
+  if (len <= 0 || len > kSkSortCap || (t0 >= t1 && !wd)) return;
   int P = 1;
   while (P < len) P <<= 1;
   uint32_t* key = s_dyn;                                   // [P]
@@ -236,6 +275,100 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_select(const float* __restric
     }
     out[t] = fval(key[lo]);
   }
+  if (!wd) return;
+  // distinct values of the segment (a feature whose every value may get its own bin): the sorted run's
+  // first occurrences, compacted by an inclusive scan of the flags
+  __syncthreads();
+  for (int i = threadIdx.x; i < P; i += blockDim.x) cum[i] = (i < len && (i == 0 || key[i] != key[i - 1])) ? 1 : 0;
+  __syncthreads();
+  for (int d = 1; d < P; d <<= 1) {
+    int64_t add[kSkSortCap / kSkThreads];
+    int c = 0;
+    for (int i = threadIdx.x; i < P; i += blockDim.x, ++c) add[c] = i >= d ? cum[i - d] : 0;
+    __syncthreads();
+    c = 0;
+    for (int i = threadIdx.x; i < P; i += blockDim.x, ++c) cum[i] += add[c];
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < len; i += blockDim.x)
+    if (i == 0 || key[i] != key[i - 1]) dval[o0 + cum[i] - 1] = fval(key[i]);
+  if (threadIdx.x == 0) ndist[s] = (int32_t)cum[len - 1];
+}
+
+// Exact-bin features (one bin per distinct value when a feature has <= maxb of them), one block per
+// feature: the distinct values in bucket order are the sample values whose equal bucket has rows and,
+// for a feature with rows in open buckets (every such bucket is a selected segment then), the
+// segments' distinct values from k_sk_select. nd[f] = the distinct count (-1: not decidable here, the
+// segment was too large for the LDS sort); cut i - 1 = distinct value i (i >= 1) when nd <= maxb.
+__global__ __launch_bounds__(1024) void k_sk_exact(const int64_t* __restrict__ cnt, const float* __restrict__ bounds,
+                                                   const int32_t* __restrict__ slot, const int64_t* __restrict__ seg_off,
+                                                   const int32_t* __restrict__ ndist, const float* __restrict__ dval,
+                                                   const int64_t* __restrict__ maxb, float* __restrict__ cuts_ex,
+                                                   int64_t* __restrict__ nd) {
+  constexpr int kPer = (kSkBuckets + 1023) / 1024;  // buckets per thread (8)
+  __shared__ int64_t s_tot[1024 / kWave];
+  __shared__ int s_bad;
+  const int f = blockIdx.x, t = threadIdx.x;
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  const int64_t* c = cnt + (int64_t)f * kSkBuckets;
+  const int32_t* sl = slot + (int64_t)f * kSkBuckets;
+  int k0 = t * kPer;
+  int64_t cntd[kPer];
+  int64_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int b = k0 + q;
+    int64_t v = 0;
+    if (b < kSkBuckets && c[b] > 0) {
+      if (b & 1) {
+        v = 1;
+      } else {
+        const int sg = sl[b];
+        if (sg >= 0) {
+          v = ndist[sg];
+          if (v < 0) atomicOr(&s_bad, 1);
+        } else {
+          atomicOr(&s_bad, 1);  // rows in an open bucket that is not a segment: not an exact feature
+        }
+      }
+    }
+    cntd[q] = v < 0 ? 0 : v;
+    mine += cntd[q];
+  }
+  // exclusive block scan of the per-thread totals
+  int64_t incl = mine;
+  const int lane = lane_id(), wv = wave_id();
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int64_t u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == kWave - 1) s_tot[wv] = incl;
+  __syncthreads();
+  int64_t base = 0, total = 0;
+  for (int i = 0; i < 1024 / kWave; ++i) {
+    if (i < wv) base += s_tot[i];
+    total += s_tot[i];
+  }
+  int64_t r = base + incl - mine;
+  const bool bad = s_bad != 0;
+  const bool fits = !bad && total <= maxb[f];
+  if (t == 0) nd[f] = bad ? -1 : total;
+  if (!fits) return;
+  float* row = cuts_ex + (int64_t)f * 257;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int b = k0 + q;
+    if (cntd[q] == 0) continue;
+    if (b & 1) {
+      if (r >= 1 && r - 1 < 256) row[r - 1] = bounds[(int64_t)f * kSkMaxBounds + (b >> 1)];
+    } else {
+      const int64_t o = seg_off[sl[b]];
+      for (int64_t j = 0; j < cntd[q]; ++j)
+        if (r + j >= 1 && r + j - 1 < 256) row[r + j - 1] = dval[o + j];
+    }
+    r += cntd[q];
+  }
 }
 
 }  // namespace
@@ -256,23 +389,40 @@ COBALT_API int cobalt_sk_hist(const float* X, int64_t n, int64_t ldx, int F, con
 }
 
 COBALT_API int cobalt_sk_gather(const float* X, int64_t n, int64_t ldx, int F, const int32_t* w, const float* bounds,
-                                const int32_t* nbound, const int32_t* slot, const int64_t* seg_off, void* cursor,
+                                const int32_t* nbound, const int32_t* slot, const int64_t* blk_off, int nseg,
                                 float* cval, int32_t* cw, int nblk, hipStream_t stream) {
-  if (F <= 0 || nblk <= 0) return -3;
+  if (F <= 0 || nblk <= 0 || nseg <= 0) return -3;
   const dim3 grid(nblk, F);
   if (w)
     hipLaunchKernelGGL(k_sk_gather<true>, grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, slot,
-                       seg_off, static_cast<unsigned long long*>(cursor), cval, cw);
+                       blk_off, nseg, cval, cw);
   else
     hipLaunchKernelGGL(k_sk_gather<false>, grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, slot,
-                       seg_off, static_cast<unsigned long long*>(cursor), cval, cw);
+                       blk_off, nseg, cval, cw);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_sk_transpose(const float* X, int64_t n, int F, float* XT, hipStream_t stream) {
+  if (F <= 0 || F > 32 || n <= 0) return -3;
+  hipLaunchKernelGGL(k_sk_transpose, dim3((unsigned)((n + kTrRows - 1) / kTrRows)), dim3(256), 0, stream, X, n, F, XT);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_sk_exact(int F, const int64_t* cnt, const float* bounds, const int32_t* slot, const int64_t* seg_off,
+                               const int32_t* ndist, const float* dval, const int64_t* maxb, float* cuts_ex, int64_t* nd,
+                               hipStream_t stream) {
+  if (F <= 0) return -3;
+  hipLaunchKernelGGL(k_sk_exact, dim3(F), dim3(1024), 0, stream, cnt, bounds, slot, seg_off, ndist, dval, maxb, cuts_ex,
+                     nd);
   CK_LAUNCH();
   return 0;
 }
 
 COBALT_API int cobalt_sk_select(const float* cval, const int32_t* cw, const int64_t* seg_off, int nseg,
                                 const int32_t* tgt_off, const int64_t* prefix, const int64_t* thr, const int64_t* maxb,
-                                float* out, hipStream_t stream) {
+                                float* out, const uint8_t* want, float* dval, int32_t* ndist, hipStream_t stream) {
   if (nseg <= 0) return 0;
   const size_t lds = (size_t)kSkSortCap * (sizeof(uint32_t) + sizeof(int64_t));
   static bool attr = false;
@@ -283,10 +433,10 @@ COBALT_API int cobalt_sk_select(const float* cval, const int32_t* cw, const int6
   }
   if (cw)
     hipLaunchKernelGGL(k_sk_select<true>, dim3(nseg), dim3(kSkThreads), lds, stream, cval, cw, seg_off, tgt_off, prefix,
-                       thr, maxb, out);
+                       thr, maxb, out, want, dval, ndist);
   else
     hipLaunchKernelGGL(k_sk_select<false>, dim3(nseg), dim3(kSkThreads), lds, stream, cval, cw, seg_off, tgt_off,
-                       prefix, thr, maxb, out);
+                       prefix, thr, maxb, out, want, dval, ndist);
   CK_LAUNCH();
   return 0;
 }

@@ -377,9 +377,13 @@ def _sk_lib():
         lib.cobalt_sk_hist.restype = I
         lib.cobalt_sk_hist.argtypes = [V, I64, I64, I, V, V, V, I, V, V, V, V]
         lib.cobalt_sk_gather.restype = I
-        lib.cobalt_sk_gather.argtypes = [V, I64, I64, I, V, V, V, V, V, V, V, V, I, V]
+        lib.cobalt_sk_gather.argtypes = [V, I64, I64, I, V, V, V, V, V, I, V, V, I, V]
         lib.cobalt_sk_select.restype = I
-        lib.cobalt_sk_select.argtypes = [V, V, V, I, V, V, V, V, V, V]
+        lib.cobalt_sk_select.argtypes = [V, V, V, I, V, V, V, V, V, V, V, V, V]
+        lib.cobalt_sk_transpose.restype = I
+        lib.cobalt_sk_transpose.argtypes = [V, I64, I, V, V]
+        lib.cobalt_sk_exact.restype = I
+        lib.cobalt_sk_exact.argtypes = [I, V, V, V, V, V, V, V, V, V, V]
         for name in ("cobalt_sk_bounds", "cobalt_sk_buckets", "cobalt_sk_sort_cap"):
             getattr(lib, name).restype = I
             getattr(lib, name).argtypes = []
@@ -430,7 +434,12 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
             dist.allreduce(t, "max")
             has_missing = t.to(dev) > 0
     maxb = feature_max_bins(max_bin, has_missing.to(dev))                            # [F] int64
-    XT = X.t().contiguous()                                                          # [F, N]
+    if X.is_contiguous() and 0 < F <= 32 and N:                                      # [F, N]
+        XT = torch.empty((F, N), dtype=torch.float32, device=dev)
+        _native.check(lib.cobalt_sk_transpose(X.data_ptr(), N, F, XT.data_ptr(), stream), "cobalt_sk_transpose")
+    else:
+        XT = X.t().contiguous()
+    mark("transpose")
     wq = None
     if weights is not None:
         wd = weights.to(device=dev, dtype=torch.float64).reshape(-1)
@@ -448,6 +457,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     if world > 1:
         samp = dist.allgather_rows(samp)
     sv = torch.sort((samp.t() + 0.0).contiguous(), dim=1).values                     # [F, S], NaN last
+    mark("sort")
     S = sv.shape[1]
     K = NBND - 1
     cnt = (~torch.isnan(sv)).sum(1)
@@ -525,6 +535,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     sel_f = sel.reshape(-1)
     seg_of = torch.cumsum(sel_f.to(torch.int64), 0) - 1
     slot = torch.where(sel_f, seg_of, -1).to(torch.int32).contiguous()
+    seg_feat = torch.nonzero(sel_f).reshape(-1) // NB                                  # feature of every segment
     loc_sizes = cnt_loc.reshape(-1)[sel_f]                                             # this rank's rows per segment
     glob_sizes = cnt_h.reshape(-1)[sel_f]
     nseg = int(loc_sizes.numel())
@@ -541,9 +552,12 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)
     cw = torch.empty(max(tot_loc, 1), dtype=torch.int32, device=dev) if wq is not None else None
     if nseg and N:
-        cursor = torch.zeros(nseg, dtype=torch.int64, device=dev)
+        # where each hist block's rows of each segment start: pass 1's per-block counts, prefix-summed
+        # over the blocks (the gather walks the same row partition)
+        per_blk = cnt_slab.reshape(nblk, -1)[:, sel_f].to(torch.int64)                 # [nblk, nseg]
+        blk_off = (torch.cumsum(per_blk, 0) - per_blk + loc_off[:-1][None, :]).contiguous()
         rc = lib.cobalt_sk_gather(XT.data_ptr(), N, N, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), slot.data_ptr(),
-                                  loc_off.data_ptr(), cursor.data_ptr(), cval.data_ptr(), _ptr(cw), nblk, stream)
+                                  blk_off.data_ptr(), nseg, cval.data_ptr(), _ptr(cw), nblk, stream)
         _native.check(rc, "cobalt_sk_gather")
     if world > 1 and nseg:  # every rank's candidates, re-packed segment by segment
         cval, cw = _merge_candidates(dist, dev, cval[:tot_loc], None if cw is None else cw[:tot_loc], loc_sizes,
@@ -553,17 +567,23 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     # 5. select the open targets from their bucket's sorted candidates
     tf, tj = torch.nonzero(need_t, as_tuple=True)
     T = int(tf.numel())
-    if T:
+    # segments of the features that may be exact (one bin per distinct value): their distinct values
+    want = uncertain[seg_feat].to(torch.uint8).contiguous() if nseg else None
+    ndist = torch.full((max(nseg, 1),), -1, dtype=torch.int32, device=dev)
+    dval = torch.empty_like(cval)
+    if T or (nseg and bool(uncertain.any())):
         tb = b[tf, tj]
         tseg = slot.reshape(F, NB)[tf, tb].to(torch.int64)
         tgt_off = torch.zeros(nseg + 1, dtype=torch.int32, device=dev)
-        tgt_off[1:] = torch.cumsum(torch.bincount(tseg, minlength=nseg), 0).to(torch.int32)
+        if T:
+            tgt_off[1:] = torch.cumsum(torch.bincount(tseg, minlength=nseg), 0).to(torch.int32)
         prefix = torch.where(tb > 0, C[tf, (tb - 1).clamp(min=0)], torch.zeros_like(tb)).contiguous()
         tthr = thr[tf, tj].contiguous()
         tmaxb = maxb[tf].contiguous()
         out = torch.empty(T, dtype=torch.float32, device=dev)
         rc = lib.cobalt_sk_select(cval.data_ptr(), _ptr(cw), glob_off.data_ptr(), nseg, tgt_off.data_ptr(),
-                                  prefix.data_ptr(), tthr.data_ptr(), tmaxb.data_ptr(), out.data_ptr(), stream)
+                                  prefix.data_ptr(), tthr.data_ptr(), tmaxb.data_ptr(), out.data_ptr(), _ptr(want),
+                                  dval.data_ptr(), ndist.data_ptr(), stream)
         _native.check(rc, "cobalt_sk_select")
         big = torch.nonzero(glob_sizes > CAP).reshape(-1).tolist()  # rare: segments beyond the LDS sort
         for s in big:
@@ -577,7 +597,8 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
             key = ((prefix[t0:t1, None] + cum[None, :]) * tmaxb[t0:t1, None]).contiguous()
             i = torch.searchsorted(key, tthr[t0:t1, None].contiguous(), right=True)[:, 0].clamp(max=o1 - o0 - 1)
             out[t0:t1] = vs[i]
-        q[tf, tj] = out
+        if T:
+            q[tf, tj] = out
 
     mark("select")
     # 6. the cut tables, as compute_cuts assembles them
@@ -589,15 +610,17 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     nbq = keep.sum(1) + 1
     # exact path: one bin per distinct value (the sample's values that occur, + for the uncertain
     # features the distinct values of their open buckets)
-    eqnz = nz[:, 1::2][:, :NBND]
-    nd = E.clone()
-    dv_rank = torch.cumsum(eqnz.to(torch.int64), 1) - 1
-    ex_ok = eqnz & (dv_rank >= 1)
-    cuts_ex = trash.clone().scatter_(1, torch.where(ex_ok, (dv_rank - 1).clamp(max=256), 256), bounds)
-    exact = exact_known.clone()
-    for f in torch.nonzero(uncertain).reshape(-1).tolist():
+    cuts_ex = trash.clone()
+    nd = torch.empty(F, dtype=torch.int64, device=dev)
+    _native.check(lib.cobalt_sk_exact(F, cnt_h.contiguous().data_ptr(), bounds.data_ptr(), slot.data_ptr(),
+                                      glob_off.data_ptr(), ndist.data_ptr(), dval.data_ptr(), maxb.contiguous().data_ptr(),
+                                      cuts_ex.data_ptr(), nd.data_ptr(), stream), "cobalt_sk_exact")
+    exact = (nd >= 0) & (nd <= maxb)
+    # rare: an exact-candidate feature with a segment beyond the LDS sort -- its distinct values on the host
+    for f in torch.nonzero(uncertain & (nd < 0)).reshape(-1).tolist():
+        eqnz = nz[f, 1::2][:NBND]
         segs = torch.nonzero(slot.reshape(F, NB)[f] >= 0).reshape(-1)
-        parts = [bounds[f][eqnz[f]]]
+        parts = [bounds[f][eqnz]]
         for bb in segs.tolist():
             s = int(slot.reshape(F, NB)[f, bb])
             parts.append(cval[int(glob_off[s]):int(glob_off[s + 1])])

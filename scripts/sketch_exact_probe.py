@@ -17,6 +17,7 @@ from cobalt_smart_lender_ai_amd.models import sketch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=10_000_000)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--only-exact", action="store_true", help="profiling: the exact path only")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 X, y = synth.make_lendingclub(a.rows, seed=0, device=dev)
@@ -36,6 +37,9 @@ def timed(fn):
 
 
 (ce, ne), t_exact = timed(lambda: sketch.device_exact_cuts(X, 256, None, hm))
+if a.only_exact:
+    print(json.dumps({"rows": a.rows, "exact_ms": round(t_exact, 3)}), flush=True)
+    sys.exit(0)
 (cs, ns), t_sort = timed(lambda: sketch.compute_cuts(X, 256, None, hm))
 samp = sketch.local_sample(X, 0, sketch.sample_stride(a.rows, 1 << 18))
 (cq, nq), t_samp = timed(lambda: sketch.compute_cuts(samp, 256, None, hm))

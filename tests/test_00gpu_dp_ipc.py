@@ -45,6 +45,22 @@ def test_ipc_data_parallel_processes_equal_single_process():
 
 
 @pytest.mark.timeout(600)
+def test_full_data_sketch_across_processes_equals_single_process():
+    """The bench's default all-row sketch under data parallelism (models/sketch.py device_exact_cuts
+    with ``dist``: global strided sample, all-reduced bucket histograms, all-gathered candidates):
+    3 processes sharing the GPU grow the 1-process model byte for byte."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, sketch_rows=None)
+    ref = dp_check.run(1, ROWS, params)[0]
+    assert ref["ok"], ref
+    for g in dp_check.run(3, ROWS, params, timeout_s=400):
+        assert g["ok"], g
+        assert g["model_sha256"] == ref["model_sha256"], g["rank"]
+
+
+@pytest.mark.timeout(600)
 def test_ipc_replica_divergence_fails_every_rank():
     """Fault injection: rank 1 grows a different tree 1 (its root totals perturbed after the exchange,
     as a stale peer read would). The in-flight digest check (csrc/gbdt.hip GbdtDev::dig) sees it at
