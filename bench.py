@@ -95,14 +95,17 @@ def main() -> None:
         diverged = False
         try:
             fit()
-        except gbdt.ReplicaDivergence as e:  # raised on every rank of the same fit (in-flight digest check)
-            print(f"[bench] rank {rank}: {e}", file=sys.stderr)
-            diverged = True
+        except (gbdt.ReplicaDivergence, pdist.CollectiveTimeout) as e:
+            # divergence: raised on every rank of the same fit (in-flight digest check); a timed-out
+            # in-kernel exchange: every rank's deadline passes (the peers stop publishing), the group
+            # is aborted and the GPU work drained
+            if world == 1 or ctx.transport != "ipc":
+                raise
+            print(f"[bench] rank {rank}: {type(e).__name__}: {e}", file=sys.stderr)
+            diverged = type(e).__name__
         # every rank agrees before acting on it, so the ranks' collectives stay in step
         if world > 1 and ctx.allreduce_scalar(1.0 if diverged else 0.0, "max", dev) > 0.5:
-            if ctx.transport != "ipc":
-                raise RuntimeError("data-parallel replicas diverged on the RCCL transport")
-            fallback = "ipc replicas diverged in warm-up; RCCL"
+            fallback = f"ipc exchange failed in warm-up ({diverged or 'on a peer'}); RCCL"
             pdist.switch_transport(ctx, "rccl")
     ctx.barrier()
     if dev.type == "cuda":

@@ -12,6 +12,13 @@ CUs, like a small GPU of its own. The mask interleaves the ranks (CU ``rank + k 
 has CUs in every XCD whichever way the runtime maps mask bits onto the XCDs. ``COBALT_CU_BUDGET``
 tells the trainer's launch heuristics how many CUs it has (e.g. the fused evaluation + partition
 pass only runs while its whole grid is resident).
+
+Measured on one MI355X (scripts/dp8_diag.py, profiles/round4/dp_shared_gpu.txt): with masks, 2-5
+processes run at full speed (5 ranks: 0.14 s per 1-tree fit, the 1-process model); from 6 processes
+on, the masked fits deadlock at the in-kernel exchange (every rank times out). Unmasked, 6 and 8
+processes are time-sliced by the GPU's queue scheduler -- slow (8 ranks: 12.6 s for one tree) but
+every rank finishes with the 1-process model, byte for byte. So the masks are the default only up
+to 5 ranks per device. None of this applies to the production layout (one process per GPU).
 """
 from __future__ import annotations
 
@@ -58,6 +65,13 @@ def shared_device_stream(rank: int, world: int, device: torch.device) -> torch.c
     return torch.cuda.ExternalStream(h.value, device=device)
 
 
+MAX_MASKED_RANKS = 5
+
+
 def want_shared_mask(world: int) -> bool:
-    """Partition the CUs when ranks share a device (``COBALT_SHARED_CU_MASK``, default on for >= 2)."""
-    return world > 1 and os.environ.get("COBALT_SHARED_CU_MASK", "1") != "0"
+    """Partition the CUs when ranks share a device (``COBALT_SHARED_CU_MASK``: default on for 2 to
+    ``MAX_MASKED_RANKS`` ranks, off above -- see the module notes; "1" forces it on, "0" off)."""
+    env = os.environ.get("COBALT_SHARED_CU_MASK")
+    if env is not None:
+        return world > 1 and env != "0"
+    return 1 < world <= MAX_MASKED_RANKS

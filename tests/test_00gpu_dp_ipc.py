@@ -8,6 +8,8 @@ abort instead of hanging.
 The file sorts before every other GPU test: the ranks (and the 1-rank reference) run in spawned
 processes, and this pytest process never initialises HIP (spawning from an initialised process is
 refused on the pool)."""
+import os
+
 import pytest
 import torch
 
@@ -42,6 +44,28 @@ def test_ipc_data_parallel_processes_equal_single_process():
             # one exchange per level per tree, plus the connect self-test's four (each slot twice)
             assert g["ipc_epochs"] == 4 + 7 * ref["trees"]
             assert g["model_sha256"] == ref["model_sha256"], (procs, env, g["rank"])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.skipif(os.environ.get("COBALT_TEST_DP8") != "1", reason="opt-in (COBALT_TEST_DP8=1): time-sliced, "
+                    "12.6 s to several minutes per run on a shared GPU")
+def test_ipc_eight_ranks_share_one_gpu():
+    """8 processes on one GPU -- the rank count of an 8-GPU node, so the fused exchange sums 8 ranks'
+    cells (ipc_sum_cells<8>). Unmasked (parallel/cumask.py: masks deadlock from 6 sharing ranks), the
+    GPU time-slices the ranks' queues: slow, one tree, but byte-identical to 1 process. Its recorded
+    runs: profiles/round4/dp_shared_gpu.txt (scripts/dp8_diag.py)."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=1)
+    ref = dp_check.run(1, 240_000, params)[0]
+    assert ref["ok"], ref
+    got = dp_check.run(8, 240_000, params, timeout_s=300, env={"COBALT_IPC_TIMEOUT_S": "200"})
+    for g in got:
+        assert g["ok"], g
+        assert g["transport"] == "ipc" and g.get("cu_budget") is None
+        assert g["ipc_epochs"] == 4 + 7
+        assert g["model_sha256"] == ref["model_sha256"], g["rank"]
 
 
 @pytest.mark.timeout(600)
