@@ -1588,6 +1588,20 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
 // NR ranks' send slots into LDS. Every cell's NR loads are in flight together
 // (one remote round trip per block instead of one per rank); `store`: the sums also go to hist_b
 // (the built child's global histogram, for the next level's subtraction), `store_tot`: the totals too.
+// The peers' cells are read with system-scope loads (they bypass this XCD's L2, so the wait needs no
+// L2-invalidating acquire; kIpcAcquireFence = true restores the fence + plain loads for A/B).
+#ifndef COBALT_IPC_ACQUIRE_FENCE
+#define COBALT_IPC_ACQUIRE_FENCE 0
+#endif
+constexpr bool kIpcAcquireFence = COBALT_IPC_ACQUIRE_FENCE != 0;
+__device__ __forceinline__ longlong2 ipc_load_cell(const char* p) {
+  if (kIpcAcquireFence) return *reinterpret_cast<const longlong2*>(p);
+  longlong2 v;
+  v.x = __hip_atomic_load(reinterpret_cast<const long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  v.y = __hip_atomic_load(reinterpret_cast<const long long*>(p) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return v;
+}
+
 template <int NR>
 __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m, int ncells,
                                               longlong2* s_cells, longlong2* hbw, bool store, bool store_tot) {
@@ -1598,7 +1612,7 @@ __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pa
     const int cell = i < mt ? cb + i : ncells + (i - mt);
     longlong2 t[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) t[r] = *reinterpret_cast<const longlong2*>(sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2));
+    for (int r = 0; r < NR; ++r) t[r] = ipc_load_cell(sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2));
     longlong2 acc = t[0];
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
@@ -1625,7 +1639,7 @@ __device__ __forceinline__ void ipc_sum_cells_wide(int nr, const IpcFusedView* i
       longlong2 t[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r)
-        t[r] = 8 * g + r < nr ? *reinterpret_cast<const longlong2*>(iv->slot[8 * g + r] + off) : make_longlong2(0, 0);
+        t[r] = 8 * g + r < nr ? ipc_load_cell(iv->slot[8 * g + r] + off) : make_longlong2(0, 0);
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         acc.x += t[r].x;
@@ -1796,7 +1810,8 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
     const int ce = kGroups ? d.hoff[fend] : d.ncells;
     // (k_eval_part publishes before its plan: its block 0 is not always an evaluating block)
     if (!kMerged && blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
-    if (!ipc_wait(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout)) return false;
+    if (!ipc_wait<kIpcAcquireFence>(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout))
+      return false;
     // the global root totals are stored at level 0 (k_eval_finish reads them)
     // (+ the replica-digest cell at level 0)
     ipc_sum_cells_n(__builtin_amdgcn_readfirstlane(iv->n), iv, (int64_t)pair * SE * (int64_t)sizeof(int64_t), cb,

@@ -15,8 +15,11 @@ __device__ __forceinline__ void ipc_publish(unsigned* myflag, unsigned epoch) {
 // Block-wide: wait until every rank has published `epoch`. Wave 0 polls all ranks' flag words at
 // once (lane r <- rank r: one round trip per poll) with s_sleep back-off and an s_memrealtime
 // deadline; on timeout the sticky word and the pinned host error word are set (the host watchdog
-// aborts) and every later wait of this rank fails at once. A system-scope acquire follows, so the
-// block reads the peers' slots fresh. Returns the same value in every thread; call from all threads.
+// aborts) and every later wait of this rank fails at once. kAcquire: a system-scope acquire follows,
+// so the block's plain loads read the peers' slots fresh -- on a multi-XCD gfx950 that invalidates the
+// whole L2 of the XCD; callers that read the slots with system-scope (cache-bypassing) loads instead
+// pass false. Returns the same value in every thread; call from all threads.
+template <bool kAcquire = true>
 __device__ __forceinline__ bool ipc_wait(const unsigned* const* ftab, int n, int me, unsigned* myflag,
                                          unsigned epoch, unsigned* err_host, unsigned long long timeout) {
   __shared__ int ipc_ok;
@@ -40,7 +43,7 @@ __device__ __forceinline__ bool ipc_wait(const unsigned* const* ftab, int n, int
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    if (kAcquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
     if (lane == 0) ipc_ok = good;
   }
   __syncthreads();
