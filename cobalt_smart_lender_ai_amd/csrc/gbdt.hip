@@ -3244,7 +3244,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   auto ep_chunk = [&](int level) -> int {
     if (!eval_part) return 0;
     const int cus = device_cu_count();
-    for (int ch = chunk_part(d); ch <= 8192; ch *= 2)
+    // the smallest item (in 1024-row steps from 4096) whose grid is one block per CU: a level whose
+    // 4096-row items overflow the CUs takes 5120 / 6144 / 7168 instead of jumping to 8192 (fewer rows
+    // per block; 1.25M rows: 6144 at every level instead of 8192)
+    static const int fine = getenv("COBALT_EP_FINE") ? atoi(getenv("COBALT_EP_FINE")) : 1;  // 0: doubling (A/B)
+    for (int ch = (fine && part_wide(d)) ? std::min(4096, chunk_part(d)) : chunk_part(d); ch <= 8192;
+         ch = fine ? ch + 1024 : ch * 2)
       if (ceil_div(d.n, ch) + (1 << level) <= cus) return ch;
     return (env_ep == 2 && ep_mode == 0) ? 8192 : 0;
   };
