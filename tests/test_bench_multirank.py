@@ -39,22 +39,23 @@ def _json_lines(out: str) -> list[dict]:
 
 
 @pytest.mark.timeout(600)
-def test_bench_two_gloo_ranks_one_json_line_and_same_auc():
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_gloo_ranks_one_json_line_and_same_auc(world):
     one = subprocess.run([sys.executable, "bench.py", "--gpus", "1", *ARGS], cwd=ROOT, env=_env(),
                          capture_output=True, text=True, timeout=300)
     assert one.returncode == 0, one.stderr[-3000:]
     (ref,) = _json_lines(one.stdout)
-    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
-                          *ARGS], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=400)
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus",
+                          str(world), *ARGS], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=400)
     assert two.returncode == 0, two.stderr[-3000:]
     lines = _json_lines(two.stdout)
     assert len(lines) == 1, two.stdout
     got = lines[0]
-    assert got["n_gpus"] == 2
+    assert got["n_gpus"] == world
     assert got["rows_global"] == 200000
-    assert got["config"]["rows_per_gpu"] == 100000
-    assert got["config"]["parallelism"] == "dp2"
+    assert got["config"]["rows_per_gpu"] == 200000 // world
+    assert got["config"]["parallelism"] == f"dp{world}"
     assert got["config"]["global_batch"] == 200000
     assert got["metric"] == ref["metric"]
     assert got["value"] > 0 and got["ms_per_step"] > 0
