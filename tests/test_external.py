@@ -64,14 +64,16 @@ def _same_trees(a, b):
 
 
 @pytest.mark.gpu
-def test_external_exact_streaming_gpu_equals_in_core():
+@pytest.mark.parametrize("colsample", [0.8, 1.0])
+def test_external_exact_streaming_gpu_equals_in_core(colsample):
     """sample_rate=1 on the GPU: level-wise page streaming (csrc/gbdt.hip k_ox_page / k_ox_reduce + the
     in-core k_eval), the trees of the in-core GPU fit byte for byte -- pages spilled to host DRAM, and
-    partly resident in HBM."""
+    partly resident in HBM. Depth 7: the deep levels' pair slots span several LDS groups (the routing
+    of a row is shared by the groups' blocks), and every tree level re-streams the staging buffers."""
     import torch
 
     X, y = _lc(90_000, 6)
-    params = {**PARAMS, "colsample_bytree": 0.8, "max_depth": 7, "n_estimators": 9}
+    params = {**PARAMS, "colsample_bytree": colsample, "max_depth": 7, "n_estimators": 9}
     ref = gbdt.train(torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda(), params, device="cuda")
     src = array_chunks(X, y, 13_000)
     ext = external.train_external(src, params, device="cuda", sample_rate=1.0)
