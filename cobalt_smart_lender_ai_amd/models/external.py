@@ -9,7 +9,7 @@ row) and spills the rows' bins to pinned host pages in a compact format (the F b
 bytes: 20 B per row for the deployed features instead of the 32-byte record, since the per-tree page
 stream is bound by the H2D copy):
 
-1. ``stream_cuts`` -- the in-core quantile sketch over the stream (same cuts as an in-core fit);
+1. ``stream_cuts`` -- the in-core quantile sketch over the stream (the cuts of an in-core fit with the same ``sketch_rows``; the default samples 2^18 rows);
 2. every chunk is binned on the GPU and its row records are copied to a pinned host page;
 3. per tree, every page streams back through ``k_ooc_page`` (double-buffered H2D on a copy stream):
    the previous tree is applied to the margins, g/h are computed, and a minimal-variance sample

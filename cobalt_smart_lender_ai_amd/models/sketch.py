@@ -651,14 +651,14 @@ def _merge_candidates(dist, dev, cval, cw, loc_sizes, glob_off):
     holds rank 0's values of s, then rank 1's, ... (the order inside a segment does not matter)."""
     world = dist.world
     cd = dist._coll_device(dev)
-    sizes = loc_sizes.to(cd)
-    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-    import torch.distributed as tdist
-
-    tdist.all_gather(all_sizes, sizes)
-    all_sizes = torch.stack(all_sizes).to(dev)                                         # [world, nseg]
+    nseg = loc_sizes.numel()
+    # (through the context: also the in-process loopback group of the tests; every rank has nseg)
+    all_sizes = dist.allgather_rows(loc_sizes.to(cd).reshape(-1, 1), pad_value=0).to(dev).reshape(world, nseg)
     vals = dist.allgather_rows(cval.reshape(-1, 1).to(cd), pad_value=0.0).to(dev)[:, 0]
-    per = vals.numel() // world
+    # rank r's values start at r * max_n (padded gather) or after the lower ranks' (packed gather)
+    n_rank = [int(v) for v in all_sizes.sum(1).tolist()]
+    padded = vals.numel() == world * max(n_rank)
+    start = [r * max(n_rank) for r in range(world)] if padded else [sum(n_rank[:r]) for r in range(world)]
     wts = None
     if cw is not None:
         wts = dist.allgather_rows(cw.to(torch.float64).reshape(-1, 1).to(cd), pad_value=0.0).to(dev)[:, 0]
@@ -676,7 +676,7 @@ def _merge_candidates(dist, dev, cval, cw, loc_sizes, glob_off):
         loff = torch.cumsum(sz, 0) - sz
         k = torch.arange(n_r, device=dev) - loff[seg]
         dest = glob_off[:-1][seg] + before[r][seg] + k
-        out_v[dest] = vals[r * per:r * per + n_r]
+        out_v[dest] = vals[start[r]:start[r] + n_r]
         if out_w is not None:
-            out_w[dest] = wts[r * per:r * per + n_r].to(torch.int32)
+            out_w[dest] = wts[start[r]:start[r] + n_r].to(torch.int32)
     return out_v, out_w

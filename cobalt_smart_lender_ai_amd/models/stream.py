@@ -96,7 +96,11 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
     N = int(n_rows)
     n_glob = n_rows_global if n_rows_global is not None else (
         int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
-    stride = sketch.sample_stride(n_glob, sketch_rows)
+    # SKETCH_AUTO (-1): the 2^18-row strided sample (a stream's rows are not all in device memory at
+    # once; None / 0 = every row's values gathered)
+    if sketch_rows is not None and sketch_rows < 0:
+        sketch_rows = 1 << 18
+    stride = sketch.sample_stride(n_glob, sketch_rows or 0)
     F = None
     parts, seen = [], 0
     miss = None  # per-feature NaN presence over the WHOLE stream (decides 255 vs 256 bins)

@@ -105,8 +105,9 @@ def test_gpu_large_n_kernel_shapes_identical_to_host_oracle():
     n = 4_300_000
     X, y = synth.make_lendingclub(n, seed=31)
     spw = float((y == 0).sum() / (y == 1).sum())
+    # every row sketched on both sides (the GPU's bucketed device sketch vs the CPU's full sort)
     p = gbdt.GBDTParams(n_estimators=2, max_depth=7, learning_rate=0.3, gamma=1.0, scale_pos_weight=spw,
-                        random_state=78)
+                        random_state=78, sketch_rows=None)
     rep = gbdt.FitReport()
     bg = gbdt.train(X.cuda(), y.cuda(), p, device="cuda", report=rep)
     bc = gbdt.train(X, y, p, device="cpu")
