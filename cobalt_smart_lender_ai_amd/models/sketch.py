@@ -409,9 +409,6 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     ranks compute the cuts of the full data. ``w_max`` scales the weights (default: the global max)."""
     import os
 
-    from .. import _native
-
-    lib = _sk_lib()
     N, F = X.shape
     dev = X.device
     timing = os.environ.get("COBALT_SK_TIMING") == "1"  # per-stage times (device-synchronised) to stderr
@@ -424,8 +421,6 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     mark("start")
     world = dist.world if dist is not None else 1
     n_glob = n_rows_global if n_rows_global is not None else N
-    NBND, NB, CAP = lib.cobalt_sk_bounds(), lib.cobalt_sk_buckets(), lib.cobalt_sk_sort_cap()
-    stream = _native.stream_handle()
     X = X.to(torch.float32)
     if has_missing is None:
         has_missing = torch.isnan(X).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
@@ -433,13 +428,6 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
             t = has_missing.to(torch.float32).to(dist._coll_device(dev))
             dist.allreduce(t, "max")
             has_missing = t.to(dev) > 0
-    maxb = feature_max_bins(max_bin, has_missing.to(dev))                            # [F] int64
-    if X.is_contiguous() and 0 < F <= 32 and N:                                      # [F, N]
-        XT = torch.empty((F, N), dtype=torch.float32, device=dev)
-        _native.check(lib.cobalt_sk_transpose(X.data_ptr(), N, F, XT.data_ptr(), stream), "cobalt_sk_transpose")
-    else:
-        XT = X.t().contiguous()
-    mark("transpose")
     wq = None
     if weights is not None:
         wd = weights.to(device=dev, dtype=torch.float64).reshape(-1)
@@ -452,10 +440,58 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
         scale = WEIGHT_SCALE / w_max if w_max and w_max > 0 else 0.0
         wq = (torch.round(wd * scale) if scale else torch.ones_like(wd)).to(torch.int32).contiguous()
 
-    # 1. boundaries: <= NBND - 1 distinct values of the global strided sample
     samp = local_sample(X, row_offset, sample_stride(n_glob, sample_rows))
     if world > 1:
         samp = dist.allgather_rows(samp)
+    return _exact_core(lambda: iter([(X, wq)]), True, N, F, dev, samp, has_missing, max_bin, dist, wq is not None,
+                       mark, marks, timing)
+
+
+def stream_exact_cuts(chunks, n_rows: int, n_features: int, samp: torch.Tensor, has_missing: torch.Tensor,
+                      max_bin: int = 256, *, dist=None, device=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """:func:`device_exact_cuts` of data that arrives in chunks (``chunks()`` yields CUDA [n_c, F]
+    float32 tensors; it is iterated twice): every row sketched, bit for bit the in-core cuts, with
+    one chunk on the device at a time. ``samp``: a (global, strided) sample for the bucket boundaries;
+    unweighted."""
+    import os
+
+    dev = torch.device(device)
+    timing = os.environ.get("COBALT_SK_TIMING") == "1"
+    marks = []
+
+    def mark(name):
+        if timing:
+            torch.cuda.synchronize(dev)
+            marks.append((name, __import__("time").perf_counter()))
+    mark("start")
+    return _exact_core(lambda: ((c, None) for c in chunks()), False, int(n_rows), int(n_features), dev, samp,
+                       has_missing, max_bin, dist, False, mark, marks, timing)
+
+
+def _sk_transpose(lib, X, stream):
+    """[n, F] float32 (CUDA) -> feature-major [F, n]."""
+    from .. import _native
+
+    N, F = X.shape
+    if X.is_contiguous() and 0 < F <= 32 and N:
+        XT = torch.empty((F, N), dtype=torch.float32, device=X.device)
+        _native.check(lib.cobalt_sk_transpose(X.data_ptr(), N, F, XT.data_ptr(), stream), "cobalt_sk_transpose")
+        return XT
+    return X.t().contiguous()
+
+
+def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, weighted, mark, marks, timing):
+    """The bucketed exact sketch over the rows of ``chunks()`` ((X_chunk, int32 weights or None)
+    pairs; ``single``: one chunk, its transpose and pass-1 slabs are reused by the gather)."""
+    from .. import _native
+
+    lib = _sk_lib()
+    world = dist.world if dist is not None else 1
+    NBND, NB, CAP = lib.cobalt_sk_bounds(), lib.cobalt_sk_buckets(), lib.cobalt_sk_sort_cap()
+    stream = _native.stream_handle()
+    maxb = feature_max_bins(max_bin, has_missing.to(dev))                            # [F] int64
+
+    # 1. boundaries: <= NBND - 1 distinct values of the global strided sample
     sv = torch.sort((samp.t() + 0.0).contiguous(), dim=1).values                     # [F, S], NaN last
     mark("sort")
     S = sv.shape[1]
@@ -476,20 +512,37 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     bounds = bounds[:, :NBND].contiguous()
     mark("bounds")
 
-    # 2. bucket histograms (row counts; weight sums when weighted) + min / max valid value
-    nblk = max(1, min(64, -(-N // 65536)))
-    cnt_slab = torch.zeros((nblk, F, NB), dtype=torch.int32, device=dev)
-    w_slab = torch.zeros((nblk, F, NB), dtype=torch.int64, device=dev) if wq is not None else None
-    bmm = torch.empty((nblk, F, 2), dtype=torch.float32, device=dev)
-    bmm[:, :, 0] = float("inf")
-    bmm[:, :, 1] = float("-inf")
-    if N:
-        rc = lib.cobalt_sk_hist(XT.data_ptr(), N, N, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), nblk,
-                                cnt_slab.data_ptr(), _ptr(w_slab), bmm.data_ptr(), stream)
-        _native.check(rc, "cobalt_sk_hist")
-    cnt_loc = cnt_slab.sum(0, dtype=torch.int64)                                      # [F, NB]
-    w_h = w_slab.sum(0) if w_slab is not None else None
-    vmin, vmax = bmm[:, :, 0].amin(0), bmm[:, :, 1].amax(0)
+    # 2. bucket histograms (row counts; weight sums when weighted) + min / max valid value, per chunk
+    def chunk_hist(XT, n, wq):
+        nblk = max(1, min(64, -(-n // 65536)))
+        cnt_slab = torch.zeros((nblk, F, NB), dtype=torch.int32, device=dev)
+        w_slab = torch.zeros((nblk, F, NB), dtype=torch.int64, device=dev) if wq is not None else None
+        bmm = torch.empty((nblk, F, 2), dtype=torch.float32, device=dev)
+        bmm[:, :, 0] = float("inf")
+        bmm[:, :, 1] = float("-inf")
+        if n:
+            rc = lib.cobalt_sk_hist(XT.data_ptr(), n, n, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), nblk,
+                                    cnt_slab.data_ptr(), _ptr(w_slab), bmm.data_ptr(), stream)
+            _native.check(rc, "cobalt_sk_hist")
+        return nblk, cnt_slab, w_slab, bmm
+
+    cnt_loc = torch.zeros((F, NB), dtype=torch.int64, device=dev)
+    w_h = torch.zeros((F, NB), dtype=torch.int64, device=dev) if weighted else None
+    vmin = torch.full((F,), float("inf"), dtype=torch.float32, device=dev)
+    vmax = torch.full((F,), float("-inf"), dtype=torch.float32, device=dev)
+    kept = None
+    for Xc, wq in chunks():
+        Xc = Xc.to(torch.float32)
+        XT = _sk_transpose(lib, Xc, stream)
+        mark("transpose")
+        nblk, cnt_slab, w_slab, bmm = chunk_hist(XT, Xc.shape[0], wq)
+        cnt_loc += cnt_slab.sum(0, dtype=torch.int64)
+        if w_h is not None:
+            w_h += w_slab.sum(0)
+        vmin = torch.minimum(vmin, bmm[:, :, 0].amin(0))
+        vmax = torch.maximum(vmax, bmm[:, :, 1].amax(0))
+        if single:
+            kept = (XT, Xc.shape[0], wq, nblk, cnt_slab)
     cnt_h = cnt_loc
     if world > 1:
         cd = dist._coll_device(dev)
@@ -548,17 +601,29 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     tot_loc = int(loc_off[-1])
     mark("targets")
 
-    # 4. candidates: the rows of the selected buckets, per segment
+    # 4. candidates: the rows of the selected buckets, per segment (a second walk over the chunks;
+    # each block writes at its offset from the chunk's per-block bucket counts)
     cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)
-    cw = torch.empty(max(tot_loc, 1), dtype=torch.int32, device=dev) if wq is not None else None
+    cw = torch.empty(max(tot_loc, 1), dtype=torch.int32, device=dev) if weighted else None
     if nseg and N:
-        # where each hist block's rows of each segment start: pass 1's per-block counts, prefix-summed
-        # over the blocks (the gather walks the same row partition)
-        per_blk = cnt_slab.reshape(nblk, -1)[:, sel_f].to(torch.int64)                 # [nblk, nseg]
-        blk_off = (torch.cumsum(per_blk, 0) - per_blk + loc_off[:-1][None, :]).contiguous()
-        rc = lib.cobalt_sk_gather(XT.data_ptr(), N, N, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), slot.data_ptr(),
-                                  blk_off.data_ptr(), nseg, cval.data_ptr(), _ptr(cw), nblk, stream)
-        _native.check(rc, "cobalt_sk_gather")
+        cursor = loc_off[:-1].clone()
+        for Xc, wq in (iter([(None, None)]) if single else chunks()):
+            if single:
+                XT, n, wq, nblk, cnt_slab = kept
+            else:
+                Xc = Xc.to(torch.float32)
+                n = Xc.shape[0]
+                XT = _sk_transpose(lib, Xc, stream)
+                nblk, cnt_slab, _, _ = chunk_hist(XT, n, wq)
+            if not n:
+                continue
+            per_blk = cnt_slab.reshape(nblk, -1)[:, sel_f].to(torch.int64)                # [nblk, nseg]
+            blk_off = (torch.cumsum(per_blk, 0) - per_blk + cursor[None, :]).contiguous()
+            rc = lib.cobalt_sk_gather(XT.data_ptr(), n, n, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(),
+                                      slot.data_ptr(), blk_off.data_ptr(), nseg, cval.data_ptr(), _ptr(cw), nblk,
+                                      stream)
+            _native.check(rc, "cobalt_sk_gather")
+            cursor += per_blk.sum(0)
     if world > 1 and nseg:  # every rank's candidates, re-packed segment by segment
         cval, cw = _merge_candidates(dist, dev, cval[:tot_loc], None if cw is None else cw[:tot_loc], loc_sizes,
                                      glob_off)

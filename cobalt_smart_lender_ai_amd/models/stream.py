@@ -87,8 +87,11 @@ class _PinnedUploader:
 
 def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256, sketch_rows: int = 1 << 18,
                 device=None, dist=None, row_offset: int = 0, n_rows_global: int | None = None):
-    """Quantile cuts of a chunk stream from the rows whose GLOBAL index is a multiple of the sketch
-    stride (the in-core sample). Returns ``(cuts, nbins, n_rows, n_rows_global, n_features)``."""
+    """Quantile cuts of a chunk stream: the in-core fit's cuts for the same ``sketch_rows``. On a GPU
+    with every row sketched (``sketch_rows`` SKETCH_AUTO / None / 0) the bucketed device sketch runs
+    over the stream, one chunk on the device at a time (sketch.stream_exact_cuts: two more passes);
+    otherwise the rows whose GLOBAL index is a multiple of the sketch stride are gathered (SKETCH_AUTO
+    on the CPU: 2^18 rows). Returns ``(cuts, nbins, n_rows, n_rows_global, n_features)``."""
     dev = _resolve_device(device, None)
     world = dist.world if dist is not None else 1
     if n_rows is None:
@@ -96,11 +99,13 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
     N = int(n_rows)
     n_glob = n_rows_global if n_rows_global is not None else (
         int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
-    # SKETCH_AUTO (-1): the 2^18-row strided sample (a stream's rows are not all in device memory at
-    # once; None / 0 = every row's values gathered)
-    if sketch_rows is not None and sketch_rows < 0:
-        sketch_rows = 1 << 18
-    stride = sketch.sample_stride(n_glob, sketch_rows or 0)
+    exact_dev = dev.type == "cuda" and (sketch_rows is None or sketch_rows <= 0)
+    if exact_dev:  # the boundary sample of sketch.device_exact_cuts (same global rows)
+        stride = sketch.sample_stride(n_glob, 1 << 16)
+    else:
+        if sketch_rows is not None and sketch_rows < 0:
+            sketch_rows = 1 << 18
+        stride = sketch.sample_stride(n_glob, sketch_rows or 0)
     F = None
     parts, seen = [], 0
     miss = None  # per-feature NaN presence over the WHOLE stream (decides 255 vs 256 bins)
@@ -121,7 +126,16 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
         hm = has_missing.to(torch.float32).to(dist._coll_device(dev))
         dist.allreduce(hm, "max")
         has_missing = hm.to(dev) > 0
-    cuts, nbins = sketch.compute_cuts(samp, max_bin, None, has_missing)
+    if exact_dev:
+        def chunks():
+            up = _PinnedUploader(dev)
+            for Xc, _ in source():
+                yield up.put(_as_np(Xc, np.float32))
+
+        cuts, nbins = sketch.stream_exact_cuts(chunks, N, F, samp, has_missing, max_bin,
+                                               dist=dist if world > 1 else None, device=dev)
+    else:
+        cuts, nbins = sketch.compute_cuts(samp, max_bin, None, has_missing)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return cuts, nbins, N, n_glob, F

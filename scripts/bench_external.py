@@ -43,10 +43,9 @@ def main() -> None:
 
     pos = float(sum(float(y.sum()) for _, y in source()))  # spw = neg/pos needs one pass over the labels
     spw = (a.rows - pos) / pos
-    # the streamed sketch samples 2^18 rows (models/stream.py); the in-core comparison uses the same cuts
+    # every row sketched in both (the streamed device sketch: sketch.stream_exact_cuts)
     params = gbdt.GBDTParams(n_estimators=a.trees, max_depth=a.depth, learning_rate=0.05, gamma=5.0, reg_lambda=1.0,
-                             min_child_weight=1.0, max_bin=256, scale_pos_weight=spw, random_state=78,
-                             sketch_rows=1 << 18)
+                             min_child_weight=1.0, max_bin=256, scale_pos_weight=spw, random_state=78)
     Xte, yte = synth.make_lendingclub(a.test_rows, seed=1, device=dev)
     torch.cuda.synchronize()
     rep = external.ExternalReport()

@@ -264,3 +264,36 @@ def test_device_exact_cuts_equal_the_full_sort(weighted):
         for f in range(X.shape[1]):
             nb = int(want_n[f])
             assert torch.equal(got_c[f, :nb].view(torch.int32), want_c[f, :nb].view(torch.int32)), f
+
+
+@pytest.mark.gpu
+def test_stream_exact_cuts_equal_in_core():
+    """The bucketed sketch over a chunk stream (sketch.stream_exact_cuts: one chunk on the device at a
+    time, pass-2 offsets carried across chunks) returns the in-core device sketch's cuts, and a streamed
+    fit with the default sketch (every row on a GPU) grows the in-core fit's trees."""
+    from cobalt_smart_lender_ai_amd.dataio import synth
+    from cobalt_smart_lender_ai_amd.models import stream
+
+    dev = torch.device("cuda", 0)
+    X2 = _adversarial_frames(400_000, dev, seed=3)
+    for X in (X2,):
+        hm = torch.isnan(X).any(0)
+        want_c, want_n = sketch.device_exact_cuts(X, 256, None, hm)
+        samp = sketch.local_sample(X, 0, sketch.sample_stride(X.shape[0], 1 << 16))
+        bounds = [0, 70_001, 150_000, 333_333, X.shape[0]]
+
+        def chunks():
+            for a, b in zip(bounds[:-1], bounds[1:]):
+                yield X[a:b].contiguous()
+
+        got_c, got_n = sketch.stream_exact_cuts(chunks, X.shape[0], X.shape[1], samp, hm, 256, device=dev)
+        assert torch.equal(got_n, want_n)
+        for f in range(X.shape[1]):
+            nb = int(want_n[f])
+            assert torch.equal(got_c[f, :nb].view(torch.int32), want_c[f, :nb].view(torch.int32)), f
+    Xh, yh = synth.make_lendingclub(300_000, seed=9)
+    Xh, yh = Xh.numpy(), yh.numpy()
+    params = dict(n_estimators=4, max_depth=6, learning_rate=0.3, random_state=2)
+    ref = gbdt.train(torch.from_numpy(Xh).cuda(), torch.from_numpy(yh).cuda(), params, device="cuda")
+    got = stream.train_stream(stream.array_chunks(Xh, yh, 70_000), params, n_rows=len(Xh), device="cuda")
+    assert got.save_raw("ubj") == ref.save_raw("ubj")
