@@ -9,7 +9,7 @@ row) and spills the rows' bins to pinned host pages in a compact format (the F b
 bytes: 20 B per row for the deployed features instead of the 32-byte record, since the per-tree page
 stream is bound by the H2D copy):
 
-1. ``stream_cuts`` -- the in-core quantile sketch over the stream (the cuts of an in-core fit with the same ``sketch_rows``; the default samples 2^18 rows);
+1. ``stream_cuts`` -- the in-core quantile sketch over the stream (the cuts of an in-core fit with the same ``sketch_rows``; by default every row for exact streaming on a GPU, a 2^18-row sample for the sampled mode);
 2. every chunk is binned on the GPU and its row records are copied to a pinned host page;
 3. per tree, every page streams back through ``k_ooc_page`` (double-buffered H2D on a copy stream):
    the previous tree is applied to the margins, g/h are computed, and a minimal-variance sample
@@ -135,8 +135,13 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
     dev = _resolve_device(device, None)
     rep = report if report is not None else ExternalReport()
     t0 = time.perf_counter()
-    cuts, nbins, N, _, F = stream_cuts(source, n_rows=n_rows, max_bin=params.max_bin,
-                                       sketch_rows=params.sketch_rows, device=dev)
+    # the sketch: exact streaming (every row) sketches every row by default, like the in-core fit on a
+    # GPU; the sampled mode keeps the 2^18-row strided sample (one pass over the stream instead of
+    # three -- with a regenerated or re-read source the extra passes cost seconds at 100M rows)
+    sk = params.sketch_rows
+    if sk is not None and sk < 0 and not exact:
+        sk = 1 << 18
+    cuts, nbins, N, _, F = stream_cuts(source, n_rows=n_rows, max_bin=params.max_bin, sketch_rows=sk, device=dev)
     if F > 24:
         raise ValueError("external-memory training packs a row into one 32-byte record (<= 24 features)")
     rep.t_sketch = time.perf_counter() - t0
