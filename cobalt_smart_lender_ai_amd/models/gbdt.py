@@ -55,8 +55,9 @@ class GBDTParams:
     base_score: float | None = None
     # rows of the strided global sample the quantile sketch uses; None / 0 = every row (exact weighted
     # quantiles; on the GPU the device sketch of csrc/sketch.hip, exact under data parallelism too);
-    # SKETCH_AUTO (default) = every row on a GPU (XGBoost hist's semantics, ~4 ms at 10M rows), a
-    # 2^18-row strided sample on the CPU and for streamed / external-memory data
+    # SKETCH_AUTO (default) = every row on a GPU (XGBoost hist's semantics: the device sketch, ~4 ms at
+    # 10M rows; up to 2^18 rows the full sort), a 2^18-row strided sample on the CPU; streams / external
+    # memory: see models/stream.stream_cuts
     sketch_rows: int | None = -1
     # quantile-sketch weights: "sample" = the sample weights (XGBoost hist semantics, the reference's
     # tree_method), "hessian" = first-round hessians (sample weight x scale_pos_weight for positives,
@@ -208,10 +209,12 @@ SKETCH_AUTO = -1
 SKETCH_SAMPLE_ROWS = 1 << 18
 
 
-def resolve_sketch_rows(sketch_rows: int | None, dev) -> int | None:
-    """SKETCH_AUTO -> None (every row) on a CUDA device, the 2^18-row sample elsewhere."""
+def resolve_sketch_rows(sketch_rows: int | None, dev, n_rows_global: int | None = None) -> int | None:
+    """SKETCH_AUTO -> None (every row, the device sketch) on a CUDA device above 2^18 rows; the
+    2^18-row sample elsewhere (up to 2^18 rows that sample IS every row, by the cheaper full sort)."""
     if sketch_rows is not None and sketch_rows < 0:
-        return None if torch.device(dev).type == "cuda" else SKETCH_SAMPLE_ROWS
+        big = n_rows_global is None or n_rows_global > SKETCH_SAMPLE_ROWS
+        return None if (torch.device(dev).type == "cuda" and big) else SKETCH_SAMPLE_ROWS
     return sketch_rows
 
 
@@ -227,12 +230,12 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     A feature gets 256 bins only if it has no missing value in the FULL data (all ranks).
     ``SKETCH_AUTO``: every row on a GPU, the 2^18-row sample on the CPU."""
     dev = _resolve_device(device, X)
-    sketch_rows = resolve_sketch_rows(sketch_rows, dev)
     world = dist.world if dist is not None else 1
     Xt = _to_tensor(X, dev)
     N, F = Xt.shape
     n_glob = n_rows_global if n_rows_global is not None else (
         int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
+    sketch_rows = resolve_sketch_rows(sketch_rows, dev, n_glob)
     ts = time.perf_counter()
     has_missing = torch.isnan(Xt).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
     if world > 1:

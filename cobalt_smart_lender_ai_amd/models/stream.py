@@ -99,7 +99,9 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
     N = int(n_rows)
     n_glob = n_rows_global if n_rows_global is not None else (
         int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
-    exact_dev = dev.type == "cuda" and (sketch_rows is None or sketch_rows <= 0)
+    # (up to 2^18 rows the strided sample is every row already: the cheaper full sort)
+    exact_dev = dev.type == "cuda" and (sketch_rows is None or sketch_rows == 0 or
+                                        (sketch_rows < 0 and n_glob > (1 << 18)))
     if exact_dev:  # the boundary sample of sketch.device_exact_cuts (same global rows)
         stride = sketch.sample_stride(n_glob, 1 << 16)
     else:
