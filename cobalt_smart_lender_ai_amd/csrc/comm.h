@@ -23,8 +23,16 @@ constexpr int kIpcStickyWord = 32;  // flag words: [0] = published epoch, [32] =
 // table of the ranks' flag words, this rank's flag word (+ sticky failure word), the pinned host error
 // word and the wait deadline. Two of them (parity 0 / 1) live in device memory for the group's
 // lifetime, so a kernel takes one pointer + the epoch instead of a per-launch copy.
+// Node-owner decision table (after the two send slots of every rank's exported buffer): per tree node
+// one record of 3 Node images (the node and its two children, 64 B each) + an 8-byte epoch tag.
+constexpr int kIpcDecStride = 256;
+constexpr int kIpcDecNodes = 2048;  // trees of depth <= 10
+constexpr int64_t kIpcDecBytes = (int64_t)kIpcDecStride * kIpcDecNodes;
+
 struct IpcFusedView {
   const char* slot[kMaxIpcRanks];
+  const char* dtab[kMaxIpcRanks];  // every rank's decision table (peer-mapped)
+  char* mydtab;
   const unsigned* const* ftab;
   unsigned* myflag;
   unsigned* err_host;

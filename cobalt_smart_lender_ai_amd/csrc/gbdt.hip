@@ -216,14 +216,22 @@ struct GbdtDev {
   int4* ep_items;
   int32_t ep_chunk, ep_zero;
   int32_t ep_plan;    // 1: items from ep_plan (COBALT_EP_PLAN=1), 0 (default): every block plans (block_plan)
+  // node ownership (fused IPC exchange): from level own_level on, a node is evaluated only by the rank
+  // owning its level-own_level ancestor; the others copy its decision (-1: every rank evaluates all)
+  int32_t own_level;
 };
 
 
 // 32-bit hash of one finalised node decision (position, status, split feature / bin / default
 // direction, threshold or leaf value): summed over a tree's nodes into GbdtDev::dig.
-__device__ __forceinline__ uint32_t node_hash(int n, int status, int feat, int bin, int dl, float cond) {
+// (G, H: the node's global sums -- under node ownership the other ranks copy a node's record, so a
+// rank whose sums went wrong at a level every rank evaluates must still show in the digest)
+__device__ __forceinline__ uint32_t node_hash(int n, int status, int feat, int bin, int dl, float cond, int64_t G,
+                                              int64_t H) {
   uint64_t x = ((uint64_t)(uint32_t)n << 32) ^ ((uint64_t)(uint32_t)status << 40) ^ ((uint64_t)(uint32_t)feat << 44) ^
                ((uint64_t)(uint32_t)(bin & 0x3FF) << 52) ^ ((uint64_t)(uint32_t)dl << 62) ^ __float_as_uint(cond);
+  x ^= (uint64_t)G * 0x9E3779B97F4A7C15ull;
+  x ^= ((uint64_t)H << 29) | ((uint64_t)H >> 35);
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdull;
   x ^= x >> 33;
@@ -1574,10 +1582,91 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
     nd.split_cond = nd.leaf_value;
   }
   if (d.dig) {  // replica digest (data parallel): this node's decision (+ its max-depth leaf children)
-    uint32_t hsum = node_hash(n, nd.status, ok ? nd.feat : -1, ok ? nd.bin : -1, ok ? nd.default_left : 0, nd.split_cond);
+    uint32_t hsum = node_hash(n, nd.status, ok ? nd.feat : -1, ok ? nd.bin : -1, ok ? nd.default_left : 0, nd.split_cond,
+                              nd.G, nd.H);
     if (ok && level + 1 == d.max_depth) {
-      hsum += node_hash(2 * n + 1, kLeaf, -1, -1, 0, nodes[2 * n + 1].split_cond);
-      hsum += node_hash(2 * n + 2, kLeaf, -1, -1, 0, nodes[2 * n + 2].split_cond);
+      hsum += node_hash(2 * n + 1, kLeaf, -1, -1, 0, nodes[2 * n + 1].split_cond, nodes[2 * n + 1].G, nodes[2 * n + 1].H);
+      hsum += node_hash(2 * n + 2, kLeaf, -1, -1, 0, nodes[2 * n + 2].split_cond, nodes[2 * n + 2].G, nodes[2 * n + 2].H);
+    }
+    atomicAdd(reinterpret_cast<unsigned long long*>(d.dig + d.dig_slot), (unsigned long long)hsum);
+  }
+}
+
+// Node ownership over the fused IPC exchange (levels >= d.own_level; 2^own_level >= ranks). A node's
+// histogram sums and split evaluation run on ONE rank -- the owner of its level-own_level ancestor, so
+// the owner also holds the parent histogram its subtree subtracts from -- instead of on every rank:
+// each rank reads 1/world of the level's cells over xGMI instead of all of them (and the sibling
+// duplication of the per-node blocks goes with it). The owner publishes the node's record and its
+// children's (everything but the rank-local row ranges) with an epoch tag into its exported decision
+// table (system-scope stores, the tag last); the other ranks poll the tag and copy the records.
+__device__ __forceinline__ int node_owner(const GbdtDev& d, int level, int n, int world) {
+  const int pos = n - ((1 << level) - 1);
+  return (pos >> (level - d.own_level)) % world;
+}
+
+__device__ __forceinline__ void own_publish(const GbdtDev& d, const IpcFusedView* iv, int n) {
+  // thread 0, after eval_finalize wrote the three records into this rank's node table
+  char* rec = iv->mydtab + (int64_t)n * kIpcDecStride;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(d.nodes + (k == 0 ? n : 2 * n + k));
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(rec + k * 64 + w * 8), src[w], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the records are written through before the tag
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(rec + 192), (unsigned long long)d.ipc_epoch,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A non-owner's block for node n (active at this level): wait for the owner's record of this epoch,
+// copy it into the local node table (the rank-local start / count words stay) and add the node's
+// replica-digest terms as the owner's eval_finalize did. Call from all threads.
+__device__ __forceinline__ void own_copy(const GbdtDev& d, const IpcFusedView* iv, int n, int level, int owner) {
+  __shared__ int s_ok;
+  const char* rec = iv->dtab[owner] + (int64_t)n * kIpcDecStride;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = __hip_atomic_load(iv->myflag + kIpcStickyWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    while (ok) {
+      const unsigned long long t = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(rec + 192),
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (t == (unsigned long long)d.ipc_epoch) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > iv->timeout) {
+        ok = 0;
+        __hip_atomic_store(iv->myflag + kIpcStickyWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(iv->err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_ok = ok;
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  if (threadIdx.x < 24) {
+    const int k = threadIdx.x >> 3, w = threadIdx.x & 7;
+    if (w != 2) {  // word 2 = (start, count): this rank's own row range
+      const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(rec + k * 64 + w * 8),
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      reinterpret_cast<unsigned long long*>(d.nodes + (k == 0 ? n : 2 * n + k))[w] = v;
+    }
+  }
+  __syncthreads();
+  // (a record whose node was not active on its owner means the trees diverged at a level every rank
+  // evaluates: the copy re-synchronises the node table so the tree completes on every rank, and the
+  // digest of those levels, compared at the next tree's root exchange, reports it on every rank alike)
+  if (threadIdx.x == 0 && d.dig) {
+    const Node nd = d.nodes[n];
+    const bool ok = nd.status == kSplit;
+    uint32_t hsum = node_hash(n, nd.status, ok ? nd.feat : -1, ok ? nd.bin : -1, ok ? nd.default_left : 0, nd.split_cond,
+                              nd.G, nd.H);
+    if (ok && level + 1 == d.max_depth) {
+      const Node& cl = d.nodes[2 * n + 1];
+      const Node& cr = d.nodes[2 * n + 2];
+      hsum += node_hash(2 * n + 1, kLeaf, -1, -1, 0, cl.split_cond, cl.G, cl.H);
+      hsum += node_hash(2 * n + 2, kLeaf, -1, -1, 0, cr.split_cond, cr.G, cr.H);
     }
     atomicAdd(reinterpret_cast<unsigned long long*>(d.dig + d.dig_slot), (unsigned long long)hsum);
   }
@@ -1810,6 +1899,13 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
     const int ce = kGroups ? d.hoff[fend] : d.ncells;
     // (k_eval_part publishes before its plan: its block 0 is not always an evaluating block)
     if (!kMerged && blockIdx.x == 0 && blockIdx.y == 0) ipc_publish(iv->myflag, d.ipc_epoch);
+    if (!kGroups && !kMerged && d.own_level >= 0 && level >= d.own_level) {
+      const int owner = node_owner(d, level, n, iv->n);
+      if (owner != iv->me) {  // another rank evaluates this node: take its decision
+        if (status == kActive) own_copy(d, iv, n, level, owner);
+        return false;
+      }
+    }
     if (!ipc_wait<kIpcAcquireFence>(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout))
       return false;
     // the global root totals are stored at level 0 (k_eval_finish reads them)
@@ -2003,7 +2099,16 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
   BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   __shared__ EvalOut s_out;
-  if (!eval_core<kGroups, kFused>(d, level, parity, tree, fg, es, pos, stamp_, &s_out)) return;
+  if (!eval_core<kGroups, kFused>(d, level, parity, tree, fg, es, pos, stamp_, &s_out)) {
+    // an owned node that is not active on its owner still publishes its record: a rank whose tree went
+    // another way (replica divergence) and waits for it then learns so instead of timing out
+    if (kFused && !kGroups && threadIdx.x == 0 && d.own_level >= 0 && level >= d.own_level) {
+      const int n = (1 << level) - 1 + pos;
+      const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
+      if (node_owner(d, level, n, iv->n) == iv->me && d.nodes[n].status != kActive) own_publish(d, iv, n);
+    }
+    return;
+  }
   if (threadIdx.x != 0) return;  // thread 0 wrote s_out
   const Cand best = s_out.best;
   const float best_cut = s_out.cut;
@@ -2017,6 +2122,8 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     return;
   }
   eval_finalize(d, level, (1 << level) - 1 + pos, s_out.G, s_out.H, best, best_cut, s_out.nb);
+  if (kFused && d.own_level >= 0 && level >= d.own_level)  // the other ranks copy this node's decision
+    own_publish(d, d.ipcv + (d.ipc_epoch & 1u), (1 << level) - 1 + pos);
   stamp_.probe(4);
 }
 
@@ -3233,6 +3340,18 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // hand-off and the late row / bin loads cost more than the launch they save -- so off by default)
   static const int env_dp_ep = getenv("COBALT_DP_EVAL_PART") ? atoi(getenv("COBALT_DP_EVAL_PART")) : 0;
   const int ep_mode = !dp ? 0 : (ipc_fused ? (env_dp_ep ? 2 : -1) : 1);
+  // node ownership (see node_owner): over the fused exchange with separate k_eval / k_partition passes,
+  // on the three deepest split levels (where the exchange volume is: 56 of a depth-7 tree's 64 pairs;
+  // the copy costs the other ranks one more remote round trip, not worth it for a level's few nodes),
+  // and never before a level with a node per rank. COBALT_DP_OWNER=0: every rank evaluates every node
+  static const int env_owner = getenv("COBALT_DP_OWNER") ? atoi(getenv("COBALT_DP_OWNER")) : 1;
+  d.own_level = -1;
+  if (ipc_fused && ep_mode == -1 && env_owner && d.world > 1 && eval_fg == 0 && c->max_nodes <= kIpcDecNodes) {
+    int l0 = 0;
+    while ((1 << l0) < d.world) ++l0;
+    l0 = std::max(l0, D - 3);
+    d.own_level = l0 < D ? l0 : -1;
+  }
   const bool eval_part = env_ep != 0 && ep_mode >= 0 && eval_fg == 0 && !eval_compact && !fuse_part && part_wide(d) &&
                          ep_steps <= 8 && d.F <= 32 && (ep_mode != 2 || fused_lds <= 65536);
   // Item size of a level's fused pass: the grid (items + one partial item per node) must fit one

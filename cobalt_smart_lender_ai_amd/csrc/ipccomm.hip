@@ -88,9 +88,12 @@ struct IpcGroup {
   int64_t cap = 0;             // bytes per send slot
   char* xbuf = nullptr;        // [2][cap], exported
   unsigned* flags = nullptr;   // uncached; flags[0] = last published epoch, exported
+  char* dtab = nullptr;        // uncached node-owner decision table (kIpcDecBytes), exported: written and
+                               // read by the ranks' kernels while they run, so not L2-cacheable memory
   unsigned* err_host = nullptr;  // pinned + mapped: [0] = a wait timed out (sticky)
   unsigned* err_dev = nullptr;
   IpcPeers peers{};
+  const char* dpeer[kMaxIpcRanks] = {};  // every rank's decision table (own + mapped peers)
   const unsigned** ftab = nullptr;  // device copy of peers.flag (polled lane-parallel)
   IpcFusedView* views = nullptr;    // device [2]: the group per slot parity (ipc_device_views)
   std::vector<void*> opened;
@@ -109,8 +112,8 @@ struct IpcGroup {
     }                                                                                     \
   } while (0)
 
-// Size of one rank's exported handle blob (send slots + flag word).
-COBALT_API int cobalt_ipc_handle_bytes() { return (int)(2 * sizeof(hipIpcMemHandle_t)); }
+// Size of one rank's exported handle blob (send slots + flag word + decision table).
+COBALT_API int cobalt_ipc_handle_bytes() { return (int)(3 * sizeof(hipIpcMemHandle_t)); }
 
 // Allocate this rank's send slots (2 x cap_bytes) and flag word on the current device and write their
 // IPC handles to handles_out (cobalt_ipc_handle_bytes() bytes). The comm is usable after connect.
@@ -127,18 +130,22 @@ COBALT_API int cobalt_ipc_create(int rank, int nranks, int64_t cap_bytes, double
   g->timeout_ticks = (uint64_t)(std::max(0.001, timeout_s) * 1e8);
   IPC_CK(hipMalloc((void**)&g->xbuf, 2 * g->cap));
   IPC_CK(hipMemset(g->xbuf, 0, 2 * g->cap));
+  IPC_CK(hipExtMallocWithFlags((void**)&g->dtab, kIpcDecBytes, hipDeviceMallocUncached));
+  IPC_CK(hipMemset(g->dtab, 0, kIpcDecBytes));
   IPC_CK(hipExtMallocWithFlags((void**)&g->flags, 256, hipDeviceMallocUncached));
   IPC_CK(hipMemset(g->flags, 0, 256));
   IPC_CK(hipHostMalloc((void**)&g->err_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
   memset(g->err_host, 0, 64);
   IPC_CK(hipHostGetDevicePointer((void**)&g->err_dev, g->err_host, 0));
-  hipIpcMemHandle_t h[2];
+  hipIpcMemHandle_t h[3];
   IPC_CK(hipIpcGetMemHandle(&h[0], g->xbuf));
   IPC_CK(hipIpcGetMemHandle(&h[1], g->flags));
+  IPC_CK(hipIpcGetMemHandle(&h[2], g->dtab));
   memcpy(handles_out, h, sizeof(h));
   IPC_CK(hipDeviceSynchronize());
   g->peers.x[rank] = g->xbuf;
   g->peers.flag[rank] = g->flags;
+  g->dpeer[rank] = g->dtab;
   *out = new CobaltComm{2, nullptr, nullptr, rank, nranks, g};
   return 0;
 }
@@ -153,18 +160,26 @@ COBALT_API int cobalt_ipc_connect(void* comm, const void* all_handles) {
     if (r == g->rank) continue;
     void* px = nullptr;
     void* pf = nullptr;
-    IPC_CK(hipIpcOpenMemHandle(&px, hs[2 * r], hipIpcMemLazyEnablePeerAccess));
+    void* pd = nullptr;
+    IPC_CK(hipIpcOpenMemHandle(&px, hs[3 * r], hipIpcMemLazyEnablePeerAccess));
     g->opened.push_back(px);
-    IPC_CK(hipIpcOpenMemHandle(&pf, hs[2 * r + 1], hipIpcMemLazyEnablePeerAccess));
+    IPC_CK(hipIpcOpenMemHandle(&pf, hs[3 * r + 1], hipIpcMemLazyEnablePeerAccess));
     g->opened.push_back(pf);
+    IPC_CK(hipIpcOpenMemHandle(&pd, hs[3 * r + 2], hipIpcMemLazyEnablePeerAccess));
+    g->opened.push_back(pd);
     g->peers.x[r] = static_cast<const char*>(px);
     g->peers.flag[r] = static_cast<const unsigned*>(pf);
+    g->dpeer[r] = static_cast<const char*>(pd);
   }
   IPC_CK(hipMalloc((void**)&g->ftab, kMaxIpcRanks * sizeof(unsigned*)));
   IPC_CK(hipMemcpy(g->ftab, g->peers.flag, kMaxIpcRanks * sizeof(unsigned*), hipMemcpyHostToDevice));
   IpcFusedView hv[2] = {};
   for (int p = 0; p < 2; ++p) {
-    for (int r = 0; r < g->n; ++r) hv[p].slot[r] = g->peers.x[r] + (int64_t)p * g->cap;
+    for (int r = 0; r < g->n; ++r) {
+      hv[p].slot[r] = g->peers.x[r] + (int64_t)p * g->cap;
+      hv[p].dtab[r] = g->dpeer[r];
+    }
+    hv[p].mydtab = g->dtab;
     hv[p].ftab = g->ftab;
     hv[p].myflag = g->flags;
     hv[p].err_host = g->err_dev;
@@ -276,6 +291,7 @@ void ipc_release(CobaltComm* c) {
   for (void* p : g->opened) (void)hipIpcCloseMemHandle(p);
   if (g->xbuf) (void)hipFree(g->xbuf);
   if (g->flags) (void)hipFree(g->flags);
+  if (g->dtab) (void)hipFree(g->dtab);
   if (g->ftab) (void)hipFree(g->ftab);
   if (g->views) (void)hipFree(g->views);
   if (g->err_host) (void)hipHostFree(g->err_host);

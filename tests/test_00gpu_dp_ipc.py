@@ -35,8 +35,12 @@ def test_ipc_data_parallel_processes_equal_single_process():
     # COBALT_DP_EVAL_PART=1), and the separate exchange kernel (COBALT_IPC_FUSED=0: k_eval_part mode 1
     # over the all-reduced histograms). The ranks share the device through disjoint CU masks
     # (parallel/cumask.py); 8 ranks: test_ipc_eight_ranks_share_one_gpu
-    for procs, env in ((2, None), (3, None), (4, None), (2, {"COBALT_DP_EVAL_PART": "1"}),
-                       (4, {"COBALT_DP_EVAL_PART": "1"}), (2, {"COBALT_IPC_FUSED": "0"})):
+    # node ownership (the default over the fused exchange: levels 4-6 of these depth-7 trees, owners by
+    # subtree) and every rank evaluating every node (COBALT_DP_OWNER=0); a depth-3 fit owns from the
+    # first level with a node per rank
+    for procs, env in ((2, None), (3, None), (4, None), (5, None), (3, {"COBALT_DP_OWNER": "0"}),
+                       (2, {"COBALT_DP_EVAL_PART": "1"}), (4, {"COBALT_DP_EVAL_PART": "1"}),
+                       (2, {"COBALT_IPC_FUSED": "0"})):
         got = dp_check.run(procs, ROWS, timeout_s=400, env=env)
         for g in got:
             assert g["ok"], (procs, env, g)
@@ -44,6 +48,11 @@ def test_ipc_data_parallel_processes_equal_single_process():
             # one exchange per level per tree, plus the connect self-test's four (each slot twice)
             assert g["ipc_epochs"] == 4 + 7 * ref["trees"]
             assert g["model_sha256"] == ref["model_sha256"], (procs, env, g["rank"])
+    shallow = dict(dp_check.DEFAULT_PARAMS, max_depth=3)
+    ref3 = dp_check.run(1, ROWS, shallow)[0]
+    for procs in (2, 3):
+        for g in dp_check.run(procs, ROWS, shallow, timeout_s=400):
+            assert g["ok"] and g["model_sha256"] == ref3["model_sha256"], (procs, g)
 
 
 @pytest.mark.timeout(600)
