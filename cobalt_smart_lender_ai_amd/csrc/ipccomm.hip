@@ -72,6 +72,45 @@ __global__ __launch_bounds__(256) void k_ipc_exchange(IpcPeers p, const unsigned
     zero_dst[i] = make_int4(0, 0, 0, 0);
 }
 
+// Decision-table probe (connect self-test of the node-owner path): every rank writes a record whose
+// words encode its rank and the round into its table's spare last slot (system-scope stores, the tag
+// last) and reads every peer's record back (tag poll + system-scope loads), as the trainer's owners and
+// copying ranks do mid-kernel. result: 0 = every peer's record arrived intact, 1 = wrong words, 2 =
+// a tag did not arrive before the deadline.
+__global__ void k_ipc_dtab_probe(const IpcFusedView* v, unsigned round, unsigned* result) {
+  if (threadIdx.x != 0) return;
+  const int n = v->n, me = v->me;
+  const int64_t slot = (int64_t)(kIpcDecNodes - 1) * kIpcDecStride;
+  const unsigned long long tag = 0x5E1F7E57ull ^ ((unsigned long long)round << 32);
+  char* mine = v->mydtab + slot;
+  for (int w = 0; w < 24; ++w)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(mine + w * 8),
+                       ((unsigned long long)(me + 1) << 40) ^ ((unsigned long long)round << 20) ^ (unsigned long long)w,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_s_waitcnt(0);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(mine + 192), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned res = 0;
+  for (int r = 0; r < n; ++r) {
+    if (r == me) continue;
+    const char* rec = v->dtab[r] + slot;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    while (__hip_atomic_load(reinterpret_cast<const unsigned long long*>(rec + 192), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM) != tag) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > v->timeout) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) { res |= 2u; continue; }
+    for (int w = 0; w < 24; ++w) {
+      const unsigned long long x = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(rec + w * 8),
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (x != (((unsigned long long)(r + 1) << 40) ^ ((unsigned long long)round << 20) ^ (unsigned long long)w))
+        res |= 1u;
+    }
+  }
+  *result = res;
+}
+
 int elem_bytes(int dtype) {
   switch (dtype) {
     case 0: case 4: return 8;
@@ -206,6 +245,26 @@ COBALT_API int cobalt_ipc_set_timeout(void* comm, double timeout_s) {
     IPC_CK(hipMemcpy(g->views, hv, sizeof(hv), hipMemcpyHostToDevice));
   }
   return 0;
+}
+
+// Decision-table probe of the connect self-test (k_ipc_dtab_probe); every rank calls it with the same
+// round. Returns the probe's result word (0 = ok), < 0 on a launch error.
+COBALT_API int cobalt_ipc_dtab_selftest(void* comm, unsigned round, hipStream_t stream) {
+  CobaltComm* c = static_cast<CobaltComm*>(comm);
+  if (!c || c->kind != 2 || !c->ipc->views) return -3;
+  unsigned* d_res = nullptr;
+  IPC_CK(hipMalloc((void**)&d_res, sizeof(unsigned)));
+  hipLaunchKernelGGL(k_ipc_dtab_probe, dim3(1), dim3(64), 0, stream, c->ipc->views, round, d_res);
+  unsigned h_res = 0;
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(&h_res, d_res, sizeof(unsigned), hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  (void)hipFree(d_res);
+  if (e != hipSuccess) {
+    comm_set_error("ipc: decision-table probe failed to run");
+    return -(int)e;
+  }
+  return (int)h_res;
 }
 
 void* ipc_send_buffer(CobaltComm* c) {

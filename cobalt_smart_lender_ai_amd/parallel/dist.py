@@ -292,6 +292,17 @@ def _ipc_selftest(ctx: DistContext, comm: int) -> None:
         want = idx * (w * (w + 1) // 2) + 1000 * rnd * w
         if not torch.equal(buf, want):
             raise RuntimeError("IPC self-test all-reduce returned wrong sums")
+    # the node-owner decision table (written and read by the ranks' kernels while they run): two rounds
+    # of a record per rank, read back by every peer (csrc/ipccomm.hip k_ipc_dtab_probe)
+    probe = getattr(lib, "cobalt_ipc_dtab_selftest", None)
+    if probe is not None:
+        for rnd in range(2):
+            res = probe(ctypes.c_void_p(comm), rnd + 1, ctypes.c_void_p(_native.stream_handle()))
+            if res != 0:
+                raise RuntimeError(f"IPC decision-table self-test failed ({res}): "
+                                   + ("a peer's record did not arrive" if res == 2 else "records corrupted")
+                                   if res > 0 else lib.cobalt_comm_last_error().decode())
+            ctx.barrier()  # (every rank read round k before any rank overwrites it with round k + 1)
 
 
 def create_rccl_comm(ctx: DistContext) -> int:
