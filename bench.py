@@ -176,6 +176,10 @@ def main() -> None:
             "sketch_rows": a.sketch_rows or "all",
             "dp_transport": ctx.transport if world > 1 else None,
             "dp_transport_fallback": fallback,
+            # csrc/gbdt.hip node ownership: deep levels evaluated by the subtree's owner rank only
+            "dp_node_ownership": (f"levels {max((world - 1).bit_length(), a.depth - 3)}-{a.depth - 1}"
+                                  if world > 1 and ctx.transport == "ipc" and os.environ.get("COBALT_DP_OWNER", "1") != "0"
+                                  and os.environ.get("COBALT_DP_EVAL_PART", "0") == "0" else None),
             "replica_check": "in-flight per-tree digest of every rank's split decisions" if world > 1 else None,
             "replicas_agree": replicas_agree,
             "auc": None if auc is None else round(auc, 5),
