@@ -32,6 +32,7 @@ def main() -> None:
     sets = {"queues": ((8, {"GPU_MAX_HW_QUEUES": "1"}), (8, {"GPU_MAX_HW_QUEUES": "2"}), (6, {}), (8, {})),
             "width": ((5, {"COBALT_IPC_TIMEOUT_S": "100"}), (6, {"COBALT_IPC_TIMEOUT_S": "100"}),
                       (6, {"COBALT_IPC_TIMEOUT_S": "100", "COBALT_SHARED_CU_MASK": "0"})),
+            "eight1": ((8, {"COBALT_IPC_TIMEOUT_S": "250", "COBALT_SHARED_CU_MASK": "0"}),),
             "eight": ((8, {"COBALT_IPC_TIMEOUT_S": "250", "COBALT_SHARED_CU_MASK": "0", "GPU_MAX_HW_QUEUES": "1"}),
                       (8, {"COBALT_IPC_TIMEOUT_S": "250", "COBALT_SHARED_CU_MASK": "0"}))}
     configs = sets[sys.argv[1] if len(sys.argv) > 1 else "queues"]
