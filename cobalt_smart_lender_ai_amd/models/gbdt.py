@@ -223,9 +223,11 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
                 sketch_mode: str = "sample") -> BinnedData:
     """Weighted quantile sketch (K12) on a global strided sample + binning (K13).
 
-    ``sketch_rows`` None / 0: every row (XGBoost ``hist`` sketches all rows): exact weighted quantiles
-    on one rank; under data parallelism every rank summarises its whole shard on its device and the
-    summaries are merged (all-gathering 10M raw rows would move the matrix itself).
+    ``sketch_rows`` None / 0: every row (XGBoost ``hist`` sketches all rows), exact weighted quantiles.
+    On a GPU this is the bucketed device sketch (``sketch.device_exact_cuts``): under data parallelism
+    its bucket histograms are all-reduced and the target buckets' candidates all-gathered, so every rank
+    gets the full data's cuts without gathering the raw rows. On the CPU under data parallelism each
+    rank summarises its shard and the summaries are merged (``sketch_mode="summary"``).
     ``sketch_weights`` ([N_local], optional): per-row sketch weights (see models/sketch.py).
     A feature gets 256 bins only if it has no missing value in the FULL data (all ranks).
     ``SKETCH_AUTO``: every row on a GPU, the 2^18-row sample on the CPU."""

@@ -62,6 +62,20 @@ def test_hessian_sketch_weights_scale_positives():
         gbdt.sketch_weights_for(gbdt.GBDTParams(sketch_weight="bogus"), y, None, "cpu")
 
 
+def test_sketch_auto_resolution():
+    """SKETCH_AUTO (the default): every row on a GPU above 2^18 rows (the exact device sketch), the
+    2^18-row sample on the CPU and for small data (where that sample is every row); explicit values
+    pass through."""
+    auto, samp = gbdt.SKETCH_AUTO, gbdt.SKETCH_SAMPLE_ROWS
+    assert gbdt.GBDTParams().sketch_rows == auto
+    assert gbdt.resolve_sketch_rows(auto, "cuda", 10_000_000) is None
+    assert gbdt.resolve_sketch_rows(auto, "cuda", None) is None
+    assert gbdt.resolve_sketch_rows(auto, "cuda", samp) == samp
+    assert gbdt.resolve_sketch_rows(auto, "cpu", 10_000_000) == samp
+    for v in (None, 0, 4096):
+        assert gbdt.resolve_sketch_rows(v, "cuda", 10_000_000) == v
+
+
 def test_host_binning_and_training_with_256_bin_features():
     X = _mixed(20_000, 4)
     y = (np.nan_to_num(X[:, 1]) + 0.002 * X[:, 0] / 1e3 > 0.5).astype(np.float32)
