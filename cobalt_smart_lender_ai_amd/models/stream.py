@@ -7,7 +7,9 @@ chunks (CSV pages, Arrow batches, NumPy shards) and only its quantised form is e
 * pass 1 (only when the row count is not given) counts rows;
 * pass 2 keeps the rows whose GLOBAL index is a multiple of the sketch stride -- exactly the sample
   the in-core path draws -- so the quantile cuts (K12) and therefore the trees are identical to
-  an in-core fit of the same rows;
+  an in-core fit of the same rows. On a GPU with every row sketched (the default, SKETCH_AUTO) that
+  sample only places the device sketch's bucket boundaries, and two more passes (bucket histogram,
+  candidate gather: ``sketch.stream_exact_cuts``) give the all-row cuts of the in-core fit;
 * pass 3 uploads each chunk through a pair of pinned staging buffers (the host parses chunk k+1
   while the device copies and bins chunk k) and quantises it in place into the preallocated row
   records + feature-major bins (``cobalt_bin_matrix_ld``, K13): 32 B + F B per row on the device
@@ -22,7 +24,7 @@ import numpy as np
 import torch
 
 from . import sketch
-from .gbdt import BinnedData, GBDTParams, _resolve_device, train_binned
+from .gbdt import SKETCH_AUTO, SKETCH_SAMPLE_ROWS, BinnedData, GBDTParams, _resolve_device, train_binned
 
 Chunk = tuple  # (X [n, F] float32, y [n])
 ChunkSource = Callable[[], Iterable[Chunk]]
@@ -85,9 +87,11 @@ class _PinnedUploader:
         return out
 
 
-def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256, sketch_rows: int = 1 << 18,
+def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256,
+                sketch_rows: int | None = SKETCH_AUTO,
                 device=None, dist=None, row_offset: int = 0, n_rows_global: int | None = None):
-    """Quantile cuts of a chunk stream: the in-core fit's cuts for the same ``sketch_rows``. On a GPU
+    """Quantile cuts of a chunk stream: the in-core fit's cuts for the same ``sketch_rows`` (default
+    SKETCH_AUTO, as ``gbdt.bin_dataset``). On a GPU
     with every row sketched (``sketch_rows`` SKETCH_AUTO / None / 0) the bucketed device sketch runs
     over the stream, one chunk on the device at a time (sketch.stream_exact_cuts: two more passes);
     otherwise the rows whose GLOBAL index is a multiple of the sketch stride are gathered (SKETCH_AUTO
@@ -101,12 +105,12 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
         int(dist.allreduce_scalar(N, "sum", dev)) if world > 1 else N)
     # (up to 2^18 rows the strided sample is every row already: the cheaper full sort)
     exact_dev = dev.type == "cuda" and (sketch_rows is None or sketch_rows == 0 or
-                                        (sketch_rows < 0 and n_glob > (1 << 18)))
+                                        (sketch_rows < 0 and n_glob > SKETCH_SAMPLE_ROWS))
     if exact_dev:  # the boundary sample of sketch.device_exact_cuts (same global rows)
         stride = sketch.sample_stride(n_glob, 1 << 16)
     else:
         if sketch_rows is not None and sketch_rows < 0:
-            sketch_rows = 1 << 18
+            sketch_rows = SKETCH_SAMPLE_ROWS
         stride = sketch.sample_stride(n_glob, sketch_rows or 0)
     F = None
     parts, seen = [], 0
@@ -143,7 +147,8 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
     return cuts, nbins, N, n_glob, F
 
 
-def bin_stream(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256, sketch_rows: int = 1 << 18,
+def bin_stream(source: ChunkSource, *, n_rows: int | None = None, max_bin: int = 256,
+               sketch_rows: int | None = SKETCH_AUTO,
                device=None, dist=None, row_offset: int = 0,
                n_rows_global: int | None = None) -> tuple[BinnedData, torch.Tensor]:
     """Quantise a chunk stream; returns the binned matrix and the labels (on ``device``)."""
