@@ -1122,7 +1122,8 @@ __device__ __forceinline__ void hist_rows_pair(const GbdtDev& d, uint64_t* s_his
   static_assert(FT4 >= 16 && FT4 <= 24, "pair split covers 16 < F <= 24");
   constexpr int FH = FT4 / 2, Q = FH / 4, S = FH % 4;  // lane 1's first byte: word Q, byte S
   constexpr int NW = (FH + 3) / 4;                     // words of bins per lane
-  constexpr int U = 4;  // rows in flight per pair (6: 257.3 ms per 10M fit, 4: 252.0; 8 spills at 80 VGPRs)
+  constexpr int U = 4;  // rows in flight per pair (6: 257.3 ms per 10M fit, 4: 252.0; 8 spills at 80 VGPRs;
+                        // round 4, same box: 5 at 78 VGPRs 241.0 vs 235.7)
   const int h = (int)(hl.lane & 1u);
   const int P = (int)(blockDim.x >> 1), pslot = (int)(threadIdx.x >> 1);
   // this lane's features: metadata and copy bases (VGPRs, selected once)
