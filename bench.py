@@ -31,6 +31,14 @@ import torch
 
 BASELINE_ROWS_PER_S = None  # the reference publishes no throughput (BASELINE.json "published": {})
 
+# AUC parity (within +-0.002 of a CPU histogram GBDT trained on the same synthetic rows with
+# the same hyper-parameters). The CPU reference of the headline configuration -- 10M training rows,
+# 300 trees, depth 7, seed 0, AUC on the next 1M rows -- is scikit-learn's HistGradientBoosting
+# (16 threads): 0.95106 (profiles/configs/cpu-hist-gbdt-10m.json, scripts/bench_configs.py
+# cpu-hist-gbdt-10m). Other configurations have no recorded reference (auc_parity_ok: null).
+PARITY_AUC = {(10_000_000, 300, 7, 0, 1_000_000): 0.95106}
+PARITY_TOL = 0.002
+
 
 def main() -> None:
     ap = argparse.ArgumentParser()
@@ -138,6 +146,11 @@ def main() -> None:
         Xt, yt = synth.make_lendingclub(a.test_rows, seed=a.seed, row_offset=n_global, device=dev)
         p = booster.predict_proba(Xt, device=dev)
         auc = float(roc_auc(yt, p))
+    parity_ref = PARITY_AUC.get((n_global, a.trees, a.depth, a.seed, a.test_rows))
+    auc_parity_ok = None if (auc is None or parity_ref is None) else abs(auc - parity_ref) <= PARITY_TOL
+    if auc_parity_ok is False:
+        print(f"[bench] WARNING: AUC {auc:.5f} drifted from the CPU reference {parity_ref:.5f} by more than "
+              f"{PARITY_TOL}", file=sys.stderr)
     ms = elapsed / max(a.steps, 1) * 1e3
     value = n_global * a.steps / elapsed
     if a.profile_fit and rank == 0:
@@ -179,10 +192,12 @@ def main() -> None:
             # csrc/gbdt.hip node ownership: deep levels evaluated by the subtree's owner rank only
             "dp_node_ownership": (f"levels {max((world - 1).bit_length(), a.depth - 3)}-{a.depth - 1}"
                                   if world > 1 and ctx.transport == "ipc" and os.environ.get("COBALT_DP_OWNER", "1") != "0"
-                                  and os.environ.get("COBALT_DP_EVAL_PART", "0") == "0" else None),
+                                  and os.environ.get("COBALT_IPC_FUSED", "1") != "0" else None),
             "replica_check": "in-flight per-tree digest of every rank's split decisions" if world > 1 else None,
             "replicas_agree": replicas_agree,
             "auc": None if auc is None else round(auc, 5),
+            "auc_parity_ref": parity_ref,
+            "auc_parity_ok": auc_parity_ok,
             "test_rows": a.test_rows,
             "fit_breakdown_ms": {
                 "sketch": round(sum(r.t_sketch for r in reps) / len(reps) * 1e3, 3),

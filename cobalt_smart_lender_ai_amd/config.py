@@ -122,3 +122,80 @@ def load_yaml(cls, path: str | Path):
     data = yaml.safe_load(Path(path).read_text()) or {}
     names = {f.name for f in dataclasses.fields(cls)}
     return cls(**{k: v for k, v in data.items() if k in names})
+
+
+# ------------------------------------------------------------------------------------------------
+# Environment knobs: EVERY ``COBALT_*`` variable the package reads, in one documented registry.
+# scope "native" = read by the HIP/C++ library through csrc/knobs.cpp (knob_int / knob_str, the only
+# getenv calls of csrc/); "python" = read by the Python package; "test" = fault injection and test-only
+# switches. tests/test_knobs.py checks that the native registry and every COBALT_* name in the source
+# tree appear here. Defaults are the measured-best settings (docs/PERF.md); knobs of rejected
+# experiments are deleted together with their code.
+# ------------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class Knob:
+    default: str
+    scope: str
+    doc: str
+
+
+KNOBS: dict[str, Knob] = {
+    # -- trainer tuning / diagnostics (native) --
+    "COBALT_STAMPS": Knob("", "native", "file: in-kernel launch / probe timestamps of sampled trees (scripts/stamp_summary.py)"),
+    "COBALT_HIST_ABLATE": Knob("0", "native", "timing-only ablations of the histogram / partition / root passes (wrong models)"),
+    "COBALT_HIST_CHUNK": Knob("auto", "native", "rows per histogram work item at levels >= 1 (~n/1536, 1024..4096)"),
+    "COBALT_HIST_CHUNK0": Knob("auto", "native", "rows per root histogram item when the root pass is not fused"),
+    "COBALT_ROOT_CHUNK": Knob("auto", "native", "rows per item of the fused gradient + root-histogram pass (whole rounds of 2 blocks per CU)"),
+    "COBALT_PART_CHUNK": Knob("auto", "native", "rows per partition item (4096 while a level fits one block per CU, else 8192; <= 8192)"),
+    "COBALT_EVAL_FG": Knob("auto", "native", "features per split-evaluation group (0 = one block per node; 8 above 32 features)"),
+    "COBALT_EVAL_PART": Knob("1", "native", "split evaluation fused into the partition pass while a level fits one block per CU (0 off, 2 forced)"),
+    "COBALT_HIST_PAIR": Knob("1", "native", "lane-pair record gathers in the histogram levels (16 < F <= 24)"),
+    "COBALT_MAX_COPY_SHIFT": Knob("4", "native", "log2 of the per-lane LDS histogram copies of a low-cardinality feature (0..6)"),
+    "COBALT_WT": Knob("auto", "native", "write-through stores: bit 0 histogram slabs, bit 1 partition row ids (3 below 4M rows, else 1)"),
+    "COBALT_BIN_SCALAR": Knob("", "native", "force the generic binning kernel for 32-byte records (tests)"),
+    "COBALT_PRED_WALK": Knob("4", "native", "trees walked at once per predictor thread (2 / 4 / 8)"),
+    # -- data parallelism --
+    "COBALT_IPC_FUSED": Knob("1", "native", "IPC exchange fused into the split evaluation (0: separate exchange kernel + fused eval/partition)"),
+    "COBALT_DP_OWNER": Knob("1", "native", "node ownership on the three deepest levels over the fused IPC exchange"),
+    "COBALT_CU_BUDGET": Knob("", "native", "CUs of this rank's CU-masked stream (set by parallel/cumask.py)"),
+    "COBALT_DP_TRANSPORT": Knob("auto", "python", "native communicator: auto (IPC within a node), ipc or rccl"),
+    "COBALT_DIST_BACKEND": Knob("auto", "python", "torch.distributed backend override (gloo for ranks sharing one GPU)"),
+    "COBALT_DIST_NATIVE": Knob("auto", "python", "create the trainer's native communicator with a gloo bootstrap (1)"),
+    "COBALT_IPC_SLOT_MB": Knob("64", "python", "IPC send-slot capacity per rank"),
+    "COBALT_IPC_TIMEOUT_S": Knob("120", "python", "in-kernel exchange deadline before the group fails on every rank"),
+    "COBALT_IPC_CONNECT_TIMEOUT_S": Knob("30", "python", "deadline of the IPC connect self-test"),
+    "COBALT_COLLECTIVE_TIMEOUT_S": Knob("1800", "python", "host watchdog deadline for one enqueued segment of trees"),
+    "COBALT_SHARED_CU_MASK": Knob("auto", "python", "CU-masked streams for ranks sharing one GPU (default up to 5 ranks)"),
+    "COBALT_BENCH_SHARED_DEVICE": Knob("0", "python", "bench.py: every rank on cuda:0 (the 1-GPU multi-rank rehearsal)"),
+    # -- trainer / serving (python) --
+    "COBALT_LABEL_IN_RECORD": Knob("1", "python", "0/1 labels ride in the row records' padding (weights derived from them)"),
+    "COBALT_TRAINER_CACHE": Knob("1", "python", "keep one trainer context per process for back-to-back fits of the same shapes"),
+    "COBALT_SEARCH_STREAMS": Knob("4", "python", "HIP streams of the randomized search's concurrent fits"),
+    "COBALT_PRED_TILE": Knob("2048", "python", "tree nodes per LDS tile of the GPU predictor"),
+    "COBALT_SK_TIMING": Knob("0", "python", "per-stage times of the device quantile sketch to stderr"),
+    "COBALT_NATIVE_LIB": Knob("", "python", "load this native library instead of _lib/libcobalt_hip.so (A/B builds, host-ASan build)"),
+    "COBALT_OFFLOAD_ARCH": Knob("gfx950", "python", "offload architecture of the native build"),
+    "COBALT_RCCL_LIB": Knob("auto", "python", "path of librccl for the native RCCL communicator"),
+    "COBALT_ARTIFACT_URI": Knob("data-lake", "python", "artifact store: a local directory or s3://bucket"),
+    "COBALT_MODEL_PATH": Knob("models/xgb_model_tree.pkl", "python", "model the API serves"),
+    "COBALT_SOURCE": Knob("local", "python", "model source of the API (s3 with boto3)"),
+    "COBALT_SCORER_SOCKET": Knob("", "python", "unix socket of the GPU scorer process behind `serve --workers N`"),
+    "COBALT_SERVE_WORKERS": Knob("1", "python", "HTTP worker processes of `serve`"),
+    # -- fault injection / tests --
+    "COBALT_FAULT_AFTER_TREES": Knob("0", "test", "a rank fails (or stalls, with COBALT_FAULT_STALL_S) after this many trees"),
+    "COBALT_FAULT_RANK": Knob("-1", "test", "the rank COBALT_FAULT_AFTER_TREES applies to (-1: every rank)"),
+    "COBALT_FAULT_STALL_S": Knob("0", "test", "the faulting rank stalls this long once instead of dying"),
+    "COBALT_FAULT_CORRUPT_RANK": Knob("-1", "test", "this rank perturbs a tree's root totals (replica-divergence test)"),
+    "COBALT_FAULT_CORRUPT_TREE": Knob("1", "test", "the tree COBALT_FAULT_CORRUPT_RANK perturbs"),
+    "COBALT_TEST_DP8": Knob("0", "test", "run the 8-process shared-GPU data-parallel test"),
+    "COBALT_REFERENCE_PKL": Knob("", "test", "path of the reference's shipped model for the golden tests"),
+    "COBALT_REFERENCE_UI": Knob("", "test", "path of the reference Streamlit script for the UI replay test"),
+    "COBALT_RECORD_UI": Knob("", "test", "record the UI replay's exchanges"),
+}
+
+
+def knob(name: str, default: str | None = None) -> str | None:
+    """The value of a registered ``COBALT_*`` knob (``default`` when unset)."""
+    if name not in KNOBS:
+        raise KeyError(f"{name} is not a registered knob (config.KNOBS)")
+    return os.environ.get(name, default)

@@ -16,7 +16,12 @@ struct CobaltComm {
 };
 
 constexpr int kMaxIpcRanks = 16;
-constexpr int kIpcStickyWord = 32;  // flag words: [0] = published epoch, [32] = sticky failure
+// flag words: [0] = published epoch, [32] = sticky failure (this rank's later waits fail at once),
+// [40] = failure notice for the PEERS: a rank whose wait timed out (or that saw a peer's notice) sets it,
+// and every peer's next wait sees it and fails too -- so one rank's timeout surfaces as a timeout on
+// every rank (instead of the others running on with a stale exchange and reporting a divergence)
+constexpr int kIpcStickyWord = 32;
+constexpr int kIpcFailWord = 40;
 
 // The IPC group as seen by a kernel that performs the exchange itself (the GBDT split evaluation sums
 // the ranks' histogram slots while it reads them), for one slot parity: rank r's send slot, the device

@@ -25,6 +25,7 @@
 #include "common.h"
 #include "comm.h"
 #include "ipc_device.h"
+#include "knobs.h"
 #include <math.h>
 #include <string.h>
 #include <stdlib.h>
@@ -157,14 +158,14 @@ struct GbdtDev {
   int32_t* cursors;       // [max_nodes][2]
   int2* layout;           // [F] histogram LDS layout: x = cell offset within tile, y = log2(copies)
   int32_t* tile_entries;  // [n_tiles] LDS cells per feature tile
-  int64_t* hist_loc[2];   // DP only: [2^level][slot_elems] this rank's LOCAL histograms of the level's nodes
   uint64_t* slab;         // [items][F][256] packed per-item partial histograms
   int64_t* slab_tot;      // [items][2] per-item (G, H) totals
   int32_t ablate;         // timing-only ablation (COBALT_HIST_ABLATE): 1 no LDS atomics, 2 no flush, 3 no rows,
                           // 4 plan only (k_hist); 12 partition without the cursor claims; root pass: 20 no exp,
                           // 21 no LDS atomics, 22 no previous-tree walk
-  int32_t dp;             // data parallel: the all-reduced slot of a pair is its LEFT child (see k_dp_local)
-  int32_t by_hess;        // build k_eval's (global) hessian choice: DP default, COBALT_BUILD_BY_HESS on one GPU
+  int32_t dp;             // data parallel (a native communicator is attached)
+  int32_t by_hess;        // build k_eval's (global) hessian choice: under data parallelism (every rank builds the
+                          // same child, so the collective sums it as is); one GPU builds the locally smaller one
   int32_t hist_pair;      // k_hist gathers each record with a lane pair (hist_rows_pair); COBALT_HIST_PAIR
   CandRec* cand;          // [2^(max_depth-1)][64] per-group split candidates (grouped evaluation)
   int64_t n;
@@ -195,7 +196,6 @@ struct GbdtDev {
   // so the gradient pass reads neither the label nor the weight array
   int32_t ylab;
   float spw;
-  int32_t pwide;  // host-side: 16-wave partition blocks (see part_wide)
   // In-flight replica check (data parallel only; dig == nullptr on one GPU). Every node decision a
   // tree finalises adds a 32-bit hash to dig[tree & 1] (eval_finalize). At level 0 of the next tree
   // the reduce writes the previous tree's sum into an extra int64 cell right after the root slot
@@ -209,13 +209,9 @@ struct GbdtDev {
   int32_t world;
   int32_t corrupt;    // fault injection (COBALT_FAULT_CORRUPT_RANK): perturb this tree's root totals
   unsigned* err_host;
-  uint64_t* dec;      // [max_nodes] k_eval_part<mode 2>: a node's decision granule {tag, decision}
-  // k_eval_part work items of the level, laid out by the histogram pass's block (0, 0) (ep_plan):
-  // {node, begin, end} per item, the count in counters[1]; ep_chunk = the level's item size (0: the
-  // level has no fused pass), ep_zero = active nodes without local rows get an empty item (DP)
-  int4* ep_items;
+  // fused evaluation + partition pass (k_eval_part): ep_chunk = the level's item size (0: the level has
+  // no fused pass), ep_zero = active nodes without local rows get an empty item (DP)
   int32_t ep_chunk, ep_zero;
-  int32_t ep_plan;    // 1: items from ep_plan (COBALT_EP_PLAN=1), 0 (default): every block plans (block_plan)
   // node ownership (fused IPC exchange): from level own_level on, a node is evaluated only by the rank
   // owning its level-own_level ancestor; the others copy its decision (-1: every rank evaluates all)
   int32_t own_level;
@@ -242,9 +238,20 @@ __device__ __forceinline__ uint32_t node_hash(int n, int status, int feat, int b
 
 // Level 0 of a tree, after the collective: `sum` is the digest cell summed over the ranks.
 __device__ __forceinline__ void digest_check(const GbdtDev& d, int64_t sum) {
-  if (!d.dig) return;
   const int64_t own = d.dig_check ? d.dig[d.dig_slot ^ 1] : 0;
   if (sum != (int64_t)d.world * own) __hip_atomic_store(d.err_host, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Final replica check of a grow call (data parallel): the in-flight check compares tree t's digest at
+// tree t + 1's root exchange, which never comes for the LAST tree of a call -- so that tree's digest gets
+// an all-reduce of its own (k_dig_stage -> the communicator's int64 sum of dig[2] -> k_dig_cmp) before the
+// host fetches or checkpoints the trees. dig[2] is the staging cell.
+__global__ void k_dig_stage(int64_t* dig, int slot) {
+  if (threadIdx.x == 0) dig[2] = dig[slot];
+}
+__global__ void k_dig_cmp(const int64_t* dig, int slot, int world, unsigned* err_host) {
+  if (threadIdx.x == 0 && dig[2] != (int64_t)world * dig[slot])
+    __hip_atomic_store(err_host, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Store of a value the next launch reads: plain, or write-through (agent-scope relaxed atomic store =
@@ -713,9 +720,9 @@ __device__ PlanOut block_plan(int n_ent, int chunk, int item, EntryFn entry, int
 }
 
 // Histogram pass of `level`: entries are the node pairs; the child histogrammed from rows is the one
-// with fewer LOCAL rows (the partition cursors), the sibling comes by exact subtraction. Under DP each
-// rank picks by its own counts and k_dp_local turns the result into the pair's local LEFT histogram
-// before the all-reduce, so no collective is needed to agree on the choice.
+// with fewer LOCAL rows (the partition cursors) on one GPU, the one with the smaller GLOBAL hessian
+// (k_eval's choice, the same on every rank) under data parallelism; the sibling comes by exact
+// subtraction.
 __device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, int p) {
   if (level == 0) return PlanEntry{0, 0, 0, (int)d.n};
   const int q = (1 << (level - 1)) - 1 + p;
@@ -739,11 +746,9 @@ __device__ __forceinline__ PlanEntry hist_entry(const GbdtDev& d, int level, int
 // Block (0, 0) of the histogram pass publishes the level's node ranges / build flags for the
 // evaluation and partition kernels, resets the level's partition counters and the item count.
 // `build` is the child whose GLOBAL histogram sits in hist_b after the reduce (+ all-reduce): the
-// locally smaller one on one GPU, always the left one under DP.
-// With keep_build (fused partition path) the build flags chosen by k_eval stay, and total < 0 leaves
-// the item count alone (it was written by the fused pass itself).
-__device__ void publish_level(const GbdtDev& d, int level, int total, bool keep_build = false) {
-  if (total >= 0 && threadIdx.x == 0) d.counters[0] = total;
+// locally smaller one on one GPU; under data parallelism k_eval's hessian choice stays.
+__device__ void publish_level(const GbdtDev& d, int level, int total) {
+  if (threadIdx.x == 0) d.counters[0] = total;
   if (level == 0) return;
   const int npairs = 1 << (level - 1);
   for (int p = threadIdx.x; p < npairs; p += blockDim.x) {
@@ -752,12 +757,12 @@ __device__ void publish_level(const GbdtDev& d, int level, int total, bool keep_
     if (par.status != kSplit) continue;
     const int L = 2 * q + 1, R = 2 * q + 2;
     const int lc = d.cursors[2 * q];
-    const bool left_small = d.dp || lc <= d.cursors[2 * q + 1];
+    const bool left_small = lc <= d.cursors[2 * q + 1];
     d.nodes[L].start = par.start;
     d.nodes[L].count = lc;
     d.nodes[R].start = par.start + lc;
     d.nodes[R].count = par.count - lc;
-    if (!keep_build) {
+    if (!d.by_hess) {
       d.nodes[L].build = left_small ? 1 : 0;
       d.nodes[R].build = left_small ? 0 : 1;
     }
@@ -767,43 +772,6 @@ __device__ void publish_level(const GbdtDev& d, int level, int total, bool keep_
     d.cursors[2 * (first + i)] = 0;
     d.cursors[2 * (first + i) + 1] = 0;
   }
-}
-
-// Block (0, 0) of the histogram pass of level L > 0 also lays out the level's fused evaluation +
-// partition items (k_eval_part then loads its item -- one load -- instead of planning: the node-table
-// loads + wave scan + barrier were ~2.5 us at the head of every block). A node's row range is its
-// parent's partition split, as publish_level computes it; wave 0 of the block.
-__device__ void ep_plan(const GbdtDev& d, int level) {
-  if (wave_id() != 0) return;
-  const int lane = lane_id();
-  const int n_ent = 1 << level, first = n_ent - 1;
-  const int chunk = d.ep_chunk;
-  int carry = 0;
-  for (int base = 0; base < n_ent; base += kWave) {
-    const int e = base + lane;
-    int node = -1, start = 0, cnt = 0;
-    if (e < n_ent) {
-      const int n = first + e, q = (n - 1) >> 1;
-      const Node& par = d.nodes[q];
-      const int st = par.status, pstart = par.start, pcount = par.count;  // loaded together
-      const int lc = d.cursors[2 * q];
-      const bool left = (n & 1) == 1;
-      if (st == kSplit) {
-        node = n;
-        start = left ? pstart : pstart + lc;
-        cnt = left ? lc : pcount - lc;
-      }
-    }
-    const int nch = node < 0 ? 0 : (cnt > 0 ? (cnt + chunk - 1) / chunk : (d.ep_zero ? 1 : 0));
-    const int incl = wave_incl_scan(nch) + carry;
-    const int excl = incl - nch;
-    for (int k = 0; k < nch; ++k) {
-      const int b = start + k * chunk;
-      d.ep_items[excl + k] = make_int4(node, b, min(start + cnt, b + chunk), 0);
-    }
-    carry = readlane32(incl, kWave - 1);
-  }
-  if (lane == 0) d.counters[1] = carry;
 }
 
 // LDS histogram helpers shared by k_hist and k_grad_hist (32-byte record fast path).
@@ -1099,12 +1067,6 @@ __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int appl
   grad_hist_body<U, FT4>(d, tree, apply_tree, chunk);
 }
 
-// One row in flight per thread within 80 VGPRs (no spill): 3 blocks per CU, 24 waves instead of 16
-template <int FT4>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k_grad_hist_w6(GbdtDev d, int tree,
-                                                                                              int apply_tree, int chunk) {
-  grad_hist_body<1, FT4>(d, tree, apply_tree, chunk);
-}
 
 // Lane-pair record gathers for the deep histogram levels (16 < F <= 24 features): lanes 2p and 2p+1
 // take the SAME row and load its two 16-byte halves in ONE instruction, so a wave-instruction fetches
@@ -1222,10 +1184,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
   // barrier after the row loop publishes it to the flush
   flush_meta_store(fmeta, ft, s_fo, s_fs);
   stamp_.probe(1);
-  if (item == 0 && blockIdx.y == 0) {
-    publish_level(d, level, pl.total, d.by_hess != 0);
-    if (level > 0 && d.ep_chunk > 0 && d.ep_plan) ep_plan(d, level);
-  }
+  if (item == 0 && blockIdx.y == 0) publish_level(d, level, pl.total);
   if (pl.node < 0) return;
   WorkItem w;
   w.node = pl.node;
@@ -1367,10 +1326,10 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
 // global atomic per non-zero cell per (run, slot) -- coalesced, 30-100x fewer than per-block flushes.
 constexpr int kRedItems = 16;
 
-__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int publish, int n_grid, int level) {
+// kDP: data parallel (the replica-digest cell of level 0); the single-GPU instantiation has none of it.
+template <bool kDP>
+__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int n_grid, int level) {
   BlockStamp stamp_(d);
-  // fused partition path: block (0, 0) publishes the level's node ranges from the finished claims
-  if (publish > 0 && blockIdx.x == 0 && blockIdx.y == 0) publish_level(d, publish, -1, true);
   const int i0 = blockIdx.x * kRedItems;
   const int ncell = d.ncells;
   const int cell = blockIdx.y * blockDim.x + threadIdx.x;
@@ -1411,7 +1370,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
   // replica check (data parallel): the previous tree's digest goes into the cell after the root slot
   // (all-reduced with it); this tree's accumulator restarts (no eval of this tree has run yet). After
   // the loads above are issued: at the kernel's head its branch delayed them (+0.4 us per launch).
-  if (level == 0 && d.dig && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+  if (kDP && level == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     int64_t* const red = d.hist_red ? d.hist_red : d.hist_b[parity];
     red[d.slot_elems] = d.dig_check ? d.dig[d.dig_slot ^ 1] : 0;
     red[d.slot_elems + 1] = 0;
@@ -1446,43 +1405,6 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
     atomicAdd(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)sg);
     atomicAdd(reinterpret_cast<unsigned long long*>(dst + 1), (unsigned long long)sh);
   }
-}
-
-// Data parallel, between the reduce and the all-reduce: hist_b holds, per pair, the histogram of
-// the child this rank built from rows (its locally smaller one). With the rank's local parent
-// histogram (kept from the previous level) the local sibling is an exact subtraction, so every rank
-// can send its LOCAL LEFT child whatever it built; the all-reduced slot is then the global left
-// child on every rank, and both children's local histograms are kept for the next level. This
-// replaces an all-reduce of the children's row counts per level (one collective, and one
-// cross-rank synchronisation, fewer per level). Grid: (pair, 256-cell block); level 0 keeps the root.
-__global__ __launch_bounds__(256) void k_dp_local(GbdtDev d, int level, int parity) {
-  BlockStamp stamp_(d);
-  const int p = blockIdx.x;
-  const int64_t e = ((int64_t)blockIdx.y * blockDim.x + threadIdx.x) * 2;  // (g, h) of one cell
-  if (e >= d.slot_elems) return;
-  const int64_t SE = d.slot_elems;
-  int64_t* hb = d.hist_b[parity] + p * SE + e;
-  if (level == 0) {
-    int64_t* loc = d.hist_loc[0] + e;
-    loc[0] = hb[0];
-    loc[1] = hb[1];
-    return;
-  }
-  const int q = (1 << (level - 1)) - 1 + p;  // the parent (level - 1, position p)
-  if (d.nodes[q].status != kSplit) return;
-  const bool left_built = d.cursors[2 * q] <= d.cursors[2 * q + 1];
-  const int64_t* par = d.hist_loc[parity ^ 1] + p * SE + e;
-  const int64_t bg = hb[0], bh = hb[1];
-  const int64_t sg = par[0] - bg, sh = par[1] - bh;
-  int64_t* lo = d.hist_loc[parity] + (int64_t)(2 * p) * SE + e;  // left child (position 2p)
-  int64_t* ro = lo + SE;                                          // right child (position 2p + 1)
-  const int64_t lg = left_built ? bg : sg, lh = left_built ? bh : sh;
-  lo[0] = lg;
-  lo[1] = lh;
-  ro[0] = left_built ? sg : bg;
-  ro[1] = left_built ? sh : bh;
-  hb[0] = lg;
-  hb[1] = lh;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1531,6 +1453,7 @@ struct EvalFeat {
 
 // Node decision from its best candidate (split or leaf; children of the last split level become leaves).
 // `nb_known` >= 0: the winning feature's bin count (the compact evaluator has it in LDS), else loaded.
+template <bool kDP>
 __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int64_t H, Cand best, float best_cut,
                               int nb_known = -1) {
   Node* nodes = d.nodes;
@@ -1582,7 +1505,7 @@ __device__ void eval_finalize(const GbdtDev& d, int level, int n, int64_t G, int
     nd.leaf_value = (float)(wgt * d.eta);
     nd.split_cond = nd.leaf_value;
   }
-  if (d.dig) {  // replica digest (data parallel): this node's decision (+ its max-depth leaf children)
+  if (kDP) {  // replica digest (data parallel): this node's decision (+ its max-depth leaf children)
     uint32_t hsum = node_hash(n, nd.status, ok ? nd.feat : -1, ok ? nd.bin : -1, ok ? nd.default_left : 0, nd.split_cond,
                               nd.G, nd.H);
     if (ok && level + 1 == d.max_depth) {
@@ -1630,14 +1553,15 @@ __device__ __forceinline__ void own_copy(const GbdtDev& d, const IpcFusedView* i
   if (threadIdx.x == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     int ok = __hip_atomic_load(iv->myflag + kIpcStickyWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    const unsigned* notice = iv->ftab[owner] + kIpcFailWord;  // the owner gave up: no record will come
     while (ok) {
       const unsigned long long t = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(rec + 192),
                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (t == (unsigned long long)d.ipc_epoch) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > iv->timeout) {
+      if (__hip_atomic_load(notice, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+          __builtin_amdgcn_s_memrealtime() - t0 > iv->timeout) {
         ok = 0;
-        __hip_atomic_store(iv->myflag + kIpcStickyWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(iv->err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ipc_fail(iv->myflag, iv->err_host);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -1658,7 +1582,7 @@ __device__ __forceinline__ void own_copy(const GbdtDev& d, const IpcFusedView* i
   // (a record whose node was not active on its owner means the trees diverged at a level every rank
   // evaluates: the copy re-synchronises the node table so the tree completes on every rank, and the
   // digest of those levels, compared at the next tree's root exchange, reports it on every rank alike)
-  if (threadIdx.x == 0 && d.dig) {
+  if (threadIdx.x == 0) {  // (own_copy runs under data parallelism only: d.dig is set)
     const Node nd = d.nodes[n];
     const bool ok = nd.status == kSplit;
     uint32_t hsum = node_hash(n, nd.status, ok ? nd.feat : -1, ok ? nd.bin : -1, ok ? nd.default_left : 0, nd.split_cond,
@@ -1798,7 +1722,9 @@ struct EvalOut {
 // other threads see it after a barrier). Shared by k_eval and the fused evaluation + partition pass.
 // `kMerged` (k_eval_part): the node counts as active whatever its status (another block of the same
 // node may already have finalised it), and only `store_hist` blocks store its histogram.
-template <bool kGroups, bool kFused, bool kMerged = false>
+// kDP: data parallel (kFused implies it): the level-0 replica-digest check and the fault-injection hook;
+// the single-GPU instantiation carries neither.
+template <bool kGroups, bool kFused, bool kDP, bool kMerged = false>
 __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parity, int tree, int fg, const EvalSlots& es,
                                           int pos, BlockStamp& stamp_, EvalOut* s_out, bool store_hist = true) {
   const int fbeg = kGroups ? blockIdx.y * fg : 0;
@@ -1912,7 +1838,7 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
     // the global root totals are stored at level 0 (k_eval_finish reads them)
     // (+ the replica-digest cell at level 0)
     ipc_sum_cells_n(__builtin_amdgcn_readfirstlane(iv->n), iv, (int64_t)pair * SE * (int64_t)sizeof(int64_t), cb,
-                    ce - cb, ce - cb + 1 + (level == 0 && d.dig ? 1 : 0), d.ncells, s_cells,
+                    ce - cb, ce - cb + 1 + (level == 0 ? 1 : 0), d.ncells, s_cells,
                     reinterpret_cast<longlong2*>(d.hist_b[parity] + pair * SE), built && status == kActive,
                     level == 0 && blockIdx.y == 0);
     __syncthreads();
@@ -1923,7 +1849,7 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
   // node totals: wave-uniform, pinned to SGPRs (vector-loaded, they held VGPRs across the scan)
   int64_t G = readlane64(level == 0 ? rg : ng, 0);
   const int64_t H = readlane64(level == 0 ? rh : nh, 0);
-  if (level == 0 && d.corrupt) G += (int64_t)1 << 24;  // fault injection: this rank grows a different tree
+  if (kDP && level == 0 && d.corrupt) G += (int64_t)1 << 24;  // fault injection: this rank grows a different tree
   // No early return for an inactive node: a branch here let hipcc sink the feature metadata loads
   // below it (a third dependent round trip). Its block computes on valid buffers and stores nothing.
   const bool active = kMerged ? status != kNone : status == kActive;
@@ -2080,7 +2006,7 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
       s_out->G = G;
       s_out->H = H;
       // replica check of the previous tree (data parallel; off the evaluation's critical path)
-      if (level == 0 && d.dig && blockIdx.x == 0 && blockIdx.y == 0) {
+      if (kDP && level == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
         int64_t dsum;
         if (kFused) {
           const int nc = kGroups ? d.hoff[fend] - d.hoff[fbeg] : d.ncells;
@@ -2095,12 +2021,13 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
   return true;
 }
 
-template <bool kGroups, bool kFused>
+template <bool kGroups, bool kFused, bool kDP>
 __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity, int tree, int fg, EvalSlots es) {
+  static_assert(kDP || !kFused, "the fused exchange is data parallel");
   BlockStamp stamp_(d);
   const int pos = blockIdx.x;
   __shared__ EvalOut s_out;
-  if (!eval_core<kGroups, kFused>(d, level, parity, tree, fg, es, pos, stamp_, &s_out)) {
+  if (!eval_core<kGroups, kFused, kDP>(d, level, parity, tree, fg, es, pos, stamp_, &s_out)) {
     // an owned node that is not active on its owner still publishes its record: a rank whose tree went
     // another way (replica divergence) and waits for it then learns so instead of timing out
     if (kFused && !kGroups && threadIdx.x == 0 && d.own_level >= 0 && level >= d.own_level) {
@@ -2122,13 +2049,14 @@ __global__ __launch_bounds__(1024) void k_eval(GbdtDev d, int level, int parity,
     o.hl = best.hl;
     return;
   }
-  eval_finalize(d, level, (1 << level) - 1 + pos, s_out.G, s_out.H, best, best_cut, s_out.nb);
+  eval_finalize<kDP>(d, level, (1 << level) - 1 + pos, s_out.G, s_out.H, best, best_cut, s_out.nb);
   if (kFused && d.own_level >= 0 && level >= d.own_level)  // the other ranks copy this node's decision
     own_publish(d, d.ipcv + (d.ipc_epoch & 1u), (1 << level) - 1 + pos);
   stamp_.probe(4);
 }
 
 // Reduce the per-group candidates of each node of the level (one wave per node, lane = group).
+template <bool kDP>
 __global__ __launch_bounds__(64) void k_eval_finish(GbdtDev d, int level, int parity, int ngroups) {
   BlockStamp stamp_(d);
   const int pos = blockIdx.x;
@@ -2156,191 +2084,7 @@ __global__ __launch_bounds__(64) void k_eval_finish(GbdtDev d, int level, int pa
     best_cut = c.cut;
   }
   wave_best(best, best_cut);
-  if (lane == 0) eval_finalize(d, level, n, G, H, best, best_cut);
-}
-
-// Compact split evaluation (F <= kEvalMaxF): the node's candidates are enumerated over its compact
-// histogram cells (sum of nbins: ~1.3k for the 20 deployed features, of which 8 are binary) instead of
-// F x 256 bin slots (5.1k), so the fp64 gain scan -- which made k_eval compute-bound on its single CU
-// (~6 us of the ~14 us per level) -- shrinks ~4x. Thread = kEvalCPT consecutive cells; a block-wide
-// int64 prefix scan over all cells, minus the prefix at each feature's first cell, gives every
-// candidate's left sums (cells are spread evenly, ceil(ncells / 1024) per thread, so all 16 waves
-// share the gain work). Gains, keys, tie-breaks and the finalisation are those of k_eval, so the
-// trees are bit-identical. Latency: one round trip for the node record + feature table, one for the
-// cells (+ the parent's for the subtraction) and their cut values, then LDS only.
-constexpr int kEvalThreads = 1024;
-constexpr int kEvalCPT = 8;        // cells per thread: ncells <= 8192
-constexpr int kEvalMaxF = 32;
-
-__global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int level, int parity, int tree) {
-  BlockStamp stamp_(d);
-  __shared__ int s_hoff[kEvalMaxF + 1];
-  __shared__ int s_nb[kEvalMaxF];
-  __shared__ int s_on[kEvalMaxF];
-  __shared__ int64_t s_wg[kEvalThreads / kWave], s_wh[kEvalThreads / kWave];
-  __shared__ int64_t s_bg[kEvalMaxF + 1], s_bh[kEvalMaxF + 1];  // prefix before each feature's first cell
-  __shared__ Cand s_best[kEvalThreads / kWave];
-  __shared__ float s_cut[kEvalThreads / kWave];
-  const int pos = blockIdx.x;
-  const int n = (1 << level) - 1 + pos;
-  const int F = d.F;
-  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const int64_t SE = d.slot_elems;
-  const int pair = level == 0 ? 0 : (pos >> 1);
-  const int64_t* hb = d.hist_b[parity] + pair * SE;
-  int64_t* hs = d.hist_s[parity] + (int64_t)pos * SE;  // this node's full histogram, for its children
-  // round trip 1: feature table (LDS) + node record (uniform)
-  if (t <= F) s_hoff[t] = d.hoff[t];
-  if (t < F) {
-    s_nb[t] = d.nbins[t];
-    s_on[t] = d.fmask[(int64_t)tree * F + t] != 0;
-  }
-  const Node* nodes = d.nodes;
-  const int status = nodes[n].status;
-  const bool built = nodes[n].build != 0;
-  // unconditional (in-bounds) loads selected after: one round trip, no per-load branch
-  const int64_t rg = hb[(int64_t)d.ncells * 2], rh = hb[(int64_t)d.ncells * 2 + 1];
-  const int64_t ng = nodes[n].G, nh = nodes[n].H;
-  const int64_t G = level == 0 ? rg : ng, H = level == 0 ? rh : nh;
-  if (status != kActive) return;  // uniform across the block
-  __syncthreads();
-  stamp_.probe(1);
-  const int nc = s_hoff[F];
-  const int cpt = (nc + kEvalThreads - 1) / kEvalThreads;  // cells per thread: every wave gets work
-  const int c0 = t * cpt;
-  // the parent's full histogram, stored by position by the previous level's evaluation
-  const int64_t* parent = level > 0 ? d.hist_s[parity ^ 1] + (int64_t)(pos >> 1) * SE : hb;
-  // feature of the thread's first cell (largest f with s_hoff[f] <= c0)
-  int f0 = 0;
-  {
-    int lo = 0, hi = F - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_hoff[mid] <= c0) lo = mid; else hi = mid - 1;
-    }
-    f0 = lo;
-  }
-  // round trip 2: cells, parent cells, cut values of the cells (and of the bin before the first one)
-  int64_t g[kEvalCPT], h[kEvalCPT];
-  float cut[kEvalCPT];
-  float cutm1 = -FLT_MAX;
-  {
-    int f = f0;
-#pragma unroll
-    for (int k = 0; k < kEvalCPT; ++k) {
-      const int c = c0 + k;
-      const bool in = k < cpt && c < nc;
-      while (f + 1 < F && s_hoff[f + 1] <= c) ++f;
-      const int b = c - s_hoff[f];
-      const int64_t bg = in ? hb[2 * c] : 0, bh = in ? hb[2 * c + 1] : 0;
-      const int64_t pg = (in && !built) ? parent[2 * c] : 0, ph = (in && !built) ? parent[2 * c + 1] : 0;
-      g[k] = built ? bg : pg - bg;
-      h[k] = built ? bh : ph - bh;
-      cut[k] = in ? d.cuts[f * kMaxBins + b] : FLT_MAX;
-    }
-    const int b0 = c0 - s_hoff[f0];
-    if (c0 < nc && b0 > 0) cutm1 = d.cuts[f0 * kMaxBins + b0 - 1];
-  }
-  if (level + 1 < d.max_depth) {  // this node's histogram, for its children's subtraction
-#pragma unroll
-    for (int k = 0; k < kEvalCPT; ++k) {
-      const int c = c0 + k;
-      if (k < cpt && c < nc) {
-        hs[2 * c] = g[k];
-        hs[2 * c + 1] = h[k];
-      }
-    }
-  }
-  // block-wide inclusive prefix scan of (g, h) over the cells; the per-cell prefixes are rebuilt from
-  // the thread's exclusive base where needed (fewer live registers than keeping them)
-  int64_t tg = 0, th = 0;
-#pragma unroll
-  for (int k = 0; k < kEvalCPT; ++k) { tg += g[k]; th += h[k]; }
-  const int64_t ig = wave_incl_scan(tg), ih = wave_incl_scan(th);
-  if (lane == kWave - 1) { s_wg[wv] = ig; s_wh[wv] = ih; }
-  __syncthreads();
-  int64_t bg = ig - tg, bh = ih - th;  // exclusive within the wave
-  for (int k = 0; k < wv; ++k) { bg += s_wg[k]; bh += s_wh[k]; }
-  // segment bases: the exclusive prefix at each feature's first cell, and the grand total
-  {
-    int f = f0;
-    int64_t rg = bg, rh = bh;
-#pragma unroll
-    for (int k = 0; k < kEvalCPT; ++k) {
-      const int c = c0 + k;
-      while (f + 1 < F && s_hoff[f + 1] <= c) ++f;
-      if (k < cpt && c < nc && c == s_hoff[f]) { s_bg[f] = rg; s_bh[f] = rh; }
-      rg += g[k];
-      rh += h[k];
-      if (k < cpt && c == nc - 1) { s_bg[F] = rg; s_bh[F] = rh; }
-    }
-  }
-  __syncthreads();
-  stamp_.probe(2);
-  const double Gd = (double)G * d.ginv, Hd = (double)H * d.hinv;
-  const double parent_gain = calc_gain(Gd, Hd, d.lambda_, d.alpha, d.mcw);
-  Cand best;
-  best.gain = -INFINITY;
-  best.key = 0x7fffffff;
-  best.gl = 0;
-  best.hl = 0;
-  float best_cut = -FLT_MAX;
-  {
-    int f = f0;
-    int64_t rg = bg, rh = bh;  // global inclusive prefix of the current cell
-#pragma unroll
-    for (int k = 0; k < kEvalCPT; ++k) {
-      const int c = c0 + k;
-      rg += g[k];
-      rh += h[k];
-      while (f + 1 < F && s_hoff[f + 1] <= c) ++f;
-      if (k >= cpt || c >= nc || !s_on[f]) continue;
-      const int b = c - s_hoff[f];
-      const int nb = s_nb[f];
-      const int64_t GLi = rg - s_bg[f], HLi = rh - s_bh[f];
-      const int64_t mg = G - (s_bg[f + 1] - s_bg[f]), mh = H - (s_bh[f + 1] - s_bh[f]);
-      // direction 0: missing -> right, left = bins <= b
-      {
-        const double gl = (double)GLi * d.ginv, hl = (double)HLi * d.hinv;
-        const double gr = (double)(G - GLi) * d.ginv, hr = (double)(H - HLi) * d.hinv;
-        if (hl >= d.mcw && hr >= d.mcw) {
-          Cand cd;
-          cd.gain = calc_gain_pair(gl, hl, gr, hr, d.lambda_, d.alpha) - parent_gain;
-          cd.key = f * 1024 + b;
-          cd.gl = GLi;
-          cd.hl = HLi;
-          if (cand_better(cd, best)) { best = cd; best_cut = cut[k]; }
-        }
-      }
-      // direction 1: missing -> left, left = bins <= b-1 (+ missing)
-      if (mg != 0 || mh != 0) {
-        const int64_t GL = GLi - g[k] + mg, HL = HLi - h[k] + mh;
-        const double gl = (double)GL * d.ginv, hl = (double)HL * d.hinv;
-        const double gr = (double)(G - GL) * d.ginv, hr = (double)(H - HL) * d.hinv;
-        if (hl >= d.mcw && hr >= d.mcw) {
-          Cand cd;
-          cd.gain = calc_gain_pair(gl, hl, gr, hr, d.lambda_, d.alpha) - parent_gain;
-          cd.key = f * 1024 + 512 + (nb - 1 - b);
-          cd.gl = GL;
-          cd.hl = HL;
-          if (cand_better(cd, best)) { best = cd; best_cut = b == 0 ? -FLT_MAX : (k == 0 ? cutm1 : cut[k - 1]); }
-        }
-      }
-    }
-  }
-  wave_best(best, best_cut);
-  if (lane == 0) { s_best[wv] = best; s_cut[wv] = best_cut; }
-  __syncthreads();
-  stamp_.probe(3);
-  if (wv != 0) return;
-  if (lane < kEvalThreads / kWave) { best = s_best[lane]; best_cut = s_cut[lane]; }
-  else { best.gain = -INFINITY; best.key = 0x7fffffff; best.gl = 0; best.hl = 0; best_cut = -FLT_MAX; }
-  wave_best(best, best_cut);
-  if (t != 0) return;
-  const int wf = best.key != 0x7fffffff ? (best.key >> 10) : 0;
-  if (level == 0) digest_check(d, hb[SE]);
-  eval_finalize(d, level, n, G, H, best, best_cut, s_nb[wf]);
-  stamp_.probe(4);
+  if (lane == 0) eval_finalize<kDP>(d, level, n, G, H, best, best_cut);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2353,14 +2097,10 @@ __global__ __launch_bounds__(kEvalThreads) void k_eval_compact(GbdtDev d, int le
 // with one atomic pair per item, pass 2 scatters with ballot ranks -- rows are read once.
 // Left rows keep their relative order inside an item; only whole items interleave, so a node's
 // row list stays sorted in 8192-row runs (the root level reads rows in identity order).
-// Block size is a template parameter: the per-item cursor claim is a pair of same-address
-// device-scope atomics, whose latency/serialisation across the 8 XCDs dominates a level when items
-// are many and small (measured: removing the claims took a 10M-row level from 58 to 24 us). The
-// default is 1024-thread blocks (16 waves x 8 steps per 8192-row item, 4096-row items while they fit
-// one per CU; see part_wide / chunk_part); 256-thread blocks (COBALT_PART_WIDE=0) were the large-row
-// shape until round 3.
-constexpr int kPartSteps = 32;  // 64-row steps per wave (maximum; see k_partition's kSteps)
-
+// The per-item cursor claim is a pair of same-address device-scope atomics, whose latency /
+// serialisation across the 8 XCDs dominates a level when items are many and small (measured: removing
+// the claims took a 10M-row level from 58 to 24 us); hence 1024-thread blocks (16 waves x 8 steps per
+// 8192-row item, 4096-row items while they fit one per CU; see chunk_part).
 // kSteps: 64-row steps per wave, sized by the host to the item (chunk <= kPartWaves * kSteps * 64):
 // steps past the item would still issue their (unconditional) bin loads and ballots.
 template <int kPartWaves, int kSteps>
@@ -2498,64 +2238,39 @@ __device__ __forceinline__ bool split_decision(const GbdtDev& d, const Cand& bes
   return ok;
 }
 
-// Data-parallel form (kDP, the fused IPC exchange): only the node's FIRST block (its lead) evaluates:
-// it waits for the ranks, sums their cells (eval_core<kFused>), finalises the node and publishes the
-// decision {tag, ok, default direction, feature, bin} as ONE 8-byte write-through granule; the node's
-// other blocks poll that granule (their row ids are loaded meanwhile). Reading every rank's cells in
-// every block would multiply the xGMI traffic by the node's item count. Forward progress: a waiting
-// block only waits for a lower-indexed block of the same launch, and the host launches this form only
-// while the whole grid is resident at once (items + nodes <= CUs, one 1024-thread block per CU), so
-// the lead is running or done. Every active node gets at least one (possibly empty) item, so each
-// rank finalises every node of the level, also those it holds no rows of. Block 0 publishes this
-// rank's slot before its plan (every epoch, whatever the level holds).
-typedef __attribute__((address_space(1))) unsigned long long gu64;  // global (not flat) accesses
-
-__device__ __forceinline__ uint64_t part_decision_word(uint32_t tag, bool ok, bool fail, int f, int j, bool dl) {
-  const uint32_t v = (ok ? 1u : 0u) | (fail ? 2u : 0u) | (dl ? 4u : 0u) | ((uint32_t)f & 0xFFu) << 8 |
-                     ((uint32_t)(j + 1) & 0x3FFu) << 16;
-  return ((uint64_t)tag << 32) | v;
-}
-
-// kMode: 0 = one GPU; 1 = data parallel with the level's global histograms already in hist_b (RCCL /
-// separate IPC exchange): every block evaluates, every active node gets an item; 2 = data parallel
-// over the fused IPC exchange: the lead-decides form above.
-template <int kSteps, int kMode>
+// kDP: data parallel with the level's global histograms already in hist_b (RCCL / the separate IPC
+// exchange kernel): every active node gets an item (possibly empty), so each rank finalises every node
+// of the level, also those it holds no rows of; the replica digest is kept.
+template <int kSteps, bool kDP>
 __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64_t zero_next, int level, int chunk,
-                                                    int tree, EvalSlots es, uint32_t tag) {
+                                                    int tree, EvalSlots es) {
   constexpr int kPW = 16;  // waves
   BlockStamp stamp_(d);
   __shared__ int32_t s_cnt[2][kPW];
   __shared__ int32_t s_base[2];
   __shared__ EvalOut s_out;
-  __shared__ uint32_t s_dec;
   {  // zero the next level's reduce destination (hist_b of the other parity, or the next IPC send slot)
     int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
     const int64_t nz = zero_next / 2;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
   }
-  constexpr bool kDP = kMode == 2;
-  if (kDP && blockIdx.x == 0) ipc_publish(d.ipcv[d.ipc_epoch & 1u].myflag, d.ipc_epoch);
   const int item = blockIdx.x;
   const int first = (1 << level) - 1;
-  // this block's item: the root's rows are fixed slices; deeper levels' items were laid out by the
-  // histogram pass (ep_plan) -- both loads in one round trip
+  // this block's item: the root's rows are fixed slices; deeper levels' items are planned by every
+  // block (block_plan over the level's node table)
   PlanOut pl;
   __shared__ int s_plan[5];
   if (level == 0) {
     const int n = (int)d.n, b = item * chunk;
-    const int items = max((n + chunk - 1) / chunk, kMode != 0 ? 1 : 0);
+    const int items = max((n + chunk - 1) / chunk, kDP ? 1 : 0);
     pl = PlanOut{item < items ? 0 : -1, 0, min(b, n), min(n, b + chunk), items};
-  } else if (!d.ep_plan) {
-    pl = block_plan<kMode != 0>(1 << level, chunk, item, [&](int e) {
+  } else {
+    pl = block_plan<kDP>(1 << level, chunk, item, [&](int e) {
       const Node& n = d.nodes[first + e];
       const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
-      return (st != kNone && (kMode != 0 || cnt > 0)) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
+      return (st != kNone && (kDP || cnt > 0)) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
     }, s_plan);
-  } else {
-    const int4 it = d.ep_items[item];
-    const int tot = d.counters[1];
-    pl = PlanOut{item < tot ? it.x : -1, 0, it.y, it.z, tot};
   }
   if (pl.node < 0) return;
   const int node = pl.node;
@@ -2580,59 +2295,14 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   const int nstart = d.nodes[node].start, ncount = d.nodes[node].count;
   const bool lead = pl.begin == nstart;  // the node's first item
   int f, j;
-  bool dlb, ok;
-  if (!kDP) {  // every block evaluates its node itself (local histograms: L2-hot, no waiting)
-    load_rows();
-    eval_core<false, false, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, lead);
-    __syncthreads();
-    const Cand best = s_out.best;
-    ok = split_decision(d, best, s_out.nb, f, j, dlb);
-    if (lead && threadIdx.x == 0) eval_finalize(d, level, node, s_out.G, s_out.H, best, s_out.cut, s_out.nb);
-  } else {
-    uint64_t* dec = reinterpret_cast<uint64_t*>(d.dec) + node;
-    if (lead) {
-      const bool good = eval_core<false, true, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, true);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        int ff = 0, jj = -1;
-        bool dd = false, oo = false;
-        if (good) {
-          oo = split_decision(d, s_out.best, s_out.nb, ff, jj, dd);
-          eval_finalize(d, level, node, s_out.G, s_out.H, s_out.best, s_out.cut, s_out.nb);
-        }
-        const uint64_t w = part_decision_word(tag, oo, !good, ff, jj, dd);
-        __hip_atomic_store((gu64*)dec, (unsigned long long)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_dec = (uint32_t)w;
-      }
-    } else {
-      load_rows();
-    }
-    if (!lead && threadIdx.x == 0) {  // poll the lead's granule (one lane), bounded by the group's deadline
-      const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      uint32_t v = 2u;  // failed unless the lead's word arrives
-      for (;;) {
-        const uint64_t w = __hip_atomic_load((gu64*)dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(w >> 32) == tag) { v = (uint32_t)w; break; }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > iv->timeout) {
-          __hip_atomic_store(iv->myflag + kIpcStickyWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(iv->err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      s_dec = v;
-    }
-    __syncthreads();
-    const uint32_t v = s_dec;
-    if (v & 2u) return;  // the exchange failed (the host watchdog reports it)
-    // the lead loads its row ids after its evaluation: held across it, they spilled
-    if (lead) load_rows();
-    ok = (v & 1u) != 0;
-    dlb = (v & 4u) != 0;
-    f = (int)((v >> 8) & 0xFFu);
-    j = (int)((v >> 16) & 0x3FFu) - 1;
-  }
+  bool dlb;
+  // every block evaluates its node itself (the histograms are L2-hot; the row ids are in flight)
+  load_rows();
+  eval_core<false, false, kDP, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, lead);
+  __syncthreads();
+  const Cand best = s_out.best;
+  const bool ok = split_decision(d, best, s_out.nb, f, j, dlb);
+  if (lead && threadIdx.x == 0) eval_finalize<kDP>(d, level, node, s_out.G, s_out.H, best, s_out.cut, s_out.nb);
   stamp_.probe(4);
   if (!ok || len == 0) return;  // a leaf (its rows are not routed) or an empty item (block-uniform)
   const uint8_t* col = d.binsT + (int64_t)f * d.ldt;
@@ -2685,152 +2355,6 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
 }
 
 // ------------------------------------------------------------------------------------------
-// Fused row partition of level L + histogram of level L + 1 (32-byte records, one feature tile).
-// The pass that routes the rows of level L's split nodes to their children also builds, from the
-// same rows, the histogram of the child k_eval chose to build (smaller global hessian), so that
-// child's rows are never re-read through ridx by a separate histogram launch, and the record
-// gathers are issued while the block's cursor claim is in flight. Both cursors of a node are
-// claimed with ONE 64-bit atomic: same-address device atomics serialise at the memory side
-// (~88 per us per word), which bounded the shallow levels, where every item claims on one node.
-// Work item = <= kPW * kPS * 64 rows of one parent node; its partial histogram goes to the item's
-// slab row with slot = the parent's position in level L (= the child pair's slot in level L + 1).
-// ------------------------------------------------------------------------------------------
-constexpr int kPartHistWaves = 8, kPartHistSteps = 16;
-constexpr int kPartHistRows = kPartHistWaves * kPartHistSteps * kWave;  // 8192 rows per work item
-
-template <int kPW, int kPS>
-__global__ __launch_bounds__(kPW * 64) void k_part_hist(GbdtDev d, int parity, int64_t zero_next, int level,
-                                                        int chunk, int tree) {
-  BlockStamp stamp_(d);
-  extern __shared__ uint64_t s_hist[];
-  __shared__ int32_t s_cnt[2][kPW];
-  __shared__ int32_t s_base[2];
-  __shared__ int s_plan[5];
-  __shared__ int64_t s_tot[2][16];
-  static_assert(kPS <= 32 && kPS % 4 == 0, "step bit masks are 32-bit; hist pipeline of 4 steps");
-  {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
-    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
-    const int64_t nz = zero_next / 2;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
-      zp[e] = make_int4(0, 0, 0, 0);
-  }
-  const int item = blockIdx.x;
-  const int first = (1 << level) - 1;
-  const PlanOut pl = block_plan(1 << level, chunk, item, [&](int e) {
-    const Node& n = d.nodes[first + e];
-    const int st = n.status, cnt = n.count, start = n.start;  // loaded together (no per-load branch)
-    return (st == kSplit && cnt > 0) ? PlanEntry{first + e, 0, start, cnt} : PlanEntry{-1, 0, 0, 0};
-  }, s_plan);
-  if (item == 0 && threadIdx.x == 0) d.counters[0] = pl.total;  // work items of the next level's reduce
-  if (pl.node < 0) return;
-  const int q = pl.node;
-  const Node nd = d.nodes[q];
-  const bool build_left = d.nodes[2 * q + 1].build != 0;
-  if (threadIdx.x == 0) {
-    WorkItem w;
-    w.node = build_left ? 2 * q + 1 : 2 * q + 2;
-    w.slot = q - first;
-    w.begin = pl.begin;
-    w.end = pl.end;
-    d.items_h[item] = w;
-  }
-  const int F = d.F;
-  const int entries = d.tile_entries[0] + kWave;  // + per-lane trash cells
-  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
-  const HistLaneRaw lraw = hist_lanes_load(d, tree, 0, F);
-  __shared__ int s_fo[kMaxFeatTile + 1], s_fs[kMaxFeatTile];
-  __shared__ uint32_t s_fm[kWave];
-  flush_meta_store(flush_meta_load(d, tree, 0, F), F, s_fo, s_fs);  // published by the barrier below
-  hist_meta_store(lraw, s_fm);
-
-  // pass 1: row ids + split-feature bins -> directions and per-wave counts (rows stay in registers)
-  const bool identity = parity == 0 && q == 0;
-  const int32_t* cur = d.ridx[parity];
-  int32_t* nxt = d.ridx[parity ^ 1];
-  const uint8_t* col = d.binsT + (int64_t)nd.feat * d.ldt;
-  const int j = nd.bin;
-  const bool dl = nd.default_left != 0;
-  const int wv = wave_id(), lane = lane_id();
-  const int len = pl.end - pl.begin;
-  const int per = ((len + kPW - 1) / kPW + kWave - 1) / kWave * kWave;
-  const int wb = min(pl.end, pl.begin + wv * per), we = min(pl.end, wb + per);
-  int r[kPS];
-  uint32_t lbits = 0, vbits = 0;
-  int nl = 0, nr = 0;
-#pragma unroll
-  for (int k = 0; k < kPS; ++k) {
-    const int i = wb + k * kWave + lane;
-    r[k] = i < we ? (identity ? i : cur[i]) : -1;
-  }
-  uint8_t bv[kPS];  // unconditional loads: all in flight at once (see k_partition)
-#pragma unroll
-  for (int k = 0; k < kPS; ++k) bv[k] = col[max(r[k], 0)];
-#pragma unroll
-  for (int k = 0; k < kPS; ++k) {
-    const bool valid = r[k] >= 0;
-    const bool left = valid && (bv[k] == kMissingBin ? dl : ((int)bv[k] <= j));
-    lbits |= (uint32_t)left << k;
-    vbits |= (uint32_t)valid << k;
-    const uint64_t lm = __ballot(left), vm = __ballot(valid);
-    nl += __popcll(lm);
-    nr += __popcll(vm) - __popcll(lm);
-  }
-  if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nr; }
-  __syncthreads();  // (also orders the LDS histogram zeroing before the atomics below)
-  const HistLanes hl = hist_lanes_finish(lraw, F, s_fm);
-  unsigned long long claim = 0;
-  if (threadIdx.x == 0) {
-    int tl = 0, tr = 0;
-    for (int k = 0; k < kPW; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
-    claim = atomicAdd(reinterpret_cast<unsigned long long*>(d.cursors + 2 * q),
-                      ((unsigned long long)(uint32_t)tr << 32) | (uint32_t)tl);
-  }
-  // pass 2 (while the claim is in flight): histogram of the build side from the records.
-  // Loads are unconditional (non-build lanes read row 0, a broadcast) so the compiler keeps all
-  // four rows of a step group in flight; only the LDS atomics are predicated.
-  const uint32_t want = build_left ? lbits : (vbits & ~lbits);
-  int64_t tg = 0, th = 0;
-  constexpr int U = 4;
-#pragma unroll
-  for (int k0 = 0; k0 < kPS; k0 += U) {
-    uint4 a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int rk = ((want >> (k0 + u)) & 1u) ? r[k0 + u] : 0;
-      const uint4* rec = reinterpret_cast<const uint4*>(d.bins + (int64_t)rk * 32);
-      a[u] = rec[0];
-      b[u] = rec[1];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if ((want >> (k0 + u)) & 1u) {
-        tg += (int64_t)(int32_t)b[u].w;
-        th += (int64_t)b[u].z;
-        hist_add_rec32<24>(s_hist, hl, a[u], b[u]);
-      }
-    }
-  }
-  if (threadIdx.x == 0) { s_base[0] = (int32_t)(uint32_t)claim; s_base[1] = (int32_t)(claim >> 32); }
-  __syncthreads();  // claim published; every histogram atomic of the block has completed
-  // pass 3: scatter (left ascending from the node start, right descending from its end)
-  int bl = s_base[0], br = s_base[1];
-  for (int k = 0; k < wv; ++k) { bl += s_cnt[0][k]; br += s_cnt[1][k]; }
-  const int rend = nd.start + nd.count - 1;
-#pragma unroll
-  for (int k = 0; k < kPS; ++k) {
-    const bool valid = (vbits >> k) & 1u, left = (lbits >> k) & 1u;
-    const uint64_t lm = __ballot(valid && left), rm = __ballot(valid && !left);
-    if (valid) {
-      if (left) nxt[nd.start + bl + mask_rank(lm)] = r[k];
-      else nxt[rend - (br + mask_rank(rm))] = r[k];
-    }
-    bl += __popcll(lm);
-    br += __popcll(rm);
-  }
-  hist_flush(d, s_hist, hl, item, 0, F, tg, th, true, s_tot, s_fo, s_fs);
-}
-
-// ------------------------------------------------------------------------------------------
 // Host-side trainer context
 // ------------------------------------------------------------------------------------------
 // RCCL all-reduce hook implemented in comm.cpp
@@ -2850,7 +2374,6 @@ struct GbdtCtx {
   EvalSlots eval_slots{};  // the table with each slot's bin count and compact offset (k_eval<false> arguments)
   std::vector<int32_t> hoff_h;  // host copy of d.hoff (sizes k_eval's fused-exchange LDS)
   int fit_first = 0;            // first tree this context grows in the current fit (no replica check)
-  uint32_t dec_tag = 0;         // k_eval_part<mode 2> decision-granule tag (one per launch)
   int fault_tree = -1;          // fault injection: tree whose root totals are perturbed on this rank
   unsigned* err_pinned = nullptr;  // mapped host word behind d.err_host
   // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
@@ -2933,8 +2456,8 @@ static int pow2_clamp(int64_t v, int lo, int hi) {
 // levels histogram at most ~N/2 rows -> aim for ~1536 items; partition items cover all split rows.
 static int chunk_hist(const GbdtDev& d, int level) {
   // COBALT_HIST_CHUNK0 / COBALT_HIST_CHUNK override the root / deeper item sizes (tuning experiments)
-  static const int env0 = getenv("COBALT_HIST_CHUNK0") ? atoi(getenv("COBALT_HIST_CHUNK0")) : 0;
-  static const int env1 = getenv("COBALT_HIST_CHUNK") ? atoi(getenv("COBALT_HIST_CHUNK")) : 0;
+  static const int env0 = knob_int(Knob::HistChunk0, 0);
+  static const int env1 = knob_int(Knob::HistChunk, 0);
   if (level == 0) return env0 > 0 ? std::min(16384, std::max(512, env0)) : d.chunk;
   if (env1 > 0) return std::min(16384, std::max(512, env1));
   // <= 4096 rows: with the reduce at ~3 us per level, more, smaller items balance the CUs better
@@ -2943,24 +2466,17 @@ static int chunk_hist(const GbdtDev& d, int level) {
   // 72.6 ms), 2048 up to ~3.1M (2.5M: 102.8 -> 100.4 ms vs 4096), 4096 above (5M: 1024 / 2048 slower)
   return pow2_clamp((d.n / 2 + 767) / 768, 1024, 4096);
 }
-// Partition item size and block shape (see k_partition); COBALT_PART_CHUNK overrides the size.
-// 16-wave blocks at every size (COBALT_PART_WIDE=0: 4-wave blocks, read when a context is created):
-// 10M rows 234.7 -> 230.6 ms, 7.5M 191.8 -> 188.6, 5M 150.2 -> 147.3 against 4-wave blocks above 4M
-// rows (profiles/round3/ab/ab_part_wide.txt); 4-wave blocks won at 10M in round 2, before the
-// partition passes went to integer arithmetic
-static int env_part_wide() { return getenv("COBALT_PART_WIDE") ? (atoi(getenv("COBALT_PART_WIDE")) != 0) : 1; }
-static bool part_wide(const GbdtDev& d) { return d.pwide != 0; }
+// Partition item size (16-wave blocks, see k_partition); COBALT_PART_CHUNK overrides it (<= 8192).
+// (16-wave blocks at every size: 10M rows 234.7 -> 230.6 ms, 5M 150.2 -> 147.3 against the 4-wave
+// blocks of rounds 1-2, profiles/round3/ab/ab_part_wide.txt; the 4-wave form is gone since round 5)
 static int device_cu_count();
 static int chunk_part(const GbdtDev& d) {
-  static const int env = getenv("COBALT_PART_CHUNK") ? atoi(getenv("COBALT_PART_CHUNK")) : 0;
-  const int cap = (part_wide(d) ? 16 : 4) * kPartSteps * kWave;
-  if (env > 0) return std::min(cap, std::max(1024, env / 1024 * 1024));
-  // wide (16-wave) blocks: 4096-row items while a level's items fit one block per CU (1M rows: 104.7
-  // vs 106.8 ms per fit with 8192 in round 1), else 8192 (1.25M: 4096-row items ran 306 blocks on 256
-  // CUs; 8192: 82.1 -> 79.5 ms, 2.5M 105.5 -> 104.1; 16384 slower at both; at 10M 4096 / 6144 / 12288 /
-  // 16384 243.0 / 234.8 / 256.0 / 250.6 vs 231.4 ms); narrow blocks keep 8192
-  // (10M rows: 4096 measured 318.6 vs 304.8 ms)
-  if (!part_wide(d)) return 8192;
+  static const int env = knob_int(Knob::PartChunk, 0);
+  if (env > 0) return std::min(16 * 8 * kWave, std::max(1024, env / 1024 * 1024));
+  // 4096-row items while a level's items fit one block per CU (1M rows: 104.7 vs 106.8 ms per fit with
+  // 8192 in round 1), else 8192 (1.25M: 4096-row items ran 306 blocks on 256 CUs; 8192: 82.1 -> 79.5 ms,
+  // 2.5M 105.5 -> 104.1; 16384 slower at both; at 10M 4096 / 6144 / 12288 / 16384 243.0 / 234.8 / 256.0
+  // / 250.6 vs 231.4 ms)
   return (d.n + 4095) / 4096 <= device_cu_count() ? 4096 : 8192;
 }
 
@@ -2982,20 +2498,7 @@ static HistKernel hist_kernel(int ft4, bool pair) {
     default: return k_hist<0, false>;
   }
 }
-static bool grad_w6() {  // the 3-blocks-per-CU root pass (COBALT_GRAD_W6=1)
-  static const int v = getenv("COBALT_GRAD_W6") ? atoi(getenv("COBALT_GRAD_W6")) : 0;
-  return v != 0;
-}
 static GradHistKernel grad_hist_kernel(int ft4) {
-  if (grad_w6()) switch (ft4) {
-    case 4: return k_grad_hist_w6<4>;
-    case 8: return k_grad_hist_w6<8>;
-    case 12: return k_grad_hist_w6<12>;
-    case 16: return k_grad_hist_w6<16>;
-    case 20: return k_grad_hist_w6<20>;
-    case 24: return k_grad_hist_w6<24>;
-    default: return nullptr;
-  }
   switch (ft4) {
     case 4: return k_grad_hist<2, 4>;
     case 8: return k_grad_hist<2, 8>;
@@ -3017,8 +2520,8 @@ static int device_cu_count() {
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
       n = v;
     if (n <= 0) n = 256;
-    const char* b = getenv("COBALT_CU_BUDGET");
-    if (b && atoi(b) > 0) n = std::min(n, atoi(b));
+    const int b = knob_int(Knob::CuBudget, 0);
+    if (b > 0) n = std::min(n, b);
   }
   return n;
 }
@@ -3045,7 +2548,6 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
     GbdtDev tmp{};
     tmp.n = N;
     tmp.chunk = cfg->chunk;
-    tmp.pwide = env_part_wide();
     const int ch = std::min(chunk_hist(tmp, 0), chunk_hist(tmp, 1));
     c->items_cap = std::max(ceil_div(N, ch), ceil_div(N, chunk_part(tmp))) + (1 << cfg->max_depth) + 8;
   }
@@ -3072,23 +2574,18 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.ginv = 1.0 / cfg->gscale;
   d.hinv = 1.0 / cfg->hscale;
   d.seed = cfg->seed;
-  d.ablate = getenv("COBALT_HIST_ABLATE") ? atoi(getenv("COBALT_HIST_ABLATE")) : 0;
-  d.pwide = env_part_wide();
-  // one planner block in k_hist + the item list in memory measured slower than every k_eval_part block
-  // planning for itself (same box, 1M rows: 78.1 vs 73.9 ms per fit; 1.25M: 80.8 vs 78.0; 10M: 229.6 vs 229.3)
-  d.ep_plan = getenv("COBALT_EP_PLAN") ? atoi(getenv("COBALT_EP_PLAN")) : 0;
+  d.ablate = knob_int(Knob::HistAblate, 0);
   // write-through slabs always (10M rows: reduce gaps 14.2 -> 12.0 us per tree, fit 243.7 -> 243.2 ms); write-through
   // row ids below 4M rows only (1M: 240.2 -> 237.4 us per tree with both; at 10M the partition itself
   // slows 210 -> 228 us per tree for 10 us of shorter histogram gaps). COBALT_WT overrides.
-  d.wt = getenv("COBALT_WT") ? atoi(getenv("COBALT_WT")) : (N < 4000000 ? 3 : 1);
+  d.wt = knob_int(Knob::WriteThrough, N < 4000000 ? 3 : 1);
   // Data parallel: every rank histograms the child with the smaller GLOBAL hessian (k_eval's choice,
-  // identical on all ranks), so the level's all-reduce sums the same child everywhere and no
-  // per-level local-left conversion (k_dp_local) is needed. On one GPU the locally smaller row
-  // count is the default (+2% histogram time otherwise); COBALT_BUILD_BY_HESS forces the hessian rule.
-  d.by_hess = (getenv("COBALT_BUILD_BY_HESS") || cfg->comm) ? 1 : 0;
+  // identical on all ranks), so the level's all-reduce sums the same child everywhere. On one GPU the
+  // locally smaller row count (+2% histogram time with the hessian rule).
+  d.by_hess = cfg->comm ? 1 : 0;
   // lane-pair record gathers in the histogram levels (16 < F <= 24): default on (10M rows: 260.4 ->
   // 252.0 ms per fit, 1M: 90.9 -> 87.9 ms); COBALT_HIST_PAIR=0 selects the one-lane-per-row kernel
-  d.hist_pair = getenv("COBALT_HIST_PAIR") ? atoi(getenv("COBALT_HIST_PAIR")) : 1;
+  d.hist_pair = knob_int(Knob::HistPair, 1);
   c->lds_hist = (size_t)cfg->feat_tile * kMaxBins * sizeof(uint64_t);
   int rc = 0;
   const size_t hist_bytes = (size_t)c->pairs_max * d.slot_elems * sizeof(int64_t);
@@ -3108,12 +2605,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.counters, 16 * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cursors, 2 * c->max_nodes * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.cand, (size_t)c->pairs_max * 64 * sizeof(CandRec)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&d.dec, c->max_nodes * sizeof(uint64_t)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&d.ep_items, c->items_cap * sizeof(int4)))) return rc;
-  CK(hipMemset(d.dec, 0, c->max_nodes * sizeof(uint64_t)));
-  if (cfg->comm) {  // local histograms of every node of a level (positions 0 .. 2^(max_depth-1))
-    for (int k = 0; k < 2; ++k)
-      if ((rc = dev_alloc(c, (void**)&d.hist_loc[k], 2 * hist_bytes))) return rc;
+  if (cfg->comm) {
     // replica check: per-tree-parity digest accumulators and the mapped host error word
     if ((rc = dev_alloc(c, (void**)&d.dig, 4 * sizeof(int64_t)))) return rc;
     CK(hipMemset(d.dig, 0, 4 * sizeof(int64_t)));
@@ -3130,8 +2622,8 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.tile_entries, ntiles * sizeof(int32_t)))) return rc;
   d.stamps = nullptr;
   d.seq = 0;
-  if (getenv("COBALT_STAMPS")) {
-    c->stamp_path = getenv("COBALT_STAMPS");
+  if (knob_str(Knob::Stamps)) {
+    c->stamp_path = knob_str(Knob::Stamps);
     c->stamp_cap = 512;
     if ((rc = dev_alloc(c, (void**)&c->stamp_buf, (size_t)c->stamp_cap * kStampBlocks * kStampSlot * sizeof(uint64_t))))
       return rc;
@@ -3145,15 +2637,12 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
 // still has a free slot (wave w runs on SIMD w mod 4), on its least-loaded wave. The 20 deployed
 // features by index order put 11 chunk steps on one SIMD (mean 6.5); the table evens that out. The
 // candidate keys, not the wave, order ties: the trees do not depend on the table.
-// COBALT_EVAL_ASSIGN=0 restores the index-order assignment (feature f on wave f mod 16, slot f / 16).
+// (index order -- feature f on wave f mod 16 -- measured 57.2 vs 51.7 us of k_eval per tree at 1M.)
 static void eval_assignment(const std::vector<int32_t>& nb, uint64_t out[4]) {
   const int F = (int)nb.size();
   uint8_t slot[32];
   memset(slot, 0xFF, sizeof(slot));
-  const bool lpt = !(getenv("COBALT_EVAL_ASSIGN") && atoi(getenv("COBALT_EVAL_ASSIGN")) == 0);
-  if (F <= 32 && !lpt) {
-    for (int f = 0; f < F; ++f) slot[(f % 16) * 2 + f / 16] = (uint8_t)f;
-  } else if (F <= 32) {
+  if (F <= 32) {
     std::vector<int> order(F), steps(F);
     for (int f = 0; f < F; ++f) {
       order[f] = f;
@@ -3208,7 +2697,7 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   // flush sums half as many copies as 64 (10M: 253.4 -> 250.3 ms per fit, 1M: 87.1 -> 85.7). At most
   // 16 since round 3 -- same-address collisions of 4 lanes traded for a quarter of the flush work (two same-box rounds at 1 / 1.25 / 2.5 / 10M rows: 0.3-0.8 ms per fit faster each,
   // profiles/round3/ab/ab_copy_shift4.txt). COBALT_MAX_COPY_SHIFT overrides the log2 (0..6).
-  const int max_sh = getenv("COBALT_MAX_COPY_SHIFT") ? std::min(6, std::max(0, atoi(getenv("COBALT_MAX_COPY_SHIFT")))) : 4;
+  const int max_sh = std::min(6, std::max(0, knob_int(Knob::MaxCopyShift, 4)));
   int max_ent = 0;
   for (int t = 0; t < ntiles; ++t) {
     int off = 0;
@@ -3245,8 +2734,6 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
     for (int pair = 0; pair < 2; ++pair)
       CK(hipFuncSetAttribute((const void*)hist_kernel(hist_ft4(c->d), pair != 0),
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
-    CK(hipFuncSetAttribute((const void*)k_part_hist<kPartHistWaves, kPartHistSteps>,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
   const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
   if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d)))
@@ -3255,14 +2742,14 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   return 0;
 }
 
-static void launch_eval_part(int steps, int mode, dim3 grid, size_t lds, hipStream_t stream, const GbdtDev& d, int parity,
-                             int64_t zero_next, int level, int chunk, int tree, const EvalSlots& es, uint32_t tag) {
+static void launch_eval_part(int steps, bool dp, dim3 grid, hipStream_t stream, const GbdtDev& d, int parity,
+                             int64_t zero_next, int level, int chunk, int tree, const EvalSlots& es) {
 #define EP_LAUNCH(S, M) \
-  hipLaunchKernelGGL((k_eval_part<S, M>), grid, dim3(1024), lds, stream, d, parity, zero_next, level, chunk, tree, es, tag)
+  hipLaunchKernelGGL((k_eval_part<S, M>), grid, dim3(1024), 0, stream, d, parity, zero_next, level, chunk, tree, es)
   if (steps <= 4) {
-    if (mode == 0) EP_LAUNCH(4, 0); else if (mode == 1) EP_LAUNCH(4, 1); else EP_LAUNCH(4, 2);
+    if (dp) EP_LAUNCH(4, true); else EP_LAUNCH(4, false);
   } else {
-    if (mode == 0) EP_LAUNCH(8, 0); else if (mode == 1) EP_LAUNCH(8, 1); else EP_LAUNCH(8, 2);
+    if (dp) EP_LAUNCH(8, true); else EP_LAUNCH(8, false);
   }
 #undef EP_LAUNCH
 }
@@ -3296,27 +2783,16 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   }
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const int ft4 = hist_ft4(d);
-  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.ablate == 0 || d.ablate >= 10) &&
-                         getenv("COBALT_NO_FUSED_ROOT") == nullptr;
+  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.ablate == 0 || d.ablate >= 10);
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
-  static const int env_fg = getenv("COBALT_EVAL_FG") ? atoi(getenv("COBALT_EVAL_FG")) : -1;
+  static const int env_fg = knob_int(Knob::EvalFg, -1);
   int eval_fg = env_fg >= 0 ? env_fg : (d.F > 32 ? 8 : 0);
   if (eval_fg == 0 && d.F > 32) eval_fg = 8;  // one k_eval block evaluates at most 32 features
   if (eval_fg > 0) eval_fg = std::min(32, std::max(eval_fg, ceil_div(d.F, 64)));
-  // compact-cell evaluation for narrow data (COBALT_EVAL_COMPACT=1; default: the F x 256-slot k_eval)
-  // Opt-in: measured 14.2 vs 13.5 us per node-level at 1M rows and 106 vs 109 us per tree at 10M
-  // (the fp64 gain scan is not what bounds k_eval; its dependent LDS / shuffle / sync steps are).
-  const int env_compact = getenv("COBALT_EVAL_COMPACT") ? atoi(getenv("COBALT_EVAL_COMPACT")) : 0;
-  const bool eval_compact = eval_fg == 0 && env_compact != 0 && d.F <= kEvalMaxF &&
-                            d.ncells <= kEvalThreads * kEvalCPT;
-  // partition fused with the next level's histogram (same record-layout conditions); opt-in while it
-  // measures slower than the separate passes (COBALT_FUSED_PART=1)
-  const bool env_fuse_part = getenv("COBALT_FUSED_PART") != nullptr && atoi(getenv("COBALT_FUSED_PART")) != 0;
-  const bool fuse_part = fuse_root && env_fuse_part;
   // IPC exchange fused into the split evaluation (k_eval publishes, waits and sums the ranks' slots
   // itself: one launch per level fewer); COBALT_IPC_FUSED=0 keeps the separate exchange kernel
-  const int env_ipc_fused = getenv("COBALT_IPC_FUSED") ? atoi(getenv("COBALT_IPC_FUSED")) : 1;
+  const int env_ipc_fused = knob_int(Knob::IpcFused, 1);
   // LDS of the fused k_eval: the block's cells (+ the totals cell) summed over the ranks
   int fused_cells = c->d.ncells;
   if (eval_fg > 0) {
@@ -3325,58 +2801,47 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       fused_cells = std::max(fused_cells, c->hoff_h[std::min(d.F, f0 + eval_fg)] - c->hoff_h[f0]);
   }
   const size_t fused_lds = (size_t)(fused_cells + 2) * 16;  // + the totals and the level-0 digest cells
-  const bool ipc_fused = ipc && env_ipc_fused != 0 && !eval_compact && !fuse_part && fused_lds <= 65536;
+  const bool ipc_fused = ipc && env_ipc_fused != 0 && fused_lds <= 65536;
   d.ipc_epoch = 0;
   d.ipcv = ipc_fused ? ipc_device_views(cc) : nullptr;
   // split evaluation fused into the partition pass (k_eval_part): one launch per level fewer, but every
   // partition block repeats its node's evaluation, so only while the level's items fit one block per CU
   // (1M rows: 248.0 -> 239.3 us per tree in the stamps; 1.25M: 87.0 -> 96.3 ms per fit, 2.5M 112 -> 130:
-  // two evaluations per CU). COBALT_EVAL_PART=0 / 2 disables / forces it.
-  static const int env_ep = getenv("COBALT_EVAL_PART") ? atoi(getenv("COBALT_EVAL_PART")) : 1;
+  // two evaluations per CU). COBALT_EVAL_PART=0 / 2 disables / forces it. Under data parallelism it needs
+  // the level's global histograms in hist_b before it runs (RCCL, or the separate IPC exchange kernel);
+  // the fused IPC exchange evaluates in k_eval (one block per node; node ownership on the deep levels).
+  static const int env_ep = knob_int(Knob::EvalPart, 1);
   const int ep_steps = ceil_div(chunk_part(d), 16 * kWave);
-  // data parallel: every block evaluating from the all-reduced hist_b (mode 1: RCCL / the separate
-  // IPC exchange: +0.9 us per level over one GPU at 1.25M rows with a 1-rank RCCL group), or the
-  // lead-decides form over the fused IPC exchange (mode 2, COBALT_DP_EVAL_PART=1: with a 1-rank IPC
-  // group 88.5 ms per 1.25M-row fit against 86.2 for k_eval + k_partition -- the lead's evaluation, its
-  // hand-off and the late row / bin loads cost more than the launch they save -- so off by default)
-  static const int env_dp_ep = getenv("COBALT_DP_EVAL_PART") ? atoi(getenv("COBALT_DP_EVAL_PART")) : 0;
-  const int ep_mode = !dp ? 0 : (ipc_fused ? (env_dp_ep ? 2 : -1) : 1);
   // node ownership (see node_owner): over the fused exchange with separate k_eval / k_partition passes,
   // on the three deepest split levels (where the exchange volume is: 56 of a depth-7 tree's 64 pairs;
   // the copy costs the other ranks one more remote round trip, not worth it for a level's few nodes),
   // and never before a level with a node per rank. COBALT_DP_OWNER=0: every rank evaluates every node
-  static const int env_owner = getenv("COBALT_DP_OWNER") ? atoi(getenv("COBALT_DP_OWNER")) : 1;
+  static const int env_owner = knob_int(Knob::DpOwner, 1);
   d.own_level = -1;
-  if (ipc_fused && ep_mode == -1 && env_owner && d.world > 1 && eval_fg == 0 && c->max_nodes <= kIpcDecNodes) {
+  if (ipc_fused && env_owner && d.world > 1 && eval_fg == 0 && c->max_nodes <= kIpcDecNodes) {
     int l0 = 0;
     while ((1 << l0) < d.world) ++l0;
     l0 = std::max(l0, D - 3);
     d.own_level = l0 < D ? l0 : -1;
   }
-  const bool eval_part = env_ep != 0 && ep_mode >= 0 && eval_fg == 0 && !eval_compact && !fuse_part && part_wide(d) &&
-                         ep_steps <= 8 && d.F <= 32 && (ep_mode != 2 || fused_lds <= 65536);
-  // Item size of a level's fused pass: the grid (items + one partial item per node) must fit one
-  // 1024-thread block per CU -- beyond that a second round of blocks doubles the level (1M rows with
-  // 4096-row items: levels 4-5 launched 261 / 277 blocks on 256 CUs), and the data-parallel form
-  // relies on the whole grid being resident at once. The partition item size while it fits, else
-  // 8192 rows, else the level runs the separate evaluation + partition (0). COBALT_EVAL_PART=2 forces
-  // the fusion on one GPU (8192-row items when none fits).
+  const bool eval_part = env_ep != 0 && !ipc_fused && eval_fg == 0 && ep_steps <= 8 && d.F <= 32;
+  // Item size of a level's fused pass: the grid (items + one partial item per node) fits one 1024-thread
+  // block per CU -- beyond that a second round of blocks doubles the level (1M rows with 4096-row items:
+  // levels 4-5 launched 261 / 277 blocks on 256 CUs). The smallest item (in 1024-row steps from 4096)
+  // whose grid is one block per CU (a level whose 4096-row items overflow the CUs takes 5120 / 6144 / 7168
+  // instead of jumping to 8192: 1.25M rows: 6144 at every level), else the level runs the separate
+  // evaluation + partition (0). COBALT_EVAL_PART=2 forces the fusion on one GPU (8192-row items).
   auto ep_chunk = [&](int level) -> int {
     if (!eval_part) return 0;
     const int cus = device_cu_count();
-    // the smallest item (in 1024-row steps from 4096) whose grid is one block per CU: a level whose
-    // 4096-row items overflow the CUs takes 5120 / 6144 / 7168 instead of jumping to 8192 (fewer rows
-    // per block; 1.25M rows: 6144 at every level instead of 8192)
-    static const int fine = getenv("COBALT_EP_FINE") ? atoi(getenv("COBALT_EP_FINE")) : 1;  // 0: doubling (A/B)
-    for (int ch = (fine && part_wide(d)) ? std::min(4096, chunk_part(d)) : chunk_part(d); ch <= 8192;
-         ch = fine ? ch + 1024 : ch * 2)
+    for (int ch = std::min(4096, chunk_part(d)); ch <= 8192; ch += 1024)
       if (ceil_div(d.n, ch) + (1 << level) <= cus) return ch;
-    return (env_ep == 2 && ep_mode == 0) ? 8192 : 0;
+    return (env_ep == 2 && !dp) ? 8192 : 0;
   };
   d.zero_red = nullptr;
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
-  static const int env_root = getenv("COBALT_ROOT_CHUNK") ? atoi(getenv("COBALT_ROOT_CHUNK")) : 0;
+  static const int env_root = knob_int(Knob::RootChunk, 0);
   // (never more root items than the work-item buffers hold)
   const int root_min = (int)((ceil_div(d.n, (int64_t)c->items_cap - 8) + 63) / 64 * 64);
   // Fused root pass: whole rounds of resident blocks (2 per CU at 95 VGPRs x 512 threads) of ~8k rows;
@@ -3384,16 +2849,16 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // 167.5 -> 158.3 us per tree in the stamps)
   int root_rule = std::min(chunk_hist(d, 0), 8192);
   if (fuse_root) {
-    const int64_t res = (grad_w6() ? 3LL : 2LL) * device_cu_count();
+    const int64_t res = 2LL * device_cu_count();
     const int64_t rounds = std::max<int64_t>(1, (d.n + res * 4096) / (res * 8192));  // nearest to n / (res * 8192)
     root_rule = (int)std::min<int64_t>(16384, std::max<int64_t>(1024, (ceil_div(d.n, rounds * res) + 63) / 64 * 64));
   }
   const int root_chunk = std::max(root_min, env_root > 0 ? std::min(16384, std::max(1024, env_root / 64 * 64))
                                                          : root_rule);
   // Per tree: grad (+ root histogram, node-table init, archive/apply of the previous tree), then per
-  // level: [fused: partition of the previous level + this level's histogram | unfused: hist] ->
-  // reduce -> [RCCL histogram all-reduce] -> eval [-> unfused: partition]; the last split level's
-  // children are finalised by eval.
+  // level: hist -> reduce -> [data parallel: the histogram collective] -> eval [-> partition], or
+  // hist -> reduce [-> collective] -> the fused evaluation + partition pass; the last split level's
+  // children are finalised by its evaluation.
   for (int t = t0; t < t0 + n_trees; ++t) {
     if (t >= c->cfg.max_trees) return -10;
     d.nodes = d.nodes_buf[t & 1];
@@ -3417,44 +2882,31 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     CK_LAUNCH();
     for (int level = 0; level < D; ++level) {
       const int parity = level & 1;
-      // this level's evaluation runs in the partition pass (k_eval_part), with items of ep_ch rows laid
-      // out by the level's histogram pass (ep_plan)
+      // this level's evaluation runs in the partition pass (k_eval_part) with items of ep_ch rows
       const int ep_ch = level + 1 < D ? ep_chunk(level) : 0;
       const bool ep_level = ep_ch > 0;
       d.ep_chunk = ep_ch;
-      d.ep_zero = ep_mode != 0 ? 1 : 0;
+      d.ep_zero = dp ? 1 : 0;
       const int slots = level == 0 ? 1 : (1 << (level - 1));
-      int ub;  // upper bound on the level's histogram work items
-      if (fuse_part && level > 0) {  // partition of level - 1 and this level's histogram in one pass
-        const int pl = level - 1;
-        ub = ceil_div(d.n, kPartHistRows) + (1 << pl);
-        GLAUNCH("k_part_hist", (k_part_hist<kPartHistWaves, kPartHistSteps>), dim3(ub), dim3(kPartHistWaves * kWave),
-                c->lds_hist, stream, d, pl & 1, (int64_t)(1 << pl) * d.slot_elems, pl, kPartHistRows, t);
-      } else {
-        const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
-        // with the row-count rule every pair builds its smaller child (<= half the parent's rows), so the
-        // level's items number at most ceil(n / 2 / chunk) + one partial item per pair: half the grid
-        // (and half the reduce grid) of the all-rows bound, fewer blocks that only plan and exit. The
-        // hessian rule (data parallel) may build the larger child: all-rows bound.
-        ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
-                                       : ceil_div(d.n, chh) + (1 << level);
-        if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-          GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
-                  stream, d, parity, t, level, chh);
-      }
+      const int chh = (level == 0 && fuse_root) ? root_chunk : chunk_hist(d, level);
+      // with the row-count rule every pair builds its smaller child (<= half the parent's rows), so the
+      // level's items number at most ceil(n / 2 / chunk) + one partial item per pair: half the grid
+      // (and half the reduce grid) of the all-rows bound, fewer blocks that only plan and exit. The
+      // hessian rule (data parallel) may build the larger child: all-rows bound.
+      const int ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
+                                               : ceil_div(d.n, chh) + (1 << level);
+      if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
+        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
+                stream, d, parity, t, level, chh);
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
-      GLAUNCH("k_hist_reduce", k_hist_reduce, dim3(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256)),
-              dim3(256), 0, stream, d, parity, fuse_part ? level : 0, std::min(ub, c->items_cap), level);
+      const dim3 rgrid(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256));
+      const int rn = std::min(ub, c->items_cap);
+      if (dp)
+        GLAUNCH("k_hist_reduce", k_hist_reduce<true>, rgrid, dim3(256), 0, stream, d, parity, rn, level);
+      else
+        GLAUNCH("k_hist_reduce", k_hist_reduce<false>, rgrid, dim3(256), 0, stream, d, parity, rn, level);
       CK_LAUNCH();
-      if (dp) {
-        // row-count choice: ranks built their locally smaller child -> turn it into the local LEFT
-        // child; hessian choice (the DP default) / fused pass: every rank built the globally chosen
-        // child, all-reduced as is
-        if (!fuse_part && !d.by_hess) {
-          GLAUNCH("k_dp_local", k_dp_local, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d,
-                  level, parity);
-          CK_LAUNCH();
-        }
+      if (dp) {  // every rank built the globally chosen child (hessian rule): all-reduced as is
         int rc;
         // level 0 carries the replica-digest cell after the root slot (see GbdtDev::dig)
         const int64_t count = (int64_t)slots * d.slot_elems + (level == 0 ? 2 : 0);
@@ -3473,50 +2925,45 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       if (ep_level) {
       } else if (eval_fg > 0) {  // features in groups of eval_fg over several CUs, then a per-node reduction
         const int ng = ceil_div(d.F, eval_fg);
+        const dim3 eg(1 << level, ng), eb(ceil_div(eval_fg, 2) * kWave);
         if (d.ipc_epoch)
-          GLAUNCH("k_eval", (k_eval<true, true>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), fused_lds,
-                  stream, d, level, parity, t, eval_fg, EvalSlots{});
+          GLAUNCH("k_eval", (k_eval<true, true, true>), eg, eb, fused_lds, stream, d, level, parity, t, eval_fg, EvalSlots{});
+        else if (dp)
+          GLAUNCH("k_eval", (k_eval<true, false, true>), eg, eb, 0, stream, d, level, parity, t, eval_fg, EvalSlots{});
         else
-          GLAUNCH("k_eval", (k_eval<true, false>), dim3(1 << level, ng), dim3(ceil_div(eval_fg, 2) * kWave), 0, stream,
-                  d, level, parity, t, eval_fg, EvalSlots{});
-        GLAUNCH("k_eval_finish", k_eval_finish, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
-      } else if (eval_compact) {
-        GLAUNCH("k_eval", k_eval_compact, dim3(1 << level), dim3(kEvalThreads), 0, stream, d, level, parity, t);
+          GLAUNCH("k_eval", (k_eval<true, false, false>), eg, eb, 0, stream, d, level, parity, t, eval_fg, EvalSlots{});
+        if (dp)
+          GLAUNCH("k_eval_finish", k_eval_finish<true>, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
+        else
+          GLAUNCH("k_eval_finish", k_eval_finish<false>, dim3(1 << level), dim3(kWave), 0, stream, d, level, parity, ng);
       } else {
         if (d.ipc_epoch)
-          GLAUNCH("k_eval", (k_eval<false, true>), dim3(1 << level), dim3(1024), fused_lds, stream, d, level, parity,
+          GLAUNCH("k_eval", (k_eval<false, true, true>), dim3(1 << level), dim3(1024), fused_lds, stream, d, level, parity,
                   t, d.F, c->eval_slots);
+        else if (dp)
+          GLAUNCH("k_eval", (k_eval<false, false, true>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t,
+                  d.F, c->eval_slots);
         else
-          GLAUNCH("k_eval", (k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F,
-                  c->eval_slots);
+          GLAUNCH("k_eval", (k_eval<false, false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t,
+                  d.F, c->eval_slots);
       }
-      if (!fuse_part && level + 1 < D) {  // the last split level's children are leaves: no row lists needed
+      if (level + 1 < D) {  // the last split level's children are leaves: no row lists needed
         const int chp = ep_level ? ep_ch : chunk_part(d);
         const int ubp = ceil_div(d.n, chp) + (1 << level);
         // (under the separate IPC exchange it overwrites the next level's hist_b slots whole: nothing to
         // zero; under the fused one the next level's send slot is the reduce destination to zero)
         const int64_t zero_next = (ipc && !ipc_fused) ? 0 : (int64_t)(1 << level) * d.slot_elems;
         d.zero_red = ipc_fused ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
-        const int pw = part_wide(d) ? 16 : 4;
-        const int steps = ceil_div(chp, pw * kWave);  // <= kPartSteps (chunk_part's cap)
+        const int steps = ceil_div(chp, 16 * kWave);  // <= 8 (chunk_part's cap)
         if (ep_level) {
-          const uint32_t tag = ++c->dec_tag;  // unique per launch: the decision granules need no reset
-          const size_t lds = ep_mode == 2 ? fused_lds : 0;
           c->d.seq = stamp_next(c, "k_eval_part");
-          launch_eval_part(steps <= 4 ? 4 : 8, ep_mode, dim3(ubp), lds, stream, d, parity, zero_next, level, chp, t,
-                           c->eval_slots, tag);
-        } else if (pw == 16 && steps <= 4)
+          launch_eval_part(steps, dp, dim3(ubp), stream, d, parity, zero_next, level, chp, t, c->eval_slots);
+        } else if (steps <= 4)
           GLAUNCH("k_partition", (k_partition<16, 4>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
                   level, chp);
-        else if (pw == 16 && steps <= 8)
+        else
           GLAUNCH("k_partition", (k_partition<16, 8>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
                   level, chp);
-        else if (pw == 16)
-          GLAUNCH("k_partition", (k_partition<16, kPartSteps>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity,
-                  zero_next, level, chp);
-        else
-          GLAUNCH("k_partition", (k_partition<4, kPartSteps>), dim3(ubp), dim3(4 * kWave), 0, stream, d, parity,
-                  zero_next, level, chp);
       }
       d.ipc_epoch = 0;
       CK_LAUNCH();
@@ -3536,6 +2983,15 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     GLAUNCH("k_apply_tree", k_apply_tree, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, c->grown - 1);
     CK_LAUNCH();
     c->applied = c->grown;
+  }
+  // the last tree of the call: its replica digest checked by a collective of its own (see k_dig_stage)
+  if (dp && c->grown > t0) {
+    const int ls = (c->grown - 1) & 1;
+    hipLaunchKernelGGL(k_dig_stage, dim3(1), dim3(64), 0, stream, d.dig, ls);
+    CK_LAUNCH();
+    if (int rc = cobalt_comm_allreduce_sum_i64(c->cfg.comm, d.dig + 2, 1, stream)) return rc;
+    hipLaunchKernelGGL(k_dig_cmp, dim3(1), dim3(64), 0, stream, d.dig, ls, d.world, d.err_host);
+    CK_LAUNCH();
   }
   d.stamps = nullptr;
   return stamp_dump(c, stream);
@@ -3776,7 +3232,7 @@ COBALT_API int cobalt_gbdt_ox_level(void* h, int level, int t, hipStream_t strea
   hipLaunchKernelGGL(k_ox_reduce, dim3(slots, ceil_div(d.slot_elems / 2, 256)), dim3(256), 0, stream, d, c->ox_slab,
                      parity, slots);
   CK_LAUNCH();
-  hipLaunchKernelGGL((k_eval<false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F,
+  hipLaunchKernelGGL((k_eval<false, false, false>), dim3(1 << level), dim3(1024), 0, stream, d, level, parity, t, d.F,
                      c->eval_slots);
   CK_LAUNCH();
   return 0;
@@ -3977,7 +3433,7 @@ COBALT_API int cobalt_bin_matrix_ld(const float* X, int64_t n, int F, int64_t ld
   const int grid = std::max(1, std::min(ceil_div(n, 256), 256 * 8));
   // 32-byte records of 16-byte aligned rows: the vectorised kernel (10M x 20: 1.37 ms with k_bin)
   if (stride == 32 && ldx == F && F % 4 == 0 && F >= 4 && F <= 24 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
-      (reinterpret_cast<uintptr_t>(bins) & 15) == 0 && getenv("COBALT_BIN_SCALAR") == nullptr) {
+      (reinterpret_cast<uintptr_t>(bins) & 15) == 0 && knob_str(Knob::BinScalar) == nullptr) {
     switch (F / 4) {
 #define BIN_CASE(K) \
       case K: hipLaunchKernelGGL(k_bin_rec32<K>, dim3(grid), dim3(256), 0, stream, X, n, cuts, nbins, bins, binsT, ldt); break;

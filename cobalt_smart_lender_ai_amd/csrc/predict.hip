@@ -17,6 +17,7 @@
 // per (row, path) runs EXTEND over the path and the UNWOUND sum per element in fp64, contributions
 // are reduced per block in LDS and flushed with one fp64 atomic per (row, feature).
 #include "common.h"
+#include "knobs.h"
 #include <algorithm>
 
 using namespace cobalt;
@@ -112,8 +113,7 @@ COBALT_API int cobalt_predict(const float* X, int64_t n, int F, int64_t ldx, con
   const size_t lds = (size_t)tile_cap * sizeof(uint2) + (size_t)block * (F | 1) * sizeof(float);
   if (lds > 160 * 1024) return -3;
   static const int walk = [] {
-    const char* e = getenv("COBALT_PRED_WALK");
-    const int w = e ? atoi(e) : kWalk;
+    const int w = cobalt::knob_int(cobalt::Knob::PredWalk, kWalk);
     return (w == 2 || w == 8) ? w : kWalk;
   }();
   const void* fn = walk == 2 ? (const void*)k_predict<2> : walk == 8 ? (const void*)k_predict<8>

@@ -148,14 +148,16 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
                                                          int nseg, float* __restrict__ cval, int32_t* __restrict__ cw) {
   __shared__ float s_u[kSkMaxBounds];
   __shared__ int32_t s_slot[kSkBuckets];
-  __shared__ uint32_t s_cur[kSkBuckets];  // per selected bucket: this block's write cursor
+  // per selected bucket: this block's rows written so far (relative to the block's int64 segment offset
+  // bo[segment]: a streamed sketch accumulates offsets across chunks, past 2^32 candidates at billions of
+  // rows, while one block's count always fits 32 bits)
+  __shared__ uint32_t s_cur[kSkBuckets];
   const int f = blockIdx.y;
   sk_load_bounds(s_u, bounds, f);
   const int64_t* bo = blk_off + (int64_t)blockIdx.x * nseg;
   for (int i = threadIdx.x; i < kSkBuckets; i += blockDim.x) {
-    const int sg = slot[(int64_t)f * kSkBuckets + i];
-    s_slot[i] = sg;
-    s_cur[i] = sg >= 0 ? (uint32_t)bo[sg] : 0u;
+    s_slot[i] = slot[(int64_t)f * kSkBuckets + i];
+    s_cur[i] = 0u;
   }
   const int m = nbound[f];
   __syncthreads();
@@ -166,8 +168,9 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
     const float v = canon(col[r]);
     if (v != v) continue;
     const int b = sk_bucket(s_u, m, v);
-    if (s_slot[b] < 0) continue;
-    const uint32_t pos = atomicAdd(&s_cur[b], 1u);
+    const int sg = s_slot[b];
+    if (sg < 0) continue;
+    const int64_t pos = bo[sg] + (int64_t)atomicAdd(&s_cur[b], 1u);
     cval[pos] = v;
     if (kW) cw[pos] = w[r];
   }

@@ -133,6 +133,16 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
         raise ValueError("sample_rate must be in (0, 1]")
     exact = sample_rate >= 1.0  # every row every tree: level-wise page streaming (no sample)
     dev = _resolve_device(device, None)
+    if exact and dev.type == "cuda":
+        # the exact pass keeps a row's node in 2^(depth + 1) - 1 <= 255 staged node slots and the feature
+        # table in LDS (csrc/gbdt.hip cobalt_gbdt_ox_init): refuse before the sketch / page passes
+        n_feat = None
+        if int(params.max_depth) <= 7:  # the feature count from the stream's first chunk (one chunk read)
+            first = next(iter(source()), None)
+            n_feat = None if first is None else int(first[0].shape[1])
+        if int(params.max_depth) > 7 or (n_feat is not None and n_feat > 32):
+            raise ValueError(f"exact out-of-core training (sample_rate=1) supports max_depth <= 7 and <= 32 "
+                             f"features (got max_depth={params.max_depth}, features={n_feat}); use sample_rate < 1")
     rep = report if report is not None else ExternalReport()
     t0 = time.perf_counter()
     # the sketch: exact streaming (every row) sketches every row by default, like the in-core fit on a

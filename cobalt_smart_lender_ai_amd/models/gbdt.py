@@ -240,15 +240,15 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     sketch_rows = resolve_sketch_rows(sketch_rows, dev, n_glob)
     ts = time.perf_counter()
     has_missing = torch.isnan(Xt).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
-    if world > 1:
-        has_missing = _allreduce_max_flags(has_missing, dist, dev)
     full = not sketch_rows
     if full and dev.type == "cuda" and sketch_mode != "summary":
         # every row, exactly (csrc/sketch.hip: bucket histograms + per-bucket selection, no row sort;
-        # under data parallelism the histograms are all-reduced, so the cuts are the full data's)
+        # under data parallelism three device all-reduces -- the missing flags ride in the first -- so
+        # the cuts are the full data's)
         sw = _to_tensor(sketch_weights, dev).reshape(-1) if sketch_weights is not None else None
-        cuts, nbins = sketch.device_exact_cuts(Xt, max_bin, sw, has_missing, dist=dist if world > 1 else None,
-                                               row_offset=row_offset, n_rows_global=n_glob)
+        cuts, nbins = sketch.device_exact_cuts(Xt, max_bin, sw, has_missing if world == 1 else None,
+                                               dist=dist if world > 1 else None, row_offset=row_offset,
+                                               n_rows_global=n_glob)
         torch.cuda.synchronize(dev)
         t_sketch = time.perf_counter() - ts
         tb = time.perf_counter()
@@ -259,6 +259,8 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
         torch.cuda.synchronize(dev)
         bd.t_bin = time.perf_counter() - tb
         return bd
+    if world > 1:
+        has_missing = _allreduce_max_flags(has_missing, dist, dev)
     stride = 1 if full else sketch.sample_stride(n_glob, sketch_rows)
     samp = sketch.local_sample(Xt, row_offset, stride)
     wsamp = None
@@ -433,24 +435,36 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     T0 = init_booster.num_trees if init_booster is not None else 0
     if init_booster is not None and init_margin is None:
         raise ValueError("init_booster needs init_margin (its margins on the training rows)")
-    # base score = weighted label mean (XGBoost boost_from_average for binary:logistic)
+    # base score = weighted label mean (XGBoost boost_from_average for binary:logistic) and the largest
+    # weight (the fixed-point scales); under data parallelism both in ONE collective: [sum w, sum w y,
+    # every rank's max weight in its own slot] summed on the device
+    need_bs = init_booster is None and params.base_score is None
+    if world > 1:
+        buf = torch.zeros(2 + world, dtype=torch.float64, device=dev)
+        if need_bs:
+            buf[0] = wt.double().sum()
+            buf[1] = (wt.double() * yt.double()).sum()
+        if N:
+            buf[2 + dist.rank] = wt.max().double()
+        if hasattr(dist, "device_allreduce") and dev.type == "cuda":
+            dist.device_allreduce(buf, "sum")
+        else:
+            t = buf.to(dist._coll_device(dev))
+            dist.allreduce(t, "sum")
+            buf = t.to(dev)
+        sw, swy, wmax = (float(v) for v in (buf[0], buf[1], buf[2:].max()))
+    else:
+        sw = float(wt.double().sum()) if need_bs else 0.0
+        swy = float((wt.double() * yt.double()).sum()) if need_bs else 0.0
+        wmax = float(wt.max()) if N else 1.0
     if init_booster is not None:
         base_score = float(init_booster.base_score)
     elif params.base_score is None:
-        sw = float(wt.double().sum())
-        swy = float((wt.double() * yt.double()).sum())
-        if world > 1:
-            sw = dist.allreduce_scalar(sw, "sum", dev)
-            swy = dist.allreduce_scalar(swy, "sum", dev)
         base_score = min(max(swy / sw if sw > 0 else 0.5, 1e-6), 1 - 1e-6)
     else:
         base_score = float(params.base_score)
     base_score = float(np.float32(base_score))
     base_margin = Booster([], base_score=base_score, num_feature=F).base_margin
-
-    wmax = float(wt.max()) if N else 1.0
-    if world > 1:
-        wmax = dist.allreduce_scalar(wmax, "max", dev)
     gscale, hscale = gbdt_host.quant_scales(wmax)
 
     T_new = (int(total_trees) - T0) if total_trees is not None else int(params.n_estimators)
@@ -487,7 +501,13 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         fault_after = int(os.environ.get("COBALT_FAULT_AFTER_TREES", "0") or 0)
         fault_rank = int(os.environ.get("COBALT_FAULT_RANK", "-1") or -1)
         if fault_after and end >= fault_after and end < T and (fault_rank < 0 or fault_rank == (dist.rank if dist else 0)):
-            raise InjectedFault(f"injected fault after tree {end}")
+            stall = float(os.environ.get("COBALT_FAULT_STALL_S", "0") or 0)
+            if stall > 0:  # a slow (not dead) rank: once, then it carries on
+                if not getattr(segment_done, "stalled", False):
+                    segment_done.stalled = True
+                    time.sleep(stall)
+            else:
+                raise InjectedFault(f"injected fault after tree {end}")
     hp = gbdt_host.HostGbdtParams(max_depth=int(params.max_depth), eta=float(params.learning_rate),
                                   reg_lambda=float(params.reg_lambda), reg_alpha=float(params.reg_alpha),
                                   gamma=float(params.gamma), min_child_weight=float(params.min_child_weight),

@@ -404,9 +404,13 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     pass histograms the rows per bucket, the target ranks are located by prefix sums, and only the
     rows of the few buckets that hold a target are gathered and sorted (in LDS, per bucket).
 
-    Under data parallelism (``dist``) every rank passes its shard: the sample is global (strided by
-    global row index), the bucket histograms are all-reduced and the candidates all-gathered, so all
-    ranks compute the cuts of the full data. ``w_max`` scales the weights (default: the global max)."""
+    Under data parallelism (``dist``) every rank passes its shard and the ranks exchange exactly three
+    fixed-layout SUM all-reduces on the device (``dist.device_allreduce``; no size exchanges, no
+    padding): (1) the global strided sample, placed by global sample index, with the missing-value flags
+    and the weight scale; (2) every rank's bucket counts (+ weight sums) and value range, by rank slot --
+    so each rank also knows where its rows go inside every global candidate segment; (3) the candidates,
+    written straight into the global segment layout. Every rank then computes the full data's cuts.
+    ``w_max`` scales the weights (default: the global max)."""
     import os
 
     N, F = X.shape
@@ -422,29 +426,94 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     world = dist.world if dist is not None else 1
     n_glob = n_rows_global if n_rows_global is not None else N
     X = X.to(torch.float32)
-    if has_missing is None:
-        has_missing = torch.isnan(X).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
-        if world > 1:
-            t = has_missing.to(torch.float32).to(dist._coll_device(dev))
-            dist.allreduce(t, "max")
-            has_missing = t.to(dev) > 0
-    wq = None
-    if weights is not None:
-        wd = weights.to(device=dev, dtype=torch.float64).reshape(-1)
-        if w_max is None:
-            w_max = float(wd.max()) if wd.numel() else 0.0
-            if world > 1:
-                w_max = dist.allreduce_scalar(w_max, "max", dev)
+    stride = sample_stride(n_glob, sample_rows)
+    samp = local_sample(X, row_offset, stride)
+    wd = weights.to(device=dev, dtype=torch.float64).reshape(-1) if weights is not None else None
+    if wd is not None:
         if bool((wd < 0).any()) or not bool(torch.isfinite(wd).all()):
             raise ValueError("sketch weights must be finite and >= 0")
+        if w_max is None:
+            w_max = float(wd.max()) if wd.numel() else 0.0
+    if world > 1:
+        # collective 1: the global sample + missing flags + weight scale (folded into the one exchange)
+        samp, has_missing, w_max = _global_sample(dist, dev, X, samp, row_offset, stride, n_glob, has_missing,
+                                                  w_max if wd is not None else None)
+    elif has_missing is None:
+        has_missing = torch.isnan(X).any(0) if N else torch.zeros(F, dtype=torch.bool, device=dev)
+    wq = None
+    if wd is not None:
         scale = WEIGHT_SCALE / w_max if w_max and w_max > 0 else 0.0
         wq = (torch.round(wd * scale) if scale else torch.ones_like(wd)).to(torch.int32).contiguous()
-
-    samp = local_sample(X, row_offset, sample_stride(n_glob, sample_rows))
-    if world > 1:
-        samp = dist.allgather_rows(samp)
     return _exact_core(lambda: iter([(X, wq)]), True, N, F, dev, samp, has_missing, max_bin, dist, wq is not None,
                        mark, marks, timing)
+
+
+def _global_sample(dist, dev, X, samp, row_offset: int, stride: int, n_glob: int, has_missing, w_max):
+    """Collective 1 of the data-parallel exact sketch: ONE int32 SUM all-reduce of a fixed layout --
+    the global strided sample (row g of the data, g % stride == 0, at sample index g // stride: the
+    ranks' rows are disjoint, so the sum of bit patterns IS the sample, NaN and -0.0 included), then
+    the F missing-value counts (unless ``has_missing`` is given), then every rank's float64 ``w_max``
+    bits in its own two slots. Returns (global sample [S, F], has_missing [F] bool, global w_max)."""
+    R, r = dist.world, dist.rank
+    N, F = X.shape
+    S = (n_glob - 1) // stride + 1 if n_glob > 0 else 0
+    first = (-row_offset) % stride
+    g0 = (row_offset + first) // stride
+    ns = samp.shape[0]
+    buf = torch.zeros(S * F + F + 2 * R, dtype=torch.int32, device=dev)
+    if ns:
+        buf[g0 * F:(g0 + ns) * F] = samp.contiguous().view(torch.int32).reshape(-1)
+    if has_missing is None and N:
+        buf[S * F:S * F + F] = torch.isnan(X).any(0).to(torch.int32)
+    if w_max is not None:
+        buf[S * F + F + 2 * r:S * F + F + 2 * r + 2] = torch.tensor([float(w_max)], dtype=torch.float64).view(
+            torch.int32).to(dev)
+    dist.device_allreduce(buf, "sum")
+    gsamp = buf[:S * F].view(torch.float32).reshape(S, F)
+    hm = has_missing.to(dev).to(torch.bool) if has_missing is not None else buf[S * F:S * F + F] > 0
+    wm = None
+    if w_max is not None:
+        wm = float(buf[S * F + F:].cpu().view(torch.float64).max())
+    return gsamp, hm, wm
+
+
+def _fkey64(v: torch.Tensor) -> torch.Tensor:
+    """Order-preserving integer key of float32 values (int64, ascending with the value; -0 < +0)."""
+    b = v.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    return torch.where(b >= 0x80000000, 0xFFFFFFFF - b, b + 0x80000000)
+
+
+def _fkey64_inv(k: torch.Tensor) -> torch.Tensor:
+    b = torch.where(k >= 0x80000000, k - 0x80000000, 0xFFFFFFFF - k)
+    return (b - ((b >= 0x80000000).to(torch.int64) << 32)).to(torch.int32).view(torch.float32)
+
+
+def _allreduce_buckets(dist, dev, cnt_loc, w_loc, vmin, vmax):
+    """Collective 2 of the data-parallel exact sketch: ONE int64 SUM all-reduce of every rank's bucket
+    counts (and weight sums) in its own rank slot, plus its value range as order keys. Returns the global
+    counts, weight sums, min / max, and this rank's row offset inside every bucket (the rows of the
+    lower ranks) -- the position of its candidates in the global segment layout, with no further
+    exchange."""
+    R, r = dist.world, dist.rank
+    F, NB = cnt_loc.shape
+    FN = F * NB
+    nw = FN if w_loc is not None else 0
+    buf = torch.zeros(R * (FN + nw + 2 * F), dtype=torch.int64, device=dev)
+    base = r * (FN + nw + 2 * F)
+    buf[base:base + FN] = cnt_loc.reshape(-1)
+    if w_loc is not None:
+        buf[base + FN:base + FN + nw] = w_loc.reshape(-1)
+    buf[base + FN + nw:base + FN + nw + F] = _fkey64(vmin)
+    buf[base + FN + nw + F:base + FN + nw + 2 * F] = _fkey64(vmax)
+    dist.device_allreduce(buf, "sum")
+    per = buf.reshape(R, FN + nw + 2 * F)
+    cnts = per[:, :FN].reshape(R, F, NB)
+    cnt_h = cnts.sum(0)
+    before = (torch.cumsum(cnts, 0) - cnts)[r]
+    w_h = per[:, FN:FN + nw].reshape(R, F, NB).sum(0) if w_loc is not None else None
+    vmin_g = _fkey64_inv(per[:, FN + nw:FN + nw + F].amin(0))
+    vmax_g = _fkey64_inv(per[:, FN + nw + F:].amax(0))
+    return cnt_h, w_h, vmin_g, vmax_g, before
 
 
 def stream_exact_cuts(chunks, n_rows: int, n_features: int, samp: torch.Tensor, has_missing: torch.Tensor,
@@ -544,21 +613,9 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
         if single:
             kept = (XT, Xc.shape[0], wq, nblk, cnt_slab)
     cnt_h = cnt_loc
-    if world > 1:
-        cd = dist._coll_device(dev)
-        cnt_h = cnt_loc.to(cd).clone()
-        dist.allreduce(cnt_h, "sum")
-        cnt_h = cnt_h.to(dev)
-        if w_h is not None:
-            t = w_h.to(cd)
-            dist.allreduce(t, "sum")
-            w_h = t.to(dev)
-        t = vmin.to(cd)
-        dist.allreduce(t, "min")
-        vmin = t.to(dev)
-        t = vmax.to(cd)
-        dist.allreduce(t, "max")
-        vmax = t.to(dev)
+    before = None  # (data parallel) this rank's offset inside every bucket's global candidate segment
+    if world > 1:  # collective 2
+        cnt_h, w_h, vmin, vmax, before = _allreduce_buckets(dist, dev, cnt_loc, w_h, vmin, vmax)
     if w_h is None:
         w_h = cnt_h
     mark("hist")
@@ -598,15 +655,26 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
     glob_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
     if nseg:
         glob_off[1:] = torch.cumsum(glob_sizes, 0)
-    tot_loc = int(loc_off[-1])
     mark("targets")
 
     # 4. candidates: the rows of the selected buckets, per segment (a second walk over the chunks;
-    # each block writes at its offset from the chunk's per-block bucket counts)
-    cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)
-    cw = torch.empty(max(tot_loc, 1), dtype=torch.int32, device=dev) if weighted else None
+    # each block writes at its offset from the chunk's per-block bucket counts). Data parallel: straight
+    # into the GLOBAL segment layout (this rank's rows of segment s start at glob_off[s] + the lower
+    # ranks' rows of s), zeros elsewhere, and collective 3 sums the ranks' buffers: values and weights
+    # in one int32 buffer [tot | tot].
+    if world > 1:
+        tot_loc = tot = int(glob_off[-1])
+        cbuf = torch.zeros(max(2 * tot if weighted else tot, 1), dtype=torch.int32, device=dev)
+        cval = cbuf[:max(tot, 1)].view(torch.float32)
+        cw = cbuf[tot:2 * tot] if weighted else None
+        start = glob_off[:-1] + before.reshape(-1)[sel_f]
+    else:
+        tot_loc = int(loc_off[-1])
+        cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)
+        cw = torch.empty(max(tot_loc, 1), dtype=torch.int32, device=dev) if weighted else None
+        start = loc_off[:-1]
     if nseg and N:
-        cursor = loc_off[:-1].clone()
+        cursor = start.clone()
         for Xc, wq in (iter([(None, None)]) if single else chunks()):
             if single:
                 XT, n, wq, nblk, cnt_slab = kept
@@ -624,9 +692,8 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
                                       stream)
             _native.check(rc, "cobalt_sk_gather")
             cursor += per_blk.sum(0)
-    if world > 1 and nseg:  # every rank's candidates, re-packed segment by segment
-        cval, cw = _merge_candidates(dist, dev, cval[:tot_loc], None if cw is None else cw[:tot_loc], loc_sizes,
-                                     glob_off)
+    if world > 1 and nseg:  # collective 3: every rank's candidates, already in the global layout
+        dist.device_allreduce(cbuf, "sum")
 
     mark("gather")
     # 5. select the open targets from their bucket's sorted candidates
@@ -711,37 +778,3 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
     return out
 
 
-def _merge_candidates(dist, dev, cval, cw, loc_sizes, glob_off):
-    """All ranks' candidate values (and weights) re-packed into the global segment layout: segment s
-    holds rank 0's values of s, then rank 1's, ... (the order inside a segment does not matter)."""
-    world = dist.world
-    cd = dist._coll_device(dev)
-    nseg = loc_sizes.numel()
-    # (through the context: also the in-process loopback group of the tests; every rank has nseg)
-    all_sizes = dist.allgather_rows(loc_sizes.to(cd).reshape(-1, 1), pad_value=0).to(dev).reshape(world, nseg)
-    vals = dist.allgather_rows(cval.reshape(-1, 1).to(cd), pad_value=0.0).to(dev)[:, 0]
-    # rank r's values start at r * max_n (padded gather) or after the lower ranks' (packed gather)
-    n_rank = [int(v) for v in all_sizes.sum(1).tolist()]
-    padded = vals.numel() == world * max(n_rank)
-    start = [r * max(n_rank) for r in range(world)] if padded else [sum(n_rank[:r]) for r in range(world)]
-    wts = None
-    if cw is not None:
-        wts = dist.allgather_rows(cw.to(torch.float64).reshape(-1, 1).to(cd), pad_value=0.0).to(dev)[:, 0]
-    nseg = all_sizes.shape[1]
-    before = torch.cumsum(all_sizes, 0) - all_sizes                                     # rows of lower ranks per segment
-    total = int(glob_off[-1])
-    out_v = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
-    out_w = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if cw is not None else None
-    for r in range(world):
-        sz = all_sizes[r]
-        n_r = int(sz.sum())
-        if n_r == 0:
-            continue
-        seg = torch.repeat_interleave(torch.arange(nseg, device=dev), sz)
-        loff = torch.cumsum(sz, 0) - sz
-        k = torch.arange(n_r, device=dev) - loff[seg]
-        dest = glob_off[:-1][seg] + before[r][seg] + k
-        out_v[dest] = vals[start[r]:start[r] + n_r]
-        if out_w is not None:
-            out_w[dest] = wts[start[r]:start[r] + n_r].to(torch.int32)
-    return out_v, out_w

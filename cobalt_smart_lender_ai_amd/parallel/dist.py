@@ -57,6 +57,33 @@ class DistContext:
         self.allreduce(t, op)
         return float(t.item())
 
+    def device_allreduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """In-place all-reduce of a contiguous device tensor, enqueued on the current stream: on the
+        trainer's native communicator when this context has one (the IPC group or RCCL -- no host round
+        trip, also in the gloo-bootstrapped rehearsal where torch's collectives would copy through the
+        CPU), else through torch.distributed. Every rank must call it with the same shape and dtype."""
+        if self.world == 1:
+            return t
+        if self.native_comm and t.is_cuda and t.is_contiguous():
+            from .. import _native
+
+            code = {torch.int64: 0, torch.uint8: 1, torch.int32: 2, torch.float32: 3, torch.float64: 4}[t.dtype]
+            opc = {"sum": 0, "max": 2, "min": 3}[op]
+            lib = _native.lib()
+            flat = t.view(-1)
+            step = max(1, (32 << 20) // t.element_size())  # within the IPC group's send slot (>= 64 MiB)
+            for s in range(0, flat.numel(), step):
+                piece = flat[s:s + step]
+                rc = lib.cobalt_comm_allreduce(ctypes.c_void_p(self.native_comm), ctypes.c_void_p(piece.data_ptr()),
+                                               piece.numel(), code, opc, ctypes.c_void_p(_native.stream_handle()))
+                if rc != 0:
+                    raise RuntimeError(f"native all-reduce failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+            return t
+        x = t.to(self._coll_device(t.device))
+        self.allreduce(x, op)
+        t.copy_(x)
+        return t
+
     def allgather_rows(self, t: torch.Tensor, pad_value: float = float("nan")) -> torch.Tensor:
         """All-gather a [n_local, F] tensor with per-rank row counts (pads with ``pad_value``)."""
         if self.world == 1:
@@ -271,38 +298,52 @@ def _quiesce() -> None:
 
 
 def _ipc_selftest(ctx: DistContext, comm: int) -> None:
+    """Connect self-test of the IPC group. Every rank runs EVERY round and every barrier whatever its
+    own rounds returned -- a failure is recorded and raised only after the loop -- so a rank whose probe
+    fails never leaves the barrier sequence early (its peers would sit in a torch barrier while it
+    entered the caller's agreement all-reduce: mismatched collectives)."""
     from .. import _native
 
     lib = _native.lib()
-    dev = torch.device("cuda", torch.cuda.current_device())
+    # (a CPU device only in the gloo rehearsal of tests/test_dist_agreement.py, with a fake library)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     n = 4099
     idx = torch.arange(n, dtype=torch.int64, device=dev)
+    errors: list[str] = []
     # four rounds: each send slot is written and read twice with different data, so a peer's stale
-    # cached copy of a reused slot (the trainer reuses them every other level) fails the test here
+    # cached copy of a reused slot (the trainer reuses them every other level) fails the test here.
+    # (no torch collective in this loop: a rank that failed a round still runs the next ones, whose
+    # in-kernel waits are bounded by the group's connect deadline)
     for rnd in range(4):
         buf = idx * (ctx.rank + 1) + 1000 * rnd
         rc = lib.cobalt_comm_allreduce(ctypes.c_void_p(comm), ctypes.c_void_p(buf.data_ptr()), n, 0, 0,
                                        ctypes.c_void_p(_native.stream_handle()))
         if rc != 0:
-            raise RuntimeError(f"IPC self-test all-reduce failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
-        torch.cuda.synchronize(dev)
+            errors.append(f"IPC self-test all-reduce failed ({rc}): {lib.cobalt_comm_last_error().decode()}")
+            continue
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
         if lib.cobalt_comm_async_error(ctypes.c_void_p(comm)):
-            raise RuntimeError(f"IPC self-test: {lib.cobalt_comm_last_error().decode()}")
+            errors.append(f"IPC self-test: {lib.cobalt_comm_last_error().decode()}")
+            continue
         w = ctx.world
         want = idx * (w * (w + 1) // 2) + 1000 * rnd * w
         if not torch.equal(buf, want):
-            raise RuntimeError("IPC self-test all-reduce returned wrong sums")
+            errors.append("IPC self-test all-reduce returned wrong sums")
     # the node-owner decision table (written and read by the ranks' kernels while they run): two rounds
-    # of a record per rank, read back by every peer (csrc/ipccomm.hip k_ipc_dtab_probe)
+    # of a record per rank, read back by every peer (csrc/ipccomm.hip k_ipc_dtab_probe). The barrier
+    # after each round runs on every rank, failed or not.
     probe = getattr(lib, "cobalt_ipc_dtab_selftest", None)
     if probe is not None:
         for rnd in range(2):
             res = probe(ctypes.c_void_p(comm), rnd + 1, ctypes.c_void_p(_native.stream_handle()))
             if res != 0:
-                raise RuntimeError(f"IPC decision-table self-test failed ({res}): "
-                                   + ("a peer's record did not arrive" if res == 2 else "records corrupted")
-                                   if res > 0 else lib.cobalt_comm_last_error().decode())
+                errors.append(f"IPC decision-table self-test failed ({res}): "
+                              + (("a peer's record did not arrive" if res == 2 else "records corrupted")
+                                 if res > 0 else lib.cobalt_comm_last_error().decode()))
             ctx.barrier()  # (every rank read round k before any rank overwrites it with round k + 1)
+    if errors:
+        raise RuntimeError("; ".join(errors))
 
 
 def create_rccl_comm(ctx: DistContext) -> int:
@@ -362,6 +403,15 @@ def wait_with_watchdog(done: "callable", *, timeout_s: float, comm_error: "calla
             raise CollectiveTimeout(f"{what}: {reason}; communicator aborted")
         time.sleep(sleep)
         sleep = min(sleep * 2, poll_s)
+    # The work can also COMPLETE after an exchange failed: a timed-out in-kernel wait marks the group
+    # failed (sticky) and the later exchanges of the segment return at once. That is a timeout, reported
+    # as one -- checked before the caller looks at the replica digest, which such a segment also breaks.
+    err = comm_error() if comm_error is not None else 0
+    if err:
+        if abort is not None:
+            abort()
+        raise CollectiveTimeout(f"{what}: communicator error {err} (an exchange deadline passed on this rank or "
+                                "a peer); communicator aborted")
 
 
 def abort_native_comm(ctx: DistContext) -> None:

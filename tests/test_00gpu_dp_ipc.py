@@ -30,23 +30,22 @@ def test_ipc_data_parallel_processes_equal_single_process():
     _check_clean(torch.cuda.is_initialized())
     ref = dp_check.run(1, ROWS)[0]
     assert ref["ok"], ref
-    # the exchange fused into the split evaluation (default: k_eval + k_partition) with 2, 3 and 4 ranks
-    # -- ipc_sum_cells<4> --, the lead-decides evaluation + partition pass (k_eval_part mode 2,
-    # COBALT_DP_EVAL_PART=1), and the separate exchange kernel (COBALT_IPC_FUSED=0: k_eval_part mode 1
-    # over the all-reduced histograms). The ranks share the device through disjoint CU masks
+    # the exchange fused into the split evaluation (default: k_eval + k_partition) with 2 to 5 ranks
+    # -- ipc_sum_cells<5> --, and the separate exchange kernel (COBALT_IPC_FUSED=0: the fused evaluation +
+    # partition pass k_eval_part<.., kDP> over the all-reduced histograms). The ranks share the device through disjoint CU masks
     # (parallel/cumask.py); 8 ranks: test_ipc_eight_ranks_share_one_gpu
     # node ownership (the default over the fused exchange: levels 4-6 of these depth-7 trees, owners by
     # subtree) and every rank evaluating every node (COBALT_DP_OWNER=0); a depth-3 fit owns from the
     # first level with a node per rank
     for procs, env in ((2, None), (3, None), (4, None), (5, None), (3, {"COBALT_DP_OWNER": "0"}),
-                       (2, {"COBALT_DP_EVAL_PART": "1"}), (4, {"COBALT_DP_EVAL_PART": "1"}),
-                       (2, {"COBALT_IPC_FUSED": "0"})):
+                       (2, {"COBALT_IPC_FUSED": "0"}), (4, {"COBALT_IPC_FUSED": "0"})):
         got = dp_check.run(procs, ROWS, timeout_s=400, env=env)
         for g in got:
             assert g["ok"], (procs, env, g)
             assert g["transport"] == "ipc"
-            # one exchange per level per tree, plus the connect self-test's four (each slot twice)
-            assert g["ipc_epochs"] == 4 + 7 * ref["trees"]
+            # one exchange per level per tree, the connect self-test's four (each slot twice) and the final
+            # replica-digest exchange of the fit's one grow call
+            assert g["ipc_epochs"] == 4 + 7 * ref["trees"] + 1
             assert g["model_sha256"] == ref["model_sha256"], (procs, env, g["rank"])
     shallow = dict(dp_check.DEFAULT_PARAMS, max_depth=3)
     ref3 = dp_check.run(1, ROWS, shallow)[0]
@@ -73,7 +72,7 @@ def test_ipc_eight_ranks_share_one_gpu():
     for g in got:
         assert g["ok"], g
         assert g["transport"] == "ipc" and g.get("cu_budget") is None
-        assert g["ipc_epochs"] == 4 + 7
+        assert g["ipc_epochs"] == 4 + 7 + 1
         assert g["model_sha256"] == ref["model_sha256"], g["rank"]
 
 
@@ -113,6 +112,44 @@ def test_ipc_replica_divergence_fails_every_rank():
     # the same fit without the fault: the check stays quiet
     got = dp_check.run(2, 200_000, params, checkpoint_every=1, timeout_s=300)
     assert all(g["ok"] for g in got), got
+
+
+@pytest.mark.timeout(600)
+def test_ipc_replica_divergence_in_the_last_tree_fails_every_rank():
+    """The last tree of a grow call has no next tree whose root exchange would carry its digest: the
+    call ends with a digest-only collective (csrc/gbdt.hip k_dig_stage / k_dig_cmp), so a divergence in
+    the fit's last tree -- or in the last tree of a checkpoint segment -- is reported on every rank
+    before the trees are fetched or checkpointed (advisor finding, round 4)."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=8)
+    for every, tree, where in ((0, 7, "before tree 8"), (4, 3, "before tree 4")):
+        got = dp_check.run(2, 200_000, params, checkpoint_every=every, timeout_s=300,
+                           env={"COBALT_FAULT_CORRUPT_RANK": "1", "COBALT_FAULT_CORRUPT_TREE": str(tree)})
+        for g in got:
+            assert not g["ok"], (every, tree, g)
+            assert g.get("error") == "ReplicaDivergence", (every, tree, g)
+            assert where in g.get("message", ""), (every, tree, g)
+
+
+@pytest.mark.timeout(600)
+def test_ipc_slow_peer_is_a_timeout_on_every_rank():
+    """A rank that stalls past the exchange deadline (alive, not dead): its peer's in-kernel wait times
+    out and posts a failure notice, the stalled rank's next wait sees it -- both ranks raise
+    CollectiveTimeout (not ReplicaDivergence: the digest of a tree whose exchange failed is never
+    compared as if the tree were complete)."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=8)
+    got = dp_check.run(2, 200_000, params, checkpoint_every=2, timeout_s=300,
+                       env={"COBALT_FAULT_AFTER_TREES": "2", "COBALT_FAULT_RANK": "1", "COBALT_FAULT_STALL_S": "12",
+                            "COBALT_IPC_TIMEOUT_S": "4"})
+    for g in got:
+        assert not g["ok"], g
+        assert g.get("error") == "CollectiveTimeout", g
+        assert g["elapsed_s"] < 150, g
 
 
 @pytest.mark.timeout(600)

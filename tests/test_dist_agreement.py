@@ -53,6 +53,27 @@ class _FakeLib:
     def cobalt_comm_last_error(self):
         return b"fake error"
 
+    # the real _ipc_selftest's entry points (stage "probe"): the all-reduce rounds run as gloo
+    # all-reduces of the CPU buffer, the decision-table probe fails on the failing rank only
+    def cobalt_comm_allreduce(self, comm, ptr, n, dtype, op, stream):
+        import ctypes
+
+        import numpy as np
+        import torch
+        import torch.distributed as tdist
+
+        buf = torch.from_numpy(np.ctypeslib.as_array((ctypes.c_int64 * n).from_address(ptr.value)))
+        tdist.all_reduce(buf)
+        self.log.append("allreduce")
+        return 0
+
+    def cobalt_comm_async_error(self, comm):
+        return 0
+
+    def cobalt_ipc_dtab_selftest(self, comm, rnd, stream):
+        self.log.append(f"probe{rnd}")
+        return 2 if self.fail == "probe" else 0
+
 
 def _rank_main(rank, world, port, out, fail_rank, stage):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -69,7 +90,10 @@ def _rank_main(rank, world, port, out, fail_rank, stage):
     def selftest(ctx, comm):
         if fail == "selftest":
             raise RuntimeError("IPC self-test all-reduce returned wrong sums")
-    pdist._ipc_selftest = selftest
+    if stage == "probe":  # the real self-test (its barrier sequence is what is under test)
+        _native.stream_handle = lambda *a: 0
+    else:
+        pdist._ipc_selftest = selftest
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = pdist.DistContext(rank=rank, world=world, local_rank=rank, backend="gloo", _owns_group=True)
     res = {"rank": rank}
@@ -96,6 +120,19 @@ def _run(fail_rank, stage):
         assert not p.is_alive(), "a rank hung: the agreement did not line the collectives up"
         assert p.exitcode == 0
     return [json.loads(Path(out, f"r{r}.json").read_text()) for r in range(2)]
+
+
+@pytest.mark.timeout(300)
+def test_one_rank_probe_failure_keeps_the_barriers_matched():
+    """Only rank 1's decision-table probe fails (advisor finding, round 4): both ranks still run every
+    self-test round and its barrier, then leave with IpcGroupFailed after the same collectives."""
+    got = _run(1, "probe")
+    for g in got:
+        assert "failed" in g and "handle" not in g, g
+        assert g["after"] == 3.0
+        assert g["log"].count("allreduce") == 4 and "probe1" in g["log"] and "probe2" in g["log"], g["log"]
+        assert g["log"][-1] == "destroy"
+    assert "decision-table self-test failed (2)" in got[1]["failed"]
 
 
 @pytest.mark.timeout(300)

@@ -100,3 +100,28 @@ def test_external_gpu_equals_host_path():
                                     report=rep2)
     assert rep2.device_page_bytes == 33_000 * ps and rep2.host_bytes == 27_000 * ps
     assert mixed.save_raw("ubj") == host.save_raw("ubj")
+
+
+def test_exact_out_of_core_refuses_unsupported_shapes_before_streaming():
+    """Exact streaming (sample_rate=1) supports max_depth <= 7 and <= 32 features on the GPU
+    (cobalt_gbdt_ox_init); it says so with a ValueError before the sketch and page passes, not with a
+    native error code after them (advisor finding, round 4). No GPU is touched before the check."""
+    import numpy as np
+    import torch
+
+    from cobalt_smart_lender_ai_amd.models.external import train_external
+
+    reads = []
+
+    def source(F):
+        def gen():
+            reads.append(F)
+            yield np.zeros((16, F), np.float32), np.zeros(16, np.float32)
+        return gen
+
+    with pytest.raises(ValueError, match="max_depth <= 7"):
+        train_external(source(4), {"max_depth": 8}, device=torch.device("cuda", 0), sample_rate=1.0)
+    assert reads == []  # refused before reading the stream
+    with pytest.raises(ValueError, match="<= 32 features"):
+        train_external(source(40), {"max_depth": 6}, device=torch.device("cuda", 0), sample_rate=1.0)
+    assert reads == [40]  # one chunk peeked for the feature count

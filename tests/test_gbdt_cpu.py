@@ -161,6 +161,13 @@ def test_collective_watchdog_aborts_and_raises():
     assert aborted == [1]
     calls = iter([False, False, True])
     pdist.wait_with_watchdog(lambda: next(calls), timeout_s=1, comm_error=lambda: 0)
+    # the segment completed, but an exchange failed on the way (a timed-out wait made the later ones
+    # return at once): a timeout, reported as one -- not left for the replica-digest check to call a
+    # divergence
+    aborted.clear()
+    with pytest.raises(pdist.CollectiveTimeout, match="deadline passed"):
+        pdist.wait_with_watchdog(lambda: True, timeout_s=60, comm_error=lambda: 6, abort=lambda: aborted.append(1))
+    assert aborted == [1]
 
 
 def test_predictor_tile_packing(reference_booster):

@@ -82,11 +82,12 @@ def test_gpu_trees_identical_to_host_oracle(kw):
 
 @pytest.mark.parametrize("env", [{"COBALT_HIST_PAIR": "0"}, {"COBALT_MAX_COPY_SHIFT": "6"}, {"COBALT_MAX_COPY_SHIFT": "5"},
                                  {"COBALT_MAX_COPY_SHIFT": "0", "COBALT_HIST_PAIR": "0"},
-                                 {"COBALT_PART_WIDE": "0"}])
+                                 {"COBALT_EVAL_PART": "0"}, {"COBALT_EVAL_FG": "4"}])
 def test_gpu_histogram_variants_identical_to_host_oracle(env, monkeypatch):
-    """The histogram variants behind switches (one lane per row instead of the default lane-pair record
-    gathers; 64, 32 or 1 per-lane copies of a low-cardinality feature instead of 16; 4-wave partition
-    blocks) grow the oracle's trees (the switches are read when a trainer context is created)."""
+    """The variants behind switches (one lane per row instead of the default lane-pair record gathers;
+    64, 32 or 1 per-lane copies of a low-cardinality feature instead of 16; the separate evaluation and
+    partition passes instead of the fused one; grouped split evaluation) grow the oracle's trees (the
+    switches are read when a trainer context is created)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     X, y = _data(60_000, seed=4)
@@ -322,31 +323,6 @@ def test_gpu_data_parallel_rank_failure_fails_fast_and_resumes(tmp_path, monkeyp
     assert all(o == ref for o in outs)
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_gpu_fused_partition_histogram_pass(world, monkeypatch):
-    """The fused partition + next-level histogram pass (COBALT_FUSED_PART=1, k_part_hist) grows the
-    same trees as the host oracle, alone and under the multi-rank protocol (loopback group)."""
-    from cobalt_smart_lender_ai_amd.parallel import loopback
-    from cobalt_smart_lender_ai_amd.parallel.dist import shard_range
-
-    n = 200_000
-    X, y = _data(n, seed=21)
-    params = dict(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9, colsample_bytree=0.8,
-                  random_state=5, scale_pos_weight=6.0)
-    ref = gbdt.train(X, y, params, device="cpu").save_raw("ubj")
-    monkeypatch.setenv("COBALT_FUSED_PART", "1")
-    if world == 1:
-        assert gbdt.train(X, y, params, device="cuda").save_raw("ubj") == ref
-        return
-
-    def rank_fit(ctx):
-        s, e = shard_range(n, ctx.rank, ctx.world)
-        return gbdt.train(X[s:e], y[s:e], params, device="cuda", dist=ctx, n_rows_global=n,
-                          row_offset=s).save_raw("ubj")
-
-    assert all(o == ref for o in loopback.run_ranks(world, rank_fit))
-
-
 def test_concurrent_search_fits_equal_sequential():
     """randomized_search's (fold, candidate) fits on 4 HIP streams score exactly like one stream."""
     from cobalt_smart_lender_ai_amd.select import search
@@ -361,16 +337,6 @@ def test_concurrent_search_fits_equal_sequential():
     one = search._fold_scores(X, y, folds, base, cands, "cuda", streams=1)
     four = search._fold_scores(X, y, folds, base, cands, "cuda", streams=4)
     assert np.array_equal(one, four)
-
-
-def test_gpu_compact_eval_identical_to_host_oracle(monkeypatch):
-    """The opt-in compact-cell split evaluator (COBALT_EVAL_COMPACT=1, k_eval_compact) grows the same
-    trees as the host oracle (and hence as the default F x 256-slot k_eval)."""
-    monkeypatch.setenv("COBALT_EVAL_COMPACT", "1")
-    X, y = _data(50_000, seed=4)
-    p = gbdt.GBDTParams(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9,
-                        colsample_bytree=0.7, reg_alpha=0.2, scale_pos_weight=6.0, random_state=3)
-    assert gbdt.train(X, y, p, device="cuda").save_raw("ubj") == gbdt.train(X, y, p, device="cpu").save_raw("ubj")
 
 
 @pytest.mark.timeout(900)
