@@ -166,8 +166,10 @@ KNOBS: dict[str, Knob] = {
     "COBALT_IPC_CONNECT_TIMEOUT_S": Knob("30", "python", "deadline of the IPC connect self-test"),
     "COBALT_COLLECTIVE_TIMEOUT_S": Knob("1800", "python", "host watchdog deadline for one enqueued segment of trees"),
     "COBALT_SHARED_CU_MASK": Knob("auto", "python", "CU-masked streams for ranks sharing one GPU (default up to 5 ranks)"),
+    "COBALT_CU_MASK_LAYOUT": Knob("interleaved", "python", "CU masks of ranks sharing one GPU: interleaved (CU rank + k world) or blocked"),
     "COBALT_BENCH_SHARED_DEVICE": Knob("0", "python", "bench.py: every rank on cuda:0 (the 1-GPU multi-rank rehearsal)"),
     # -- trainer / serving (python) --
+    "COBALT_PACKED_RECORDS": Knob("1", "python", "packed 16-byte row records where the bin codes fit 91 bits (0: 32-byte records)"),
     "COBALT_LABEL_IN_RECORD": Knob("1", "python", "0/1 labels ride in the row records' padding (weights derived from them)"),
     "COBALT_TRAINER_CACHE": Knob("1", "python", "keep one trainer context per process for back-to-back fits of the same shapes"),
     "COBALT_SEARCH_STREAMS": Knob("4", "python", "HIP streams of the randomized search's concurrent fits"),

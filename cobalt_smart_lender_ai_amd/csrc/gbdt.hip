@@ -215,6 +215,10 @@ struct GbdtDev {
   // node ownership (fused IPC exchange): from level own_level on, a node is evaluated only by the rank
   // owning its level-own_level ancestor; the others copy its decision (-1: every rank evaluates all)
   int32_t own_level;
+  // packed 16-byte row records (stride 16, cobalt_pack_layout): pk[f] = bit offset | width << 8 of
+  // feature f's code (device memory; the histogram kernels fold it into their per-feature metadata word)
+  int32_t packed;
+  const uint32_t* pk;
 };
 
 
@@ -391,6 +395,39 @@ __device__ __forceinline__ uint32_t node_meta(const Node& nd) {
 }
 __device__ __forceinline__ bool meta_left(uint32_t m, uint32_t b) {
   return (b == kMissingBin) ? ((m >> 25) & 1u) : (b < ((m >> 16) & 0x1FFu));
+}
+
+// ------------------------------------------------------------------------------------------
+// Packed 16-byte row records (the default for <= 24 features whose codes fit 91 bits; cobalt_pack_layout).
+// Dwords 0, 1 and bits 0..26 of dword 2 hold the F bin codes, each `width` bits at its bit `offset`, no
+// code crossing a dword; width = ceil(log2(nbins + 1)) -- room for the all-ones missing code -- and 8 for a
+// 256-bin feature, whose code 255 is a real bin exactly as in the uint8 layout. Bit 27 of dword 2: the
+// 0/1 label (binary-label fits). The quantised pair: g in dword 3 bits 0..17 (two's complement, |g| <
+// 2^17), h (0 .. 2^17) in dword 3 bits 18..31 (low 14 bits) and dword 2 bits 28..31 (high 4). Half the
+// bytes of the 32-byte record per row: the gradient pass streams 16 B in and out instead of a 32-byte
+// read + a dirtied 32-byte sector, and a histogram gather moves one 16-byte record per lane.
+// ------------------------------------------------------------------------------------------
+constexpr int kPkBinBits = 91;
+constexpr uint32_t kPkLabelBit = 27;
+__device__ __forceinline__ uint32_t pk_code(const uint4& r, uint32_t pk) {
+  const uint32_t off = pk & 0x7Fu, word = off >> 5;
+  const uint32_t w = word == 0 ? r.x : (word == 1 ? r.y : r.z);
+  return __builtin_amdgcn_ubfe(w, off & 31u, (pk >> 8) & 0xFu);
+}
+// The code as the uint8 layout has it (missing -> 255), for the tree walks.
+__device__ __forceinline__ uint32_t pk_bin8(const uint4& r, uint32_t pk) {
+  const uint32_t c = pk_code(r, pk);
+  return c == (1u << ((pk >> 8) & 0xFu)) - 1u ? 255u : c;
+}
+__device__ __forceinline__ int32_t pk_g(const uint4& r) { return ((int32_t)(r.w << 14)) >> 14; }
+__device__ __forceinline__ uint32_t pk_h(const uint4& r) { return (r.w >> 18) | ((r.z >> 28) << 14); }
+__device__ __forceinline__ uint64_t pk_gh(const uint4& r) {  // packed (g, h) as the LDS histograms add it
+  return ((uint64_t)(uint32_t)pk_g(r) << 32) | pk_h(r);
+}
+__device__ __forceinline__ void pk_set_gh(uint4& r, int64_t gq, int64_t hq) {
+  const uint32_t h = (uint32_t)hq;
+  r.w = ((uint32_t)(int32_t)gq & 0x3FFFFu) | (h << 18);
+  r.z = (r.z & 0x0FFFFFFFu) | ((h >> 14) << 28);
 }
 
 // Stage tree `t` (heap-ordered node records) into LDS as {meta, leaf value}.
@@ -794,6 +831,7 @@ struct HistLanes {
 struct HistLaneRaw {
   bool on;
   int sh, nb;
+  uint32_t pk;  // packed records: the feature's code layout (0 otherwise)
 };
 
 __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tree, int f0, int ft) {
@@ -805,6 +843,8 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   const uint8_t fmv = d.fmask[(int64_t)tree * d.F + f];
   const int ly0 = d.layout[f].y;
   const int nb0 = d.nbins[f];
+  const uint32_t pk0 = d.packed ? d.pk[f] : 0u;
+  r.pk = in ? pk0 : 0u;
   r.on = in && fmv != 0;
   const int ly = in ? ly0 : 0;
   r.sh = ly & 7;
@@ -812,10 +852,12 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   return r;
 }
 
-// Per-feature histogram metadata of lane fl's feature: nbins | (copy shift + 3) << 16; a feature past
-// the tile or masked out by colsample gets nbins 0 (the 32-byte path adds it into a trash cell).
+// Per-feature histogram metadata of lane fl's feature: nbins | (copy shift + 3) << 16 | packed-code width
+// << 20 | packed-code bit offset << 24; a feature past the tile or masked out by colsample gets nbins 0
+// (it adds into a trash cell).
 __device__ __forceinline__ uint32_t hist_meta(const HistLaneRaw& raw) {
-  return raw.on ? ((uint32_t)raw.nb | ((uint32_t)(raw.sh + 3) << 16)) : (3u << 16);
+  const uint32_t pkm = ((raw.pk >> 8) & 0xFu) << 20 | (raw.pk & 0x7Fu) << 24;
+  return (raw.on ? ((uint32_t)raw.nb | ((uint32_t)(raw.sh + 3) << 16)) : (3u << 16)) | pkm;
 }
 
 // Stage the metadata of the tile's features in LDS (s_fm[64], lane fl = feature fl) from ONE wave: the
@@ -840,7 +882,7 @@ __device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, i
   for (int fl = 0; fl < 24; ++fl) {
     const uint32_t m = hist_meta_of(s_fm, fl);
     hl.fm[fl] = m;
-    hl.lb8[fl] = (m & 0xffffu) ? ((uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << ((m >> 16) - 3)) - 1u))) * 8u
+    hl.lb8[fl] = (m & 0xffffu) ? ((uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << (((m >> 16) & 15u) - 3)) - 1u))) * 8u
                                : hl.trash * 8u;
   }
   return hl;
@@ -865,9 +907,26 @@ __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes
       const int q = fl >> 2;
       const uint32_t word = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : b.y;
       const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
-      const uint32_t off = hl.lb8[fl] + (min(bb, m & 0xffffu) << (m >> 16));
+      const uint32_t off = hl.lb8[fl] + (min(bb, m & 0xffffu) << ((m >> 16) & 15u));
       atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
     }
+  }
+}
+
+// The same for one packed 16-byte record (d.pk: the features' bit offsets / widths, uniform kernel
+// arguments): per feature one bit-field extract from the record word, then hist_add_rec32's clamp /
+// shift-add / ds_add_u64. Padding features (pk = 0: a 0-bit field) add into the trash cell.
+template <int FT4>
+__device__ __forceinline__ void hist_add_pk(uint64_t* s_hist, const HistLanes& hl, const uint4& r) {
+  static_assert(FT4 % 4 == 0 && FT4 > 0 && FT4 <= 24, "packed records hold <= 24 features");
+  const uint64_t gp = pk_gh(r);
+  char* base = reinterpret_cast<char*>(s_hist);
+#pragma unroll
+  for (int fl = 0; fl < FT4; ++fl) {
+    const uint32_t m = hl.fm[fl];  // nbins | copy shift | code width << 20 | code offset << 24
+    const uint32_t bb = pk_code(r, (m >> 24) | (((m >> 20) & 15u) << 8));
+    const uint32_t off = hl.lb8[fl] + (min(bb, m & 0xffffu) << ((m >> 16) & 15u));
+    atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
   }
 }
 
@@ -945,7 +1004,9 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // holding the freshly quantised (g, h) and the bins -- the separate root histogram pass (a full
 // 32 B/row re-read) disappears. Block b = root work item b: rows [b*chunk, (b+1)*chunk).
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
-template <int U, int FT4>
+// kPk: packed 16-byte records (one 16-byte load and store per row; the walk extracts the split
+// feature's code with its layout entry, staged in LDS because the walk indexes it per lane).
+template <int U, int FT4, bool kPk>
 __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int apply_tree, int chunk) {
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_dyn[];
@@ -960,6 +1021,8 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
   uint64_t* s_hist = s_dyn;
   uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries);
   float* s_leaf = reinterpret_cast<float*>(s_meta + d.max_nodes);
+  __shared__ uint32_t s_pk[kPk ? 24 : 1];  // the features' packed-code layout (the walk indexes it per lane)
+  if (kPk && threadIdx.x < d.F) s_pk[threadIdx.x] = d.pk[threadIdx.x];
   {  // zero the root histogram slot (k_hist_reduce accumulates into it)
     int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[0]);
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
@@ -1001,9 +1064,14 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + (int64_t)u * B;
       const int64_t ii = i < end ? i : begin;
-      const uint4* rec = reinterpret_cast<const uint4*>(d.bins + ii * 32);
-      ra[u] = rec[0];
-      rb[u] = rec[1];
+      if constexpr (kPk) {
+        ra[u] = reinterpret_cast<const uint4*>(d.bins)[ii];
+        rb[u] = make_uint4(0, 0, 0, 0);
+      } else {
+        const uint4* rec = reinterpret_cast<const uint4*>(d.bins + ii * 32);
+        ra[u] = rec[0];
+        rb[u] = rec[1];
+      }
       mf[u] = d.margin[ii];
       yl[u] = 0.0f;
       wt[u] = 0.0f;
@@ -1021,9 +1089,14 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
         uint32_t m = s_meta[0];
         while (m & kMetaSplit) {
           const int f = m & 0xFFFF, q = f >> 2;
-          const uint32_t word = q == 0 ? ra[u].x : q == 1 ? ra[u].y : q == 2 ? ra[u].z : q == 3 ? ra[u].w
-                              : q == 4 ? rb[u].x : rb[u].y;
-          const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
+          uint32_t b;
+          if constexpr (kPk) {
+            b = pk_bin8(ra[u], s_pk[f]);
+          } else {
+            const uint32_t word = q == 0 ? ra[u].x : q == 1 ? ra[u].y : q == 2 ? ra[u].z : q == 3 ? ra[u].w
+                                : q == 4 ? rb[u].x : rb[u].y;
+            b = (word >> (8 * (f & 3))) & 0xffu;
+          }
           const bool left = meta_left(m, b);
           nidx = 2 * nidx + (left ? 1 : 2);
           m = s_meta[nidx];
@@ -1034,7 +1107,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       const double mm = (double)mf[u];
       const double p = d.ablate == 20 ? 0.5 + 0.01 * mm : 1.0 / (1.0 + exp(-mm));  // (20: timing-only, no exp)
       if (d.ylab) {
-        yl[u] = (float)(rb[u].y >> 24);
+        yl[u] = kPk ? (float)((ra[u].z >> kPkLabelBit) & 1u) : (float)(rb[u].y >> 24);
         wt[u] = yl[u] != 0.0f ? d.spw : 1.0f;
       }
       const double y = (double)yl[u];
@@ -1047,12 +1120,18 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       }
       int64_t gq, hq;
       quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq);
-      rb[u].z = (uint32_t)hq;
-      rb[u].w = (uint32_t)(int32_t)gq;
-      reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
       tg += gq;
       th += hq;
-      if (d.ablate != 21) hist_add_rec32<FT4>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
+      if constexpr (kPk) {
+        pk_set_gh(ra[u], gq, hq);
+        reinterpret_cast<uint4*>(d.bins)[i] = ra[u];  // the whole 16-byte record: full lines per wave
+        if (d.ablate != 21) hist_add_pk<FT4>(s_hist, hl, ra[u]);
+      } else {
+        rb[u].z = (uint32_t)hq;
+        rb[u].w = (uint32_t)(int32_t)gq;
+        reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
+        if (d.ablate != 21) hist_add_rec32<FT4>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
+      }
     }
   }
   __syncthreads();
@@ -1062,9 +1141,9 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
 
 // U rows in flight per thread; 2 per CU of 512 threads at 95 VGPRs (no waves-per-EU bound: capping U = 2
 // at 80 VGPRs spills, 276.5 vs 269.7 ms per 10M fit)
-template <int U, int FT4>
+template <int U, int FT4, bool kPk>
 __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
-  grad_hist_body<U, FT4>(d, tree, apply_tree, chunk);
+  grad_hist_body<U, FT4, kPk>(d, tree, apply_tree, chunk);
 }
 
 
@@ -1095,7 +1174,7 @@ __device__ __forceinline__ void hist_rows_pair(const GbdtDev& d, uint64_t* s_his
     const uint32_t m = h ? hl.fm[FH + k] : hl.fm[k];
     const uint32_t fl = (uint32_t)(k + h * FH);
     fmv[k] = m;
-    lbv[k] = (m & 0xffffu) ? (fl * kMaxBins + (hl.lane & ((1u << ((m >> 16) - 3)) - 1u))) * 8u : hl.trash * 8u;
+    lbv[k] = (m & 0xffffu) ? (fl * kMaxBins + (hl.lane & ((1u << (((m >> 16) & 15u) - 3)) - 1u))) * 8u : hl.trash * 8u;
   }
   char* base = reinterpret_cast<char*>(s_hist);
   const int ilast = max(end - 1, begin);
@@ -1145,10 +1224,51 @@ __device__ __forceinline__ void hist_rows_pair(const GbdtDev& d, uint64_t* s_his
 #pragma unroll
       for (int k = 0; k < FH; ++k) {
         const uint32_t bb = (v[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        const uint32_t off = lbv[k] + (min(bb, fmv[k] & 0xffffu) << (fmv[k] >> 16));
+        const uint32_t off = lbv[k] + (min(bb, fmv[k] & 0xffffu) << ((fmv[k] >> 16) & 15u));
         atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
       }
     }
+  }
+}
+
+// Packed 16-byte records: one lane per row, one 16-byte load per row (a wave-instruction gathers 64
+// whole records), U rows in flight per lane with the next rows' ids prefetched one iteration ahead.
+template <int FT4>
+__device__ __forceinline__ void hist_rows_pk(const GbdtDev& d, uint64_t* s_hist, const HistLanes& hl,
+                                             const int32_t* rix, bool identity, int begin, int end, int64_t& tg,
+                                             int64_t& th) {
+  constexpr int U = 6;
+  const int B = (int)blockDim.x;
+  const uint4* recs = reinterpret_cast<const uint4*>(d.bins);
+  const int ilast = max(end - 1, begin);
+  int rn[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = begin + (int)threadIdx.x + u * B;
+    const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
+    rn[u] = i < end ? rv : -1;
+  }
+  for (int i0 = begin + (int)threadIdx.x; i0 < end; i0 += U * B) {
+    int r[U];
+    uint4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = rn[u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = recs[r[u] >= 0 ? r[u] : r[0]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + U * B + u * B;
+      const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
+      rn[u] = i < end ? rv : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r[u] < 0) { x[u].w = 0u; x[u].z &= 0x0FFFFFFFu; }  // no row: a zero pair
+      tg += (int64_t)pk_g(x[u]);
+      th += (int64_t)pk_h(x[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) hist_add_pk<FT4>(s_hist, hl, x[u]);
   }
 }
 
@@ -1156,8 +1276,8 @@ constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 
 // FT4 > 0: 32-byte records with one tile of <= FT4 features (FT4 = F rounded up to 4); 0: generic rows.
 // (6 waves per SIMD = the 3 blocks per CU that the LDS tile allows: keeps the kernel within 80 VGPRs)
-// PAIR: the lane-pair record gathers of hist_rows_pair (FT4 >= 16).
-template <int FT4, bool PAIR>
+// PAIR: the lane-pair record gathers of hist_rows_pair (FT4 >= 16); kPk: packed 16-byte records.
+template <int FT4, bool PAIR, bool kPk = false>
 __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_hist(
     GbdtDev d, int parity, int tree, int level, int chunk) {
   BlockStamp stamp_(d);
@@ -1204,7 +1324,9 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
   constexpr int U = 4;  // rows in flight per thread
-  if constexpr (PAIR) {
+  if constexpr (kPk) {
+    hist_rows_pk<FT4>(d, s_hist, hl, rix, identity, w.begin, w.end, tg, th);
+  } else if constexpr (PAIR) {
     hist_rows_pair<FT4>(d, s_hist, hl, rix, identity, w.begin, w.end, tg, th);
   } else if constexpr (FT4 > 0) {
     // 32-byte records (bins | pad | (g,h)): one pair of 16-byte loads per row
@@ -1297,7 +1419,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
 #pragma unroll
       for (int fl = 0; fl < 32; ++fl) {
         const uint32_t m = fmv[fl];
-        const uint32_t nb = m & 0xffffu, sh3 = m >> 16;
+        const uint32_t nb = m & 0xffffu, sh3 = (m >> 16) & 15u;
         if (nb == 0) continue;  // uniform: masked by colsample, or past the tile
         // as hist_add_rec32: the missing code clamps to the feature's unread cell nbins
         const uint32_t lb8 = ((uint32_t)(fl * kMaxBins) + (lane & ((1u << (sh3 - 3)) - 1u))) * 8u;
@@ -2375,6 +2497,10 @@ struct GbdtCtx {
   std::vector<int32_t> hoff_h;  // host copy of d.hoff (sizes k_eval's fused-exchange LDS)
   int fit_first = 0;            // first tree this context grows in the current fit (no replica check)
   int fault_tree = -1;          // fault injection: tree whose root totals are perturbed on this rank
+  uint32_t* pk_buf = nullptr;   // packed records: the code layout (cobalt_gbdt_set_pack)
+  // the last grow call's plan (cobalt_gbdt_plan): fused IPC exchange, ownership level, packed records,
+  // resident blocks of the fused k_eval, levels run by the fused evaluation + partition pass
+  int32_t plan[5] = {0, -1, 0, 0, 0};
   unsigned* err_pinned = nullptr;  // mapped host word behind d.err_host
   // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
   const char* stamp_path = nullptr;
@@ -2485,9 +2611,18 @@ static int chunk_part(const GbdtDev& d) {
 typedef void (*HistKernel)(GbdtDev, int, int, int, int);
 typedef void (*GradHistKernel)(GbdtDev, int, int, int);
 static int hist_ft4(const GbdtDev& d) {
-  return (d.stride == 32 && d.F <= 24 && d.feat_tile >= d.F) ? (d.F + 3) / 4 * 4 : 0;
+  return ((d.stride == 32 || d.packed) && d.F <= 24 && d.feat_tile >= d.F) ? (d.F + 3) / 4 * 4 : 0;
 }
-static HistKernel hist_kernel(int ft4, bool pair) {
+static HistKernel hist_kernel(int ft4, bool pair, bool packed = false) {
+  if (packed) switch (ft4) {
+    case 4: return k_hist<4, false, true>;
+    case 8: return k_hist<8, false, true>;
+    case 12: return k_hist<12, false, true>;
+    case 16: return k_hist<16, false, true>;
+    case 20: return k_hist<20, false, true>;
+    case 24: return k_hist<24, false, true>;
+    default: return nullptr;
+  }
   switch (ft4) {
     case 4: return k_hist<4, false>;
     case 8: return k_hist<8, false>;
@@ -2498,14 +2633,23 @@ static HistKernel hist_kernel(int ft4, bool pair) {
     default: return k_hist<0, false>;
   }
 }
-static GradHistKernel grad_hist_kernel(int ft4) {
+static GradHistKernel grad_hist_kernel(int ft4, bool packed = false) {
+  if (packed) switch (ft4) {
+    case 4: return k_grad_hist<2, 4, true>;
+    case 8: return k_grad_hist<2, 8, true>;
+    case 12: return k_grad_hist<2, 12, true>;
+    case 16: return k_grad_hist<2, 16, true>;
+    case 20: return k_grad_hist<2, 20, true>;
+    case 24: return k_grad_hist<2, 24, true>;
+    default: return nullptr;
+  }
   switch (ft4) {
-    case 4: return k_grad_hist<2, 4>;
-    case 8: return k_grad_hist<2, 8>;
-    case 12: return k_grad_hist<2, 12>;
-    case 16: return k_grad_hist<2, 16>;
-    case 20: return k_grad_hist<2, 20>;
-    case 24: return k_grad_hist<2, 24>;
+    case 4: return k_grad_hist<2, 4, false>;
+    case 8: return k_grad_hist<2, 8, false>;
+    case 12: return k_grad_hist<2, 12, false>;
+    case 16: return k_grad_hist<2, 16, false>;
+    case 20: return k_grad_hist<2, 20, false>;
+    case 24: return k_grad_hist<2, 24, false>;
     default: return nullptr;
   }
 }
@@ -2535,7 +2679,11 @@ static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
 COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if (cfg->max_depth < 1 || cfg->max_depth > 10) return -1;
   if (cfg->chunk < 64 || cfg->chunk > 16384) return -2;
-  if (cfg->row_stride % 16 != 0 || cfg->row_stride < ((cfg->n_feat + 7) / 8) * 8 + 8) return -3;
+  // row_stride 16: packed 16-byte records (<= 24 features; the layout comes with cobalt_gbdt_set_pack)
+  const bool packed = cfg->row_stride == 16;
+  if (packed ? (cfg->n_feat > 24 || cfg->feat_tile < cfg->n_feat)
+             : (cfg->row_stride % 16 != 0 || cfg->row_stride < ((cfg->n_feat + 7) / 8) * 8 + 8))
+    return -3;
   if (cfg->feat_tile % 4 != 0 || cfg->feat_tile <= 0 || cfg->feat_tile > 64) return -4;
   if (cfg->n_rows >= (int64_t)INT32_MAX) return -5;
   GbdtCtx* c = new GbdtCtx();
@@ -2557,6 +2705,7 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.row_offset = cfg->row_offset;
   d.F = F;
   d.stride = cfg->row_stride;
+  d.packed = packed ? 1 : 0;
   d.goff = ((F + 7) / 8) * 8;
   d.max_depth = cfg->max_depth;
   d.max_nodes = c->max_nodes;
@@ -2618,6 +2767,9 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&c->pk_buf, 24 * sizeof(uint32_t)))) return rc;
+  CK(hipMemset(c->pk_buf, 0, 24 * sizeof(uint32_t)));
+  d.pk = c->pk_buf;
   if ((rc = dev_alloc(c, (void**)&d.hoff, (F + 1) * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.tile_entries, ntiles * sizeof(int32_t)))) return rc;
   d.stamps = nullptr;
@@ -2731,14 +2883,14 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   CK(hipMemcpy(c->d.tile_entries, ent.data(), ntiles * sizeof(int32_t), hipMemcpyHostToDevice));
   c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t);
   if (c->lds_hist > 64 * 1024) {
-    for (int pair = 0; pair < 2; ++pair)
-      CK(hipFuncSetAttribute((const void*)hist_kernel(hist_ft4(c->d), pair != 0),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
+    for (int pair = 0; pair < 3; ++pair)
+      if (HistKernel k = hist_kernel(hist_ft4(c->d), pair == 1, pair == 2))
+        CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
   const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
-  if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d)))
-    CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d)), hipFuncAttributeMaxDynamicSharedMemorySize,
-                           (int)grad_hist_lds));
+  if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0))
+    CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
   return 0;
 }
 
@@ -2783,7 +2935,9 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   }
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const int ft4 = hist_ft4(d);
-  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.ablate == 0 || d.ablate >= 10);
+  // (packed records have no unfused root pass: k_grad reads the 32-byte layout)
+  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.packed || d.ablate == 0 || d.ablate >= 10);
+  if (d.packed && (!fuse_root || sampled)) return -15;
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
   static const int env_fg = knob_int(Knob::EvalFg, -1);
@@ -2801,7 +2955,22 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       fused_cells = std::max(fused_cells, c->hoff_h[std::min(d.F, f0 + eval_fg)] - c->hoff_h[f0]);
   }
   const size_t fused_lds = (size_t)(fused_cells + 2) * 16;  // + the totals and the level-0 digest cells
-  const bool ipc_fused = ipc && env_ipc_fused != 0 && fused_lds <= 65536;
+  // Co-residency guard. The fused exchange waits inside k_eval: every block polls the peers' epoch flags
+  // (each published by block 0 of that rank's launch) and, under node ownership, the owner's record of
+  // the SAME block index -- waits on lower-or-equal block indices of the peers' launches, which in-order
+  // dispatch starts first, so progress does not need a whole grid resident. The launch is still kept to
+  // what this rank's CUs hold at once (occupancy x the CUs of its stream, COBALT_CU_BUDGET on a CU-masked
+  // share of a shared device): a deeper level's grid than that runs the separate exchange kernel instead.
+  int resident = 0;
+  if (ipc) {
+    int per_cu = 0;
+    const void* kf = eval_fg > 0 ? (const void*)k_eval<true, true, true> : (const void*)k_eval<false, true, true>;
+    const int threads = eval_fg > 0 ? ceil_div(eval_fg, 2) * kWave : 1024;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, threads, fused_lds) == hipSuccess)
+      resident = per_cu * device_cu_count();
+  }
+  const int deepest_grid = (1 << (D - 1)) * (eval_fg > 0 ? ceil_div(d.F, eval_fg) : 1);
+  const bool ipc_fused = ipc && env_ipc_fused != 0 && fused_lds <= 65536 && resident >= deepest_grid;
   d.ipc_epoch = 0;
   d.ipcv = ipc_fused ? ipc_device_views(cc) : nullptr;
   // split evaluation fused into the partition pass (k_eval_part): one launch per level fewer, but every
@@ -2825,6 +2994,17 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     d.own_level = l0 < D ? l0 : -1;
   }
   const bool eval_part = env_ep != 0 && !ipc_fused && eval_fg == 0 && ep_steps <= 8 && d.F <= 32;
+  c->plan[0] = ipc_fused ? 1 : 0;
+  c->plan[1] = d.own_level;
+  c->plan[2] = d.packed;
+  c->plan[3] = resident;
+  c->plan[4] = 0;  // levels run by the fused evaluation + partition pass (bit mask, set below)
+  for (int level = 0; level + 1 < D; ++level)
+    if (eval_part) {
+      const int cus = device_cu_count();
+      for (int ch = std::min(4096, chunk_part(d)); ch <= 8192; ch += 1024)
+        if (ceil_div(d.n, ch) + (1 << level) <= cus) { c->plan[4] |= 1 << level; break; }
+    }
   // Item size of a level's fused pass: the grid (items + one partial item per node) fits one 1024-thread
   // block per CU -- beyond that a second round of blocks doubles the level (1M rows with 4096-row items:
   // levels 4-5 launched 261 / 277 blocks on 256 CUs). The smallest item (in 1024-row steps from 4096)
@@ -2874,7 +3054,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
               stream, d);
     else if (fuse_root)
-      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
+      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.packed != 0), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
               stream, d, t, apply, root_chunk);
     else
       GLAUNCH("k_grad", k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
@@ -2896,7 +3076,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       const int ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
                                                : ceil_div(d.n, chh) + (1 << level);
       if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
+        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0, d.packed != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
                 stream, d, parity, t, level, chh);
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       const dim3 rgrid(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256));
@@ -3293,17 +3473,37 @@ __global__ __launch_bounds__(256) void k_put_label(uint8_t* bins, const float* l
     bins[i * 32 + 23] = label[i] != 0.0f ? 1 : 0;
 }
 
+__global__ __launch_bounds__(256) void k_put_label_pk(uint4* recs, const float* label, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint4 r = recs[i];
+    r.z = (r.z & ~(1u << kPkLabelBit)) | ((label[i] != 0.0f ? 1u : 0u) << kPkLabelBit);
+    recs[i] = r;
+  }
+}
+
 COBALT_API int cobalt_gbdt_set_binary_labels(void* h, float spw, hipStream_t stream) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   GbdtDev& d = c->d;
-  if (!d.bins || !d.label || d.stride != 32 || d.F > 23) return -13;
+  if (!d.bins || !d.label || (!d.packed && (d.stride != 32 || d.F > 23))) return -13;
   if (d.n > 0) {
     const int grid = std::min(ceil_div(d.n, 256), 4096);
-    hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
+    if (d.packed)
+      hipLaunchKernelGGL(k_put_label_pk, dim3(grid), dim3(256), 0, stream, reinterpret_cast<uint4*>(d.bins), d.label, d.n);
+    else
+      hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
     CK(hipGetLastError());
   }
   d.ylab = 1;
   d.spw = spw;
+  return 0;
+}
+
+// The packed-record layout (cobalt_pack_layout's out, host memory) of a context created with row_stride 16.
+COBALT_API int cobalt_gbdt_set_pack(void* h, const int32_t* layout) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  if (!c->d.packed || !c->pk_buf) return -3;
+  CK(hipMemcpy(c->pk_buf, layout, c->d.F * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->d.pk = c->pk_buf;
   return 0;
 }
 
@@ -3313,6 +3513,15 @@ COBALT_API int cobalt_gbdt_set_start(void* h, int t0) {
   c->grown = t0;
   c->applied = t0;
   c->fit_first = t0;
+  return 0;
+}
+
+// The last grow call's launch plan (GbdtCtx::plan): out[0] fused IPC exchange, [1] node-ownership level
+// (-1 off), [2] packed records, [3] blocks of the fused k_eval this rank's CUs hold at once, [4] bit mask of
+// the levels run by the fused evaluation + partition pass.
+COBALT_API int cobalt_gbdt_plan(void* h, int32_t* out) {
+  GbdtCtx* c = static_cast<GbdtCtx*>(h);
+  for (int k = 0; k < 5; ++k) out[k] = c->plan[k];
   return 0;
 }
 
@@ -3424,6 +3633,106 @@ __global__ __launch_bounds__(256) void k_bin_rec32(const float* __restrict__ X, 
     rec[0] = make_uint4(w[0], w[1], w[2], w[3]);
     rec[1] = make_uint4(w[4], w[5], 0u, 0u);
   }
+}
+
+// Packed 16-byte records (see pk_code): the layout of F features from their bin counts -- each code
+// ceil(log2(nbins + 1)) bits (8 for 256 bins), placed first-fit in order of decreasing width into
+// dword 0, dword 1 and the low 27 bits of dword 2, never across a dword. out[f] = bit offset | width << 8.
+// Returns 1 when every feature fits (F <= 24), else 0 (the caller keeps 32-byte records).
+COBALT_API int cobalt_pack_layout(const int32_t* nbins, int F, int32_t* out) {
+  if (F < 1 || F > 24) return 0;
+  int cap[3] = {32, 32, (int)kPkLabelBit}, used[3] = {0, 0, 0};
+  std::vector<int> order(F), width(F);
+  for (int f = 0; f < F; ++f) {
+    const int nb = std::max(1, std::min(256, (int)nbins[f]));
+    int w = 1;
+    if (nb >= 256) w = 8;
+    else while ((1 << w) < nb + 1) ++w;
+    width[f] = w;
+    order[f] = f;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return width[a] > width[b]; });
+  for (int f : order) {
+    int k = 0;
+    while (k < 3 && used[k] + width[f] > cap[k]) ++k;
+    if (k == 3) return 0;
+    out[f] = (k * 32 + used[k]) | (width[f] << 8);
+    used[k] += width[f];
+  }
+  return 1;
+}
+
+template <int F4>
+__global__ __launch_bounds__(256) void k_bin_pk(const float* __restrict__ X, int64_t n, const float* __restrict__ cuts,
+                                                const int32_t* __restrict__ nbins, const int32_t* __restrict__ pack,
+                                                uint4* __restrict__ recs, uint8_t* __restrict__ binsT, int64_t ldt) {
+  constexpr int F = 4 * F4;
+  __shared__ float s_cuts[F * kMaxBins];
+  __shared__ int s_nb[F];
+  __shared__ uint32_t s_pk[F];
+  for (int i = threadIdx.x; i < F * kMaxBins; i += blockDim.x) s_cuts[i] = cuts[i];
+  if (threadIdx.x < F) {
+    s_nb[threadIdx.x] = nbins[threadIdx.x];
+    s_pk[threadIdx.x] = (uint32_t)pack[threadIdx.x];
+  }
+  __syncthreads();
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < n;
+       row += (int64_t)gridDim.x * blockDim.x) {
+    const float4* x4 = reinterpret_cast<const float4*>(X + row * F);
+    float v[F];
+#pragma unroll
+    for (int q = 0; q < F4; ++q) {
+      const float4 t = x4[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    }
+    uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      const int nb = s_nb[f];
+      const uint32_t pk = s_pk[f];
+      const uint32_t width = (pk >> 8) & 0xFu, off = pk & 0x7Fu;
+      uint32_t b, code;
+      if (v[f] != v[f]) {
+        b = kMissingBin;
+        code = (1u << width) - 1u;
+      } else {  // upper_bound over cuts[f][0..nb), clamped to nb - 1
+        const float* c = s_cuts + f * kMaxBins;
+        int lo = 0, hi = nb;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (c[mid] <= v[f]) lo = mid + 1; else hi = mid;
+        }
+        b = code = lo >= nb ? (uint32_t)(nb - 1) : (uint32_t)lo;
+      }
+      binsT[(int64_t)f * ldt + row] = (uint8_t)b;
+      const uint32_t k = off >> 5;
+      const uint32_t sh = code << (off & 31u);
+      w[0] |= k == 0 ? sh : 0u;
+      w[1] |= k == 1 ? sh : 0u;
+      w[2] |= k == 2 ? sh : 0u;
+    }
+    recs[row] = make_uint4(w[0], w[1], w[2], 0u);
+  }
+}
+
+// Quantise n rows into packed 16-byte records (layout from cobalt_pack_layout, a device int32 [F]) and the
+// feature-major bins (row pitch ldt). X: 16-byte aligned fp32 rows, F % 4 == 0.
+COBALT_API int cobalt_bin_matrix_pk(const float* X, int64_t n, int F, const float* cuts, const int32_t* nbins,
+                                    const int32_t* pack, void* recs, uint8_t* binsT, int64_t ldt, hipStream_t stream) {
+  if (F % 4 != 0 || F < 4 || F > 24 || ldt < n || (reinterpret_cast<uintptr_t>(X) & 15) != 0 ||
+      (reinterpret_cast<uintptr_t>(recs) & 15) != 0)
+    return -3;
+  if (n == 0) return 0;
+  const int grid = std::max(1, std::min(ceil_div(n, 256), 256 * 8));
+  switch (F / 4) {
+#define BINPK_CASE(K)                                                                                       \
+    case K: hipLaunchKernelGGL(k_bin_pk<K>, dim3(grid), dim3(256), 0, stream, X, n, cuts, nbins, pack,       \
+                               static_cast<uint4*>(recs), binsT, ldt); break;
+    BINPK_CASE(1) BINPK_CASE(2) BINPK_CASE(3) BINPK_CASE(4) BINPK_CASE(5) BINPK_CASE(6)
+#undef BINPK_CASE
+  }
+  CK_LAUNCH();
+  return 0;
 }
 
 COBALT_API int cobalt_bin_matrix_ld(const float* X, int64_t n, int F, int64_t ldx, const float* cuts,

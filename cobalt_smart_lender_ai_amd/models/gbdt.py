@@ -152,6 +152,7 @@ class BinnedData:
     nbins: torch.Tensor
     records: torch.Tensor | None = None
     binsT: torch.Tensor | None = None
+    pack: np.ndarray | None = None          # packed 16-byte records: the code layout (ops/gbdt_ops.pack_layout)
     bins_host: np.ndarray | None = None
     t_sketch: float = 0.0
     t_bin: float = 0.0
@@ -253,9 +254,7 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
         t_sketch = time.perf_counter() - ts
         tb = time.perf_counter()
         bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
-        from ..ops import gbdt_ops
-
-        bd.records, bd.binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
+        _bin_device(bd, Xt, cuts, nbins)
         torch.cuda.synchronize(dev)
         bd.t_bin = time.perf_counter() - tb
         return bd
@@ -280,14 +279,24 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     tb = time.perf_counter()
     bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
     if dev.type == "cuda":
-        from ..ops import gbdt_ops
-
-        bd.records, bd.binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
+        _bin_device(bd, Xt, cuts, nbins)
         torch.cuda.synchronize(dev)
     else:
         bd.bins_host = sketch.bin_matrix_host(Xt.cpu().numpy(), cuts.cpu().numpy(), nbins.cpu().numpy())
     bd.t_bin = time.perf_counter() - tb
     return bd
+
+
+def _bin_device(bd: BinnedData, Xt: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> None:
+    """Binning on the GPU: packed 16-byte row records where the codes fit (the gradient pass and the
+    histogram gathers move half the bytes), else 32-byte records; feature-major bins either way."""
+    from ..ops import gbdt_ops
+
+    pk = gbdt_ops.bin_matrix_packed(Xt, cuts, nbins)
+    if pk is not None:
+        bd.records, bd.binsT, bd.pack = pk
+    else:
+        bd.records, bd.binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
 
 
 def sketch_weights_for(params: "GBDTParams", y, sample_weight=None, device=None):
@@ -306,7 +315,7 @@ def sketch_weights_for(params: "GBDTParams", y, sample_weight=None, device=None)
 def subset_rows(bd: BinnedData, rows: np.ndarray) -> BinnedData:
     """Rows ``rows`` of a binned matrix with the same cuts (CV folds re-use one binning)."""
     idx = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=bd.device)
-    out = BinnedData(bd.device, len(rows), len(rows), bd.n_features, 0, bd.cuts, bd.nbins)
+    out = BinnedData(bd.device, len(rows), len(rows), bd.n_features, 0, bd.cuts, bd.nbins, pack=bd.pack)
     if bd.records is not None:
         out.records = bd.records.index_select(0, idx).contiguous()
         out.binsT = bd.binsT.index_select(1, idx).contiguous()
@@ -329,7 +338,10 @@ def subset_features(bd: BinnedData, feats) -> BinnedData:
         from ..ops import gbdt_ops
 
         rec = torch.zeros((bd.n_rows, gbdt_ops.row_stride(len(f))), dtype=torch.uint8, device=bd.device)
-        rec[:, : len(f)] = bd.records.index_select(1, idx)
+        if bd.pack is not None:  # packed records: the narrower 32-byte records from the feature-major bins
+            rec[:, : len(f)] = bd.binsT.index_select(0, idx).t()
+        else:
+            rec[:, : len(f)] = bd.records.index_select(1, idx)
         out.records = rec
         out.binsT = bd.binsT.index_select(0, idx).contiguous()
     else:
@@ -530,14 +542,18 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                                      reg_lambda=hp.reg_lambda, reg_alpha=hp.reg_alpha, gamma=hp.gamma,
                                      min_child_weight=hp.min_child_weight, subsample=hp.subsample,
                                      gscale=gscale, hscale=hscale, base_margin=base_margin,
-                                     seed=hp.seed, row_offset=bd.row_offset, world_size=world, comm=comm)
+                                     seed=hp.seed, row_offset=bd.row_offset, world_size=world, comm=comm,
+                                     packed=bd.pack is not None)
         fm = torch.as_tensor(fmask_np, device=dev).contiguous()
         tr.set_data(bd.records, bd.binsT, bd.cuts.contiguous(), bd.nbins.to(torch.int32).contiguous(),
                     yt.contiguous(), wt, margin, fm)
+        if bd.pack is not None:
+            tr.set_pack(bd.pack)
         # 0/1 labels and no sample weights: the labels ride in the row records' padding and the weights
         # follow from them (8 fewer bytes per row in every gradient pass); COBALT_LABEL_IN_RECORD=0 off
         if (sample_weight is None and os.environ.get("COBALT_LABEL_IN_RECORD", "1") != "0"
-                and bd.records.shape[1] == 32 and F <= 23 and bool(((yt == 0) | (yt == 1)).all())):
+                and (bd.pack is not None or (bd.records.shape[1] == 32 and F <= 23))
+                and bool(((yt == 0) | (yt == 1)).all())):
             tr.set_binary_labels(float(np.float32(spw)))
         tp = rep.mark("trainer_setup", tp, dev)
         completed = False
@@ -553,6 +569,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
             for s0 in range(T0, T, seg):
                 s1 = min(T, s0 + seg)
                 tr.grow(s0, s1 - s0)
+                rep.extra["plan"] = tr.plan()
                 if world > 1:  # fail fast (abort the communicator) if a peer rank dies mid-segment
                     _watch_segment(dist, dev, s0, s1, tr)
                 tp = rep.mark("grow", tp, dev)

@@ -50,11 +50,21 @@ def interleaved_mask(rank: int, world: int, n_cu: int) -> list[int]:
     return words
 
 
+def blocked_mask(rank: int, world: int, n_cu: int) -> list[int]:
+    """32-bit mask words selecting the contiguous CU range ``[rank n / world, (rank + 1) n / world)``."""
+    words = [0] * ((n_cu + 31) // 32)
+    for cu in range(rank * n_cu // world, (rank + 1) * n_cu // world):
+        words[cu // 32] |= 1 << (cu % 32)
+    return words
+
+
 def shared_device_stream(rank: int, world: int, device: torch.device) -> torch.cuda.ExternalStream:
     """A stream of ``device`` restricted to this rank's 1/world of the CUs; sets ``COBALT_CU_BUDGET``
-    (call before the first fit: the trainer reads it once)."""
+    (call before the first fit: the trainer reads it once). ``COBALT_CU_MASK_LAYOUT``: ``interleaved``
+    (default: CU rank + k * world) or ``blocked`` (a contiguous range; scripts/dp_queue_diag.py)."""
     n_cu = torch.cuda.get_device_properties(device).multi_processor_count
-    words = interleaved_mask(rank, world, n_cu)
+    layout = os.environ.get("COBALT_CU_MASK_LAYOUT", "interleaved")
+    words = blocked_mask(rank, world, n_cu) if layout == "blocked" else interleaved_mask(rank, world, n_cu)
     arr = (ctypes.c_uint32 * len(words))(*words)
     h = ctypes.c_void_p()
     with torch.cuda.device(device):

@@ -71,10 +71,12 @@ def rank_main(rank: int, world: int, port: int, out_dir: str, rows: int, params:
             X, y = synth.make_lendingclub(e - s, seed=seed, row_offset=s, device=dev)
             ck = str(Path(out_dir) / "ckpt.ubj") if checkpoint_every else None
             t1 = time.monotonic()
+            rep = gbdt.FitReport()
             b = gbdt.train(X, y, params, device=dev, dist=ctx, n_rows_global=rows, row_offset=s,
-                           checkpoint_path=ck, checkpoint_every=checkpoint_every, resume=False)
+                           checkpoint_path=ck, checkpoint_every=checkpoint_every, resume=False, report=rep)
             torch.cuda.synchronize(dev)
             res["fit_s"] = time.monotonic() - t1
+            res["plan"] = rep.extra.get("plan")
         raw = b.save_raw("ubj")
         res["model_sha256"] = hashlib.sha256(raw).hexdigest()
         res["trees"] = b.num_trees

@@ -43,9 +43,10 @@ def test_ipc_data_parallel_processes_equal_single_process():
         for g in got:
             assert g["ok"], (procs, env, g)
             assert g["transport"] == "ipc"
-            # one exchange per level per tree, the connect self-test's four (each slot twice) and the final
+            # the connect self-test's four exchanges (each slot twice), the exact sketch's three device
+            # all-reduces, the fit scalars' one, one exchange per level per tree and the final
             # replica-digest exchange of the fit's one grow call
-            assert g["ipc_epochs"] == 4 + 7 * ref["trees"] + 1
+            assert g["ipc_epochs"] == 4 + 3 + 1 + 7 * ref["trees"] + 1
             assert g["model_sha256"] == ref["model_sha256"], (procs, env, g["rank"])
     shallow = dict(dp_check.DEFAULT_PARAMS, max_depth=3)
     ref3 = dp_check.run(1, ROWS, shallow)[0]
@@ -72,7 +73,7 @@ def test_ipc_eight_ranks_share_one_gpu():
     for g in got:
         assert g["ok"], g
         assert g["transport"] == "ipc" and g.get("cu_budget") is None
-        assert g["ipc_epochs"] == 4 + 7 + 1
+        assert g["ipc_epochs"] == 4 + 1 + 7 + 1  # (240k rows: the 2^18-row sample sketch, gathered over gloo)
         assert g["model_sha256"] == ref["model_sha256"], g["rank"]
 
 
@@ -112,6 +113,27 @@ def test_ipc_replica_divergence_fails_every_rank():
     # the same fit without the fault: the check stays quiet
     got = dp_check.run(2, 200_000, params, checkpoint_every=1, timeout_s=300)
     assert all(g["ok"] for g in got), got
+
+
+@pytest.mark.timeout(600)
+def test_cu_budget_below_the_exchange_grid_falls_back_to_the_separate_exchange():
+    """Co-residency guard (csrc/gbdt.hip grow_impl): when this rank's CUs cannot hold the deepest level's
+    fused-exchange grid at once (here a CU budget of 16 against 64 blocks of 1024 threads), the trainer
+    runs the separate exchange kernel + the fused evaluation / partition pass instead -- the same model,
+    reported in the launch plan; with the whole device the fused exchange and node ownership are used."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    ref = dp_check.run(1, ROWS)[0]
+    assert ref["ok"], ref
+    for env, fused in (({"COBALT_SHARED_CU_MASK": "0", "COBALT_CU_BUDGET": "16"}, False),
+                       ({"COBALT_SHARED_CU_MASK": "0"}, True)):
+        got = dp_check.run(2, ROWS, timeout_s=400, env=env)
+        for g in got:
+            assert g["ok"], (env, g)
+            assert g["plan"]["ipc_fused"] is fused, (env, g["plan"])
+            assert (g["plan"]["own_level"] >= 0) is fused, (env, g["plan"])
+            assert g["model_sha256"] == ref["model_sha256"], (env, g["rank"])
 
 
 @pytest.mark.timeout(600)

@@ -1,57 +1,78 @@
-"""Data-parallel training over >= 2 GPUs (one process per GPU, RCCL): the model equals the 1-GPU fit
-byte for byte. The file sorts first so its ranks are spawned before
-this process initialises HIP (a spawn from an initialised process is refused on the pool). Skipped on
-single-GPU hosts (the 1-rank RCCL protocol test in test_gpu_gbdt.py and
-the 2-rank gloo test in test_gbdt_cpu.py cover the protocol there)."""
+"""Data-parallel training over physical GPUs (one process per GPU): the model equals the 1-GPU fit byte
+for byte, for every rank count an 8-GPU node runs (2, 4, 8 <= device_count) over both transports --
+the IPC one-shot exchange across GPUs (gloo bootstrap + the native IPC group; the default within a
+node) and RCCL (nccl bootstrap + the native RCCL communicator) -- at depth 7, so node ownership is
+active on the deep levels of the IPC runs. The ranks run in spawned processes (parallel/dp_check.py);
+this file sorts first so the pytest process has not initialised HIP when it spawns them. On a 1-GPU box
+every case skips (tests/test_00gpu_dp_ipc.py covers processes sharing one GPU, test_gpu_gbdt.py the
+1-rank protocols)."""
+import json
 import os
-import socket
+import subprocess
+import sys
+from pathlib import Path
 
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
-PARAMS = dict(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9, colsample_bytree=0.8,
-              random_state=5, scale_pos_weight=6.0)
+ROOT = Path(__file__).resolve().parents[1]
 N = 400_000
 
 
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _params(trees=6):
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    return dict(dp_check.DEFAULT_PARAMS, n_estimators=trees)
 
 
-def _worker(rank, world, port, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    from cobalt_smart_lender_ai_amd.dataio import synth
-    from cobalt_smart_lender_ai_amd.models import gbdt
-    from cobalt_smart_lender_ai_amd.parallel import dist as pdist
-
-    ctx = pdist.init_from_env()
-    dev = torch.device("cuda", rank)
-    s, e = pdist.shard_range(N, rank, world)
-    X, y = synth.make_lendingclub(e - s, seed=3, row_offset=s, device=dev)
-    b = gbdt.train(X, y, PARAMS, device=dev, dist=ctx, n_rows_global=N, row_offset=s)
-    if rank == 0:
-        with open(out, "wb") as fh:
-            fh.write(b.save_raw("ubj"))
-    pdist.shutdown()
+def _expected_ipc_epochs(trees: int) -> int:
+    # connect self-test (4) + the exact sketch's three device all-reduces + the fit scalars' one +
+    # one exchange per level per tree + the final replica-digest exchange of the fit's one grow call
+    return 4 + 3 + 1 + 7 * trees + 1
 
 
-@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 GPUs")
-@pytest.mark.timeout(600)
-def test_two_gpu_data_parallel_equals_single_gpu(tmp_path):
-    import torch.multiprocessing as mp
-
-    from cobalt_smart_lender_ai_amd.dataio import synth
-    from cobalt_smart_lender_ai_amd.models import gbdt
-
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("transport", ["ipc", "rccl"])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_multi_gpu_data_parallel_equals_single_gpu(world, transport):
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs")
     if torch.cuda.is_initialized():
         pytest.skip("HIP already initialised in this process; run this file on its own")
-    out = str(tmp_path / "dp.ubj")
-    mp.spawn(_worker, args=(2, _port(), out), nprocs=2, join=True)
-    X, y = synth.make_lendingclub(N, seed=3, device="cuda:0")
-    ref = gbdt.train(X, y, PARAMS, device="cuda:0").save_raw("ubj")
-    assert open(out, "rb").read() == ref
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    ref = dp_check.run(1, N, _params())[0]
+    assert ref["ok"], ref
+    got = dp_check.run(world, N, _params(), transport=transport, one_gpu_per_rank=True, timeout_s=600)
+    for g in got:
+        assert g["ok"], g  # (a replica divergence would raise on every rank: the in-flight digest check)
+        assert g["transport"] == transport, g
+        assert g["model_sha256"] == ref["model_sha256"], (world, transport, g["rank"])
+        if transport == "ipc":
+            assert g["ipc_epochs"] == _expected_ipc_epochs(ref["trees"]), g
+
+
+@pytest.mark.timeout(900)
+def test_torchrun_bench_on_every_gpu():
+    """The driver's multi-GPU bench command on this node's GPUs: one JSON line, every rank holds the same
+    model, and the AUC equals the 1-GPU bench's on the same rows (same trees)."""
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs >= 2 GPUs")
+    if torch.cuda.is_initialized():
+        pytest.skip("HIP already initialised in this process; run this file on its own")
+    common = ["--rows", "1000000", "--steps", "1", "--warmup", "1", "--test-rows", "100000"]
+    env = {**os.environ, "MASTER_ADDR": "127.0.0.1"}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                        "--master-addr", "127.0.0.1", "--master-port", "29631", "bench.py", "--gpus", str(n), *common],
+                       cwd=ROOT, capture_output=True, text=True, timeout=800, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    multi = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    r1 = subprocess.run([sys.executable, "bench.py", *common], cwd=ROOT, capture_output=True, text=True, timeout=600,
+                        env=env)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    one = json.loads([ln for ln in r1.stdout.splitlines() if ln.startswith("{")][-1])
+    assert multi["n_gpus"] == n and multi["replicas_agree"] is True, multi
+    assert multi["auc"] == one["auc"], (multi["auc"], one["auc"])
