@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """SMOTE kNN at the full-data minority size (~295k rows x 20 features, k=5 + self) on the MFMA distance
-kernel (csrc/knn.hip) -- the workload of scripts/gpu_pmc_knn.sh."""
+kernel (csrc/knn.hip)."""
 import sys
 import time
 from pathlib import Path

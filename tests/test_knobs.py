@@ -12,8 +12,8 @@ def test_native_getenv_only_in_the_registry():
     for p in sorted((PKG / "csrc").glob("*")):
         for i, line in enumerate(p.read_text().splitlines(), 1):
             if "getenv(" in line and not line.lstrip().startswith("//"):
-                calls.append(f"{p.name}:{i}")
-    assert calls == ["knobs.cpp:19"], calls
+                calls.append(p.name)
+    assert calls == ["knobs.cpp"], calls
 
 
 def test_native_registry_names_are_documented():
