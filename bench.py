@@ -55,6 +55,8 @@ def main() -> None:
     ap.add_argument("--sketch-rows", type=int, default=0,
                     help="rows of the quantile-sketch sample; 0 (default) = every row, the exact device sketch "
                          "(XGBoost hist's all-row semantics; csrc/sketch.hip)")
+    ap.add_argument("--grad-bits", type=int, default=17, choices=[17, 25],
+                    help="fixed-point gradient bits: 17 (packed u64 histogram cells, default) or 25 (int64 cells)")
     a = ap.parse_args()
 
     from cobalt_smart_lender_ai_amd.dataio import synth
@@ -89,7 +91,7 @@ def main() -> None:
     spw = (n_global - pos) / pos
     params = gbdt.GBDTParams(n_estimators=a.trees, max_depth=a.depth, learning_rate=0.05, gamma=5.0,
                              reg_lambda=1.0, min_child_weight=1.0, max_bin=256, scale_pos_weight=spw,
-                             random_state=78, sketch_rows=a.sketch_rows or None)
+                             random_state=78, sketch_rows=a.sketch_rows or None, grad_bits=a.grad_bits)
 
     def fit():
         rep = gbdt.FitReport(sync_phases=a.profile_fit)
@@ -171,8 +173,8 @@ def main() -> None:
             "scaling": a.scaling,
             "vs_baseline": None if BASELINE_ROWS_PER_S is None else value / BASELINE_ROWS_PER_S,
             "dtype": "fp32",
-            "precision": "fp32 features; fp64 gradient math quantised to 17-bit dithered (unbiased) fixed point; "
-                         "exact int64 histogram sums; fp64 split gains",
+            "precision": f"fp32 features; fp64 gradient math quantised to {a.grad_bits}-bit dithered (unbiased) fixed "
+                         "point; exact int64 histogram sums; fp64 split gains",
             "data": "synthetic LendingClub-shaped (20 deployed features, 12.9% positives), generated on device",
             "config": {
                 "model": f"GBDT binary:logistic, {a.trees} trees depth {a.depth} eta 0.05 gamma 5 lambda 1 max_bin 256 "

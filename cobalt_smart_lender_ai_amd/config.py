@@ -157,6 +157,7 @@ KNOBS: dict[str, Knob] = {
     # -- data parallelism --
     "COBALT_IPC_FUSED": Knob("1", "native", "IPC exchange fused into the split evaluation (0: separate exchange kernel + fused eval/partition)"),
     "COBALT_DP_OWNER": Knob("1", "native", "node ownership on the three deepest levels over the fused IPC exchange"),
+    "COBALT_DP_EVAL_PART": Knob("1", "native", "fused IPC exchange: evaluator blocks + partition items in one pass while the grid fits the CUs (0 off)"),
     "COBALT_CU_BUDGET": Knob("", "native", "CUs of this rank's CU-masked stream (set by parallel/cumask.py)"),
     "COBALT_DP_TRANSPORT": Knob("auto", "python", "native communicator: auto (IPC within a node), ipc or rccl"),
     "COBALT_DIST_BACKEND": Knob("auto", "python", "torch.distributed backend override (gloo for ranks sharing one GPU)"),

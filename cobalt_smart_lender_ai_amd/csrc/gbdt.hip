@@ -132,6 +132,8 @@ struct GbdtConfig {
   int32_t world_size;
   uint64_t seed;
   void* comm;            // native RCCL communicator (cobalt_comm_*) or nullptr
+  int32_t grad_bits;     // quantised (g, h) magnitude bits: 17 (packed u64 LDS cells) or 25 (wide cells)
+  int32_t packed;        // 1: packed 16-byte row records (row_stride 16, the layout via cobalt_gbdt_set_pack)
 };
 
 struct GbdtDev {
@@ -219,6 +221,11 @@ struct GbdtDev {
   // feature f's code (device memory; the histogram kernels fold it into their per-feature metadata word)
   int32_t packed;
   const uint32_t* pk;
+  // k_eval_part<.., 2>: per-node decision granules {launch tag, decision} (decision_word)
+  uint64_t* dec;
+  // wide gradients (grad_bits 25): |g_q| < 2^25, h_q <= 2^25, and the LDS histograms hold a cell as two
+  // int64 words (g, h) -- ds_add_u64 each -- instead of one packed u64; slabs likewise (see kWide)
+  int32_t wide;
 };
 
 
@@ -351,7 +358,10 @@ __global__ __launch_bounds__(256) void k_bin(const float* __restrict__ X, int64_
 // to 0 and rounding errors of histogram sums average out instead of accumulating a bias. The draw is
 // deterministic (same trees on every device and rank count). Bounds: a <= 16384-row histogram block
 // sums to |sum g| < 2^31 and sum h <= 2^31, so the packed u64 (signed g high, h low) never carries.
+// Wide gradients (GbdtConfig::grad_bits 25): 25-bit magnitudes, summed in int64 cells (a 16384-row block
+// < 2^39; 10M rows < 2^49, exact in the host oracle's float64 sums too).
 constexpr int64_t kGClip = (1 << 17) - 1, kHClip = 1 << 17;
+constexpr int64_t kGClipW = (1 << 25) - 1, kHClipW = 1 << 25;
 constexpr uint64_t kDitherSalt = 0xD1B54A32D192ED03ull;
 
 __device__ __forceinline__ uint64_t tree_key_of(uint64_t seed, int tree) {
@@ -359,14 +369,15 @@ __device__ __forceinline__ uint64_t tree_key_of(uint64_t seed, int tree) {
 }
 
 __device__ __forceinline__ void quantize_gh(double g, double h, double gscale, double hscale, uint64_t dkey,
-                                            int64_t grow, int64_t& gq, int64_t& hq) {
+                                            int64_t grow, int64_t& gq, int64_t& hq, bool wide = false) {
   const uint64_t r = splitmix64(dkey ^ (uint64_t)grow);
   const double ug = (double)(uint32_t)(r >> 32) * (1.0 / 4294967296.0);
   const double uh = (double)(uint32_t)r * (1.0 / 4294967296.0);
   gq = (int64_t)floor(g * gscale + ug);
   hq = (int64_t)floor(h * hscale + uh);
-  gq = gq > kGClip ? kGClip : (gq < -kGClip ? -kGClip : gq);
-  hq = hq > kHClip ? kHClip : (hq < 0 ? 0 : hq);
+  const int64_t gc = wide ? kGClipW : kGClip, hc = wide ? kHClipW : kHClip;
+  gq = gq > gc ? gc : (gq < -gc ? -gc : gq);
+  hq = hq > hc ? hc : (hq < 0 ? 0 : hq);
 }
 // Reset the node table of a new tree (root active with all local rows) and the per-node counters.
 __device__ void init_tree_block(const GbdtDev& d) {
@@ -526,7 +537,7 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
       if (!(uniform01(hsh) < d.subsample)) { g = 0.0; h = 0.0; }
     }
     int64_t gq, hq;
-    quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq);
+    quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq, d.wide != 0);
     if (rec32) {
       rb.z = (uint32_t)hq;
       rb.w = (uint32_t)(int32_t)gq;
@@ -852,12 +863,12 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   return r;
 }
 
-// Per-feature histogram metadata of lane fl's feature: nbins | (copy shift + 3) << 16 | packed-code width
-// << 20 | packed-code bit offset << 24; a feature past the tile or masked out by colsample gets nbins 0
-// (it adds into a trash cell).
-__device__ __forceinline__ uint32_t hist_meta(const HistLaneRaw& raw) {
+// Per-feature histogram metadata of lane fl's feature: nbins | (copy shift + cs) << 16 | packed-code
+// width << 20 | packed-code bit offset << 24 (cs = log2 of the LDS cell bytes: 3, or 4 for wide cells);
+// a feature past the tile or masked out by colsample gets nbins 0 (it adds into a trash cell).
+__device__ __forceinline__ uint32_t hist_meta(const HistLaneRaw& raw, uint32_t cs = 3) {
   const uint32_t pkm = ((raw.pk >> 8) & 0xFu) << 20 | (raw.pk & 0x7Fu) << 24;
-  return (raw.on ? ((uint32_t)raw.nb | ((uint32_t)(raw.sh + 3) << 16)) : (3u << 16)) | pkm;
+  return (raw.on ? ((uint32_t)raw.nb | ((uint32_t)raw.sh + cs) << 16) : (cs << 16)) | pkm;
 }
 
 // Stage the metadata of the tile's features in LDS (s_fm[64], lane fl = feature fl) from ONE wave: the
@@ -865,15 +876,16 @@ __device__ __forceinline__ uint32_t hist_meta(const HistLaneRaw& raw) {
 // mask (a readlane of a lane that is inactive where the compiler places it would read a stale VGPR).
 // A caller's later barrier publishes it. Using the block's last wave keeps wave 0 -- the work planner
 // -- from waiting on the metadata loads before it issues the plan's.
-__device__ __forceinline__ void hist_meta_store(const HistLaneRaw& raw, uint32_t* s_fm) {
-  if (wave_id() == (int)(blockDim.x / kWave) - 1) s_fm[lane_id()] = hist_meta(raw);
+__device__ __forceinline__ void hist_meta_store(const HistLaneRaw& raw, uint32_t* s_fm, uint32_t cs = 3) {
+  if (wave_id() == (int)(blockDim.x / kWave) - 1) s_fm[lane_id()] = hist_meta(raw, cs);
 }
 
 __device__ __forceinline__ uint32_t hist_meta_of(const uint32_t* s_fm, int fl) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fm[fl]);
 }
 
-__device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, int ft, const uint32_t* s_fm) {
+__device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, int ft, const uint32_t* s_fm,
+                                                       uint32_t cs = 3) {
   HistLanes hl;
   hl.lane = lane_id();
   hl.fbits = __ballot(raw.on);
@@ -882,8 +894,8 @@ __device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, i
   for (int fl = 0; fl < 24; ++fl) {
     const uint32_t m = hist_meta_of(s_fm, fl);
     hl.fm[fl] = m;
-    hl.lb8[fl] = (m & 0xffffu) ? ((uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << (((m >> 16) & 15u) - 3)) - 1u))) * 8u
-                               : hl.trash * 8u;
+    hl.lb8[fl] = (m & 0xffffu) ? ((uint32_t)(fl * kMaxBins) + (hl.lane & ((1u << (((m >> 16) & 15u) - cs)) - 1u))) << cs
+                               : hl.trash << cs;
   }
   return hl;
 }
@@ -894,11 +906,13 @@ __device__ __forceinline__ HistLanes hist_lanes_finish(const HistLaneRaw& raw, i
 // 255 clamps to cell nbins, which the layout keeps inside the feature's 256 cells and the flush never
 // reads (a 256-bin feature has no missing values: its code 255 is a real bin); features masked out by
 // colsample, and the tile's padding up to FT4 (= features rounded up to 4), add into a trash cell.
-template <int FT4>
+// kWide: 16-byte cells {int64 g, int64 h}, two ds_add_u64 per (row, feature).
+template <int FT4, bool kWide = false>
 __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes& hl, const uint4& a,
                                                const uint4& b) {
   static_assert(FT4 % 4 == 0 && FT4 > 0 && FT4 <= 24, "32-byte records hold <= 24 bins");
   const uint64_t gp = ((uint64_t)b.w << 32) | b.z;
+  const uint64_t gw = (uint64_t)(int64_t)(int32_t)b.w, hw = (uint64_t)b.z;
   char* base = reinterpret_cast<char*>(s_hist);
 #pragma unroll
   for (int fl = 0; fl < FT4; ++fl) {
@@ -908,7 +922,12 @@ __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes
       const uint32_t word = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : b.y;
       const uint32_t bb = (word >> (8 * (fl & 3))) & 0xffu;
       const uint32_t off = hl.lb8[fl] + (min(bb, m & 0xffffu) << ((m >> 16) & 15u));
-      atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
+      if constexpr (kWide) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gw);
+        atomicAdd(reinterpret_cast<unsigned long long*>(base + off + 8), (unsigned long long)hw);
+      } else {
+        atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
+      }
     }
   }
 }
@@ -962,6 +981,7 @@ __device__ __forceinline__ void flush_meta_store(const FlushMeta& m, int ft, int
   if (t < ft) s_fs[t] = m.fs;
 }
 
+template <bool kWide = false>
 __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistLanes& hl, int item, int f0, int ft,
                            int64_t tg, int64_t th, bool tot_block, int64_t (*s_tot)[16], const int* s_fo,
                            const int* s_fs) {
@@ -970,7 +990,8 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
   // measured slower at 1M rows: 20.3 vs 18.7 us per k_hist, the 64-bit shuffles of the 64-copy binary
   // features go through ds_bpermute and cost more LDS cycles than the reads they replace.)
   const int c0 = s_fo[0], c1 = s_fo[ft];
-  uint64_t* slab = d.slab + (int64_t)item * d.ncells;
+  constexpr int kW = kWide ? 2 : 1;  // u64 words per cell
+  uint64_t* slab = d.slab + (int64_t)item * d.ncells * kW;
   for (int e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
     int lo = 0, hi = ft - 1;  // largest fl with s_fo[fl] <= e
     while (lo < hi) {
@@ -978,12 +999,16 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
       if (s_fo[mid] <= e) lo = mid; else hi = mid - 1;
     }
     const int sh = s_fs[lo];
-    uint64_t v = 0;
+    uint64_t v = 0, v2 = 0;
     if (sh >= 0) {
-      const uint64_t* cell = s_hist + lo * kMaxBins + ((e - s_fo[lo]) << sh);
-      for (int c = 0; c < (1 << sh); ++c) v += cell[c];
+      const uint64_t* cell = s_hist + (lo * kMaxBins + ((e - s_fo[lo]) << sh)) * kW;
+      for (int c = 0; c < (1 << sh); ++c) {
+        v += cell[c * kW];
+        if (kWide) v2 += cell[c * kW + 1];
+      }
     }
-    store_wt(slab + e, v, (d.wt & 1) != 0);
+    store_wt(slab + (int64_t)e * kW, v, (d.wt & 1) != 0);
+    if (kWide) store_wt(slab + (int64_t)e * kW + 1, v2, (d.wt & 1) != 0);
   }
   if (tot_block) {
     tg = wave_sum(tg);
@@ -1006,8 +1031,11 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
 // kPk: packed 16-byte records (one 16-byte load and store per row; the walk extracts the split
 // feature's code with its layout entry, staged in LDS because the walk indexes it per lane).
-template <int U, int FT4, bool kPk>
+template <int U, int FT4, bool kPk, bool kWide>
 __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int apply_tree, int chunk) {
+  static_assert(!(kPk && kWide), "wide gradients use 32-byte records");
+  constexpr int kW = kWide ? 2 : 1;            // u64 words per LDS cell
+  constexpr uint32_t kCs = kWide ? 4u : 3u;    // log2 of the cell bytes
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_dyn[];
   __shared__ int64_t s_tot[2][16];
@@ -1019,7 +1047,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
   const HistLaneRaw lraw = hist_lanes_load(d, tree, 0, ft);
   const FlushMeta fmeta = flush_meta_load(d, tree, 0, ft);
   uint64_t* s_hist = s_dyn;
-  uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries);
+  uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries * kW);
   float* s_leaf = reinterpret_cast<float*>(s_meta + d.max_nodes);
   __shared__ uint32_t s_pk[kPk ? 24 : 1];  // the features' packed-code layout (the walk indexes it per lane)
   if (kPk && threadIdx.x < d.F) s_pk[threadIdx.x] = d.pk[threadIdx.x];
@@ -1040,9 +1068,9 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
     init_tree_block(d);
     if (threadIdx.x == 0) d.counters[0] = gridDim.x;
   }
-  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
+  for (int i = threadIdx.x; i < entries * kW; i += blockDim.x) s_hist[i] = 0ull;
   flush_meta_store(fmeta, ft, s_fo, s_fs);
-  hist_meta_store(lraw, s_fm);
+  hist_meta_store(lraw, s_fm, kCs);
   __syncthreads();
   stamp_.probe(1);
   const int item = blockIdx.x;
@@ -1052,7 +1080,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
     w.node = 0; w.slot = 0; w.begin = (int32_t)begin; w.end = (int32_t)end;
     d.items_h[item] = w;
   }
-  const HistLanes hl = hist_lanes_finish(lraw, ft, s_fm);
+  const HistLanes hl = hist_lanes_finish(lraw, ft, s_fm, kCs);
   const uint64_t tree_key = tree_key_of(d.seed, tree);
   const uint64_t dkey = splitmix64(tree_key ^ kDitherSalt);
   int64_t tg = 0, th = 0;
@@ -1119,7 +1147,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
         if (!(uniform01(hsh) < d.subsample)) { g = 0.0; h = 0.0; }
       }
       int64_t gq, hq;
-      quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq);
+      quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq, kWide);
       tg += gq;
       th += hq;
       if constexpr (kPk) {
@@ -1130,20 +1158,20 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
         rb[u].z = (uint32_t)hq;
         rb[u].w = (uint32_t)(int32_t)gq;
         reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
-        if (d.ablate != 21) hist_add_rec32<FT4>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
+        if (d.ablate != 21) hist_add_rec32<FT4, kWide>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
       }
     }
   }
   __syncthreads();
   stamp_.probe(2);
-  hist_flush(d, s_hist, hl, item, 0, ft, tg, th, true, s_tot, s_fo, s_fs);
+  hist_flush<kWide>(d, s_hist, hl, item, 0, ft, tg, th, true, s_tot, s_fo, s_fs);
 }
 
 // U rows in flight per thread; 2 per CU of 512 threads at 95 VGPRs (no waves-per-EU bound: capping U = 2
 // at 80 VGPRs spills, 276.5 vs 269.7 ms per 10M fit)
-template <int U, int FT4, bool kPk>
+template <int U, int FT4, bool kPk, bool kWide = false>
 __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
-  grad_hist_body<U, FT4, kPk>(d, tree, apply_tree, chunk);
+  grad_hist_body<U, FT4, kPk, kWide>(d, tree, apply_tree, chunk);
 }
 
 
@@ -1277,9 +1305,14 @@ constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 // FT4 > 0: 32-byte records with one tile of <= FT4 features (FT4 = F rounded up to 4); 0: generic rows.
 // (6 waves per SIMD = the 3 blocks per CU that the LDS tile allows: keeps the kernel within 80 VGPRs)
 // PAIR: the lane-pair record gathers of hist_rows_pair (FT4 >= 16); kPk: packed 16-byte records.
-template <int FT4, bool PAIR, bool kPk = false>
-__global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_hist(
+// kWide: wide gradients (16-byte LDS cells; the one-lane-per-row 32-byte path only).
+// (wide cells: one block per CU by LDS, 2 waves per SIMD -- twice the rows in flight per thread instead)
+template <int FT4, bool PAIR, bool kPk = false, bool kWide = false>
+__global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(kWide ? 2 : 6))) void k_hist(
     GbdtDev d, int parity, int tree, int level, int chunk) {
+  static_assert(!kWide || (FT4 > 0 && !PAIR && !kPk), "wide cells: 32-byte records, one lane per row");
+  constexpr int kW = kWide ? 2 : 1;
+  constexpr uint32_t kCs = kWide ? 4u : 3u;
   BlockStamp stamp_(d);
   extern __shared__ uint64_t s_hist[];
   __shared__ int64_t s_tot[2][16];
@@ -1295,9 +1328,9 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
   const HistLaneRaw lraw = hist_lanes_load(d, tree, f0, ft);
   const FlushMeta fmeta = flush_meta_load(d, tree, f0, ft);
   const int entries = ft * kMaxBins + kWave;  // tile_entries[y] == ft * 256, + per-lane trash cells
-  for (int i = threadIdx.x; i < entries; i += blockDim.x) s_hist[i] = 0ull;
+  for (int i = threadIdx.x; i < entries * kW; i += blockDim.x) s_hist[i] = 0ull;
   __shared__ uint32_t s_fm[kWave];
-  hist_meta_store(lraw, s_fm);  // (last wave; block_plan's barrier publishes it)
+  hist_meta_store(lraw, s_fm, kCs);  // (last wave; block_plan's barrier publishes it)
   const PlanOut pl = block_plan(n_ent, chunk, item, [&](int p) { return hist_entry(d, level, p); },
                                 s_plan);
   // after the plan (storing first would wait for the metadata before the plan's loads go out); the
@@ -1313,7 +1346,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
   w.end = pl.end;
   if (blockIdx.y == 0 && threadIdx.x == 0) d.items_h[item] = w;
   if (d.ablate == 4) return;  // timing-only: plan + publish only
-  const HistLanes hl = hist_lanes_finish(lraw, ft, s_fm);
+  const HistLanes hl = hist_lanes_finish(lraw, ft, s_fm, kCs);
   const uint64_t fbits = hl.fbits;
   stamp_.probe(2);
 
@@ -1323,7 +1356,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
   const int lane = lane_id();
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
-  constexpr int U = 4;  // rows in flight per thread
+  constexpr int U = kWide ? 8 : 4;  // rows in flight per thread
   if constexpr (kPk) {
     hist_rows_pk<FT4>(d, s_hist, hl, rix, identity, w.begin, w.end, tg, th);
   } else if constexpr (PAIR) {
@@ -1367,7 +1400,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
         th += (int64_t)b2[u].z;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) hist_add_rec32<FT4>(s_hist, hl, a[u], b2[u]);
+      for (int u = 0; u < U; ++u) hist_add_rec32<FT4, kWide>(s_hist, hl, a[u], b2[u]);
     }
   } else {
     // Generic records (F > 24: the RFE stage's wide fits, or F <= 8): the tile's <= 32 bins are bytes
@@ -1440,7 +1473,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(6)
   // Per-item partial histogram -> slab (plain coalesced stores; the packed u64 of the K copies can
   // be summed directly because the per-item sums obey the same < 2^31 / < 2^32 bounds).
   if (d.ablate == 2) return;  // timing-only: no flush
-  hist_flush(d, s_hist, hl, item, f0, ft, tg, th, blockIdx.y == 0, s_tot, s_fo, s_fs);
+  hist_flush<kWide>(d, s_hist, hl, item, f0, ft, tg, th, blockIdx.y == 0, s_tot, s_fo, s_fs);
 }
 
 // Reduce the per-item slabs into the level's histogram slots: thread = one compact (feature, bin)
@@ -1472,6 +1505,15 @@ __global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int 
       slot[k] = d.items_h[it].slot;
       g[k] = d.slab_tot[2 * it];
       h[k] = d.slab_tot[2 * it + 1];
+    }
+  } else if (d.wide) {  // 16-byte slab cells {g, h}
+#pragma unroll
+    for (int k = 0; k < kRedItems; ++k) {
+      const int it = min(i0 + k, n_grid - 1);
+      slot[k] = d.items_h[it].slot;
+      const longlong2 v = reinterpret_cast<const longlong2*>(d.slab)[(int64_t)it * ncell + cell];
+      g[k] = v.x;
+      h[k] = v.y;
     }
   } else {
     uint64_t v[kRedItems];
@@ -2360,25 +2402,85 @@ __device__ __forceinline__ bool split_decision(const GbdtDev& d, const Cand& bes
   return ok;
 }
 
-// kDP: data parallel with the level's global histograms already in hist_b (RCCL / the separate IPC
-// exchange kernel): every active node gets an item (possibly empty), so each rank finalises every node
-// of the level, also those it holds no rows of; the replica digest is kept.
-template <int kSteps, bool kDP>
+// A node's split decision as ONE 8-byte granule {tag, decision} (kMode 2): written by the node's
+// evaluator block with a write-through store, polled by the node's partition blocks.
+__device__ __forceinline__ uint64_t decision_word(uint32_t tag, bool ok, bool fail, int f, int j, bool dl) {
+  const uint32_t v = (ok ? 1u : 0u) | (fail ? 2u : 0u) | (dl ? 4u : 0u) | ((uint32_t)(j + 1) & 0x3FFu) << 3 |
+                     (uint32_t)f << 13;
+  return ((uint64_t)tag << 32) | v;
+}
+
+// kMode 0: one GPU. 1: data parallel with the level's global histograms already in hist_b (RCCL / the
+// separate IPC exchange kernel): every block evaluates its node. In both, every active node gets an
+// item (possibly empty, kMode 1), so each rank finalises every node of the level, also those it holds no
+// rows of.
+// kMode 2: data parallel over the fused IPC exchange. Blocks 0 .. 2^level - 1 are the level's EVALUATOR
+// blocks -- one per node position, exactly k_eval<false, true, true>: the exchange (block 0 publishes,
+// every evaluator sums its node's cells over the ranks), node ownership on the deep levels, the replica
+// digest -- and each publishes its node's decision granule; the blocks after them are the partition
+// items, which plan and load their row ids while the evaluation runs and then poll their node's granule
+// (one lane, bounded by the group's deadline). One evaluation per node (no xGMI traffic multiplied by the
+// items) and no k_eval -> k_partition boundary. The host launches it only while the whole grid is
+// resident at once (evaluators + items <= CUs): a waiting item never holds a CU its evaluator needs.
+template <int kSteps, int kMode>
 __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64_t zero_next, int level, int chunk,
-                                                    int tree, EvalSlots es) {
+                                                    int tree, EvalSlots es, uint32_t tag) {
+  constexpr bool kDP = kMode != 0;
   constexpr int kPW = 16;  // waves
   BlockStamp stamp_(d);
   __shared__ int32_t s_cnt[2][kPW];
   __shared__ int32_t s_base[2];
   __shared__ EvalOut s_out;
-  {  // zero the next level's reduce destination (hist_b of the other parity, or the next IPC send slot)
-    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
-    const int64_t nz = zero_next / 2;
+  // zero the next level's reduce destination (hist_b of the other parity, or the next IPC send slot;
+  // kMode 2: the evaluators do, see below)
+  int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
+  const int64_t nz = zero_next / 2;
+  if (kMode != 2)
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
+  const int nlev = 1 << level;
+  const int first = nlev - 1;
+  if (kMode == 2 && (int)blockIdx.x < nlev) {  // the evaluator of node first + blockIdx.x
+    const int pos = blockIdx.x, n = first + pos;
+    const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
+    const bool owned = d.own_level >= 0 && level >= d.own_level;
+    const bool mine = !owned || node_owner(d, level, n, iv->n) == iv->me;
+    const bool good = eval_core<false, true, true>(d, level, parity, tree, d.F, es, pos, stamp_, &s_out);
+    if (threadIdx.x == 0) {
+      uint64_t w = 0;
+      if (good) {
+        int f = 0, j = -1;
+        bool dl = false;
+        const bool ok = split_decision(d, s_out.best, s_out.nb, f, j, dl);
+        eval_finalize<true>(d, level, n, s_out.G, s_out.H, s_out.best, s_out.cut, s_out.nb);
+        if (owned) own_publish(d, iv, n);
+        w = decision_word(tag, ok, false, f, j, dl);
+      } else {
+        const Node nd = d.nodes[n];  // a non-owner's copy of the owner's record (own_copy), or inactive
+        if (owned && mine && nd.status != kActive) own_publish(d, iv, n);  // (as k_eval: a diverged peer learns)
+        const bool failed =
+            __hip_atomic_load(iv->myflag + kIpcStickyWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        // (no node here and no failure: no partition block waits for it)
+        if (nd.status != kNone || failed)
+          w = decision_word(tag, nd.status == kSplit, failed || nd.status == kActive, nd.feat, nd.bin,
+                            nd.default_left != 0);
+      }
+      if (w) __hip_atomic_store(reinterpret_cast<unsigned long long*>(d.dec) + n, (unsigned long long)w,
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // The next send slot (this epoch - 1's) is zeroed once every peer has published this epoch: a peer
+    // then has finished reading its previous contents. The evaluators that exchanged waited for that in
+    // eval_core; a non-owner (it waited only for its node's owner) polls the flags once more, after its
+    // decision is out. A failed exchange zeroes nothing (the fit is aborted).
+    const bool synced =
+        mine ? __hip_atomic_load(iv->myflag + kIpcStickyWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u
+             : ipc_wait<false>(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout);
+    if (!synced) return;
+    for (int64_t e = (int64_t)pos * blockDim.x + threadIdx.x; e < nz; e += (int64_t)nlev * blockDim.x)
+      zp[e] = make_int4(0, 0, 0, 0);
+    return;
   }
-  const int item = blockIdx.x;
-  const int first = (1 << level) - 1;
+  const int item = kMode == 2 ? (int)blockIdx.x - nlev : (int)blockIdx.x;
   // this block's item: the root's rows are fixed slices; deeper levels' items are planned by every
   // block (block_plan over the level's node table)
   PlanOut pl;
@@ -2417,14 +2519,42 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   const int nstart = d.nodes[node].start, ncount = d.nodes[node].count;
   const bool lead = pl.begin == nstart;  // the node's first item
   int f, j;
-  bool dlb;
-  // every block evaluates its node itself (the histograms are L2-hot; the row ids are in flight)
+  bool dlb, ok;
   load_rows();
-  eval_core<false, false, kDP, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, lead);
-  __syncthreads();
-  const Cand best = s_out.best;
-  const bool ok = split_decision(d, best, s_out.nb, f, j, dlb);
-  if (lead && threadIdx.x == 0) eval_finalize<kDP>(d, level, node, s_out.G, s_out.H, best, s_out.cut, s_out.nb);
+  if constexpr (kMode == 2) {  // the node's evaluator decides; the row ids are in flight meanwhile
+    if (len == 0) return;
+    __shared__ uint32_t s_dec;
+    if (threadIdx.x == 0) {
+      const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t v = 2u;  // failed unless the evaluator's granule arrives
+      for (;;) {
+        const uint64_t w = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(d.dec) + node,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(w >> 32) == tag) { v = (uint32_t)w; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > iv->timeout) {
+          ipc_fail(iv->myflag, iv->err_host);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_dec = v;
+    }
+    __syncthreads();
+    const uint32_t v = s_dec;
+    if (v & 2u) return;  // the exchange failed (the host watchdog reports it)
+    ok = (v & 1u) != 0;
+    dlb = (v & 4u) != 0;
+    j = (int)((v >> 3) & 0x3FFu) - 1;
+    f = (int)(v >> 13);
+  } else {
+    // every block evaluates its node itself (the histograms are L2-hot; the row ids are in flight)
+    eval_core<false, false, kDP, true>(d, level, parity, tree, d.F, es, node - first, stamp_, &s_out, lead);
+    __syncthreads();
+    const Cand best = s_out.best;
+    ok = split_decision(d, best, s_out.nb, f, j, dlb);
+    if (lead && threadIdx.x == 0) eval_finalize<kDP>(d, level, node, s_out.G, s_out.H, best, s_out.cut, s_out.nb);
+  }
   stamp_.probe(4);
   if (!ok || len == 0) return;  // a leaf (its rows are not routed) or an empty item (block-uniform)
   const uint8_t* col = d.binsT + (int64_t)f * d.ldt;
@@ -2498,6 +2628,7 @@ struct GbdtCtx {
   int fit_first = 0;            // first tree this context grows in the current fit (no replica check)
   int fault_tree = -1;          // fault injection: tree whose root totals are perturbed on this rank
   uint32_t* pk_buf = nullptr;   // packed records: the code layout (cobalt_gbdt_set_pack)
+  uint32_t dec_tag = 0;         // k_eval_part<.., 2>: the launch tag of the decision granules (d.dec)
   // the last grow call's plan (cobalt_gbdt_plan): fused IPC exchange, ownership level, packed records,
   // resident blocks of the fused k_eval, levels run by the fused evaluation + partition pass
   int32_t plan[5] = {0, -1, 0, 0, 0};
@@ -2613,7 +2744,16 @@ typedef void (*GradHistKernel)(GbdtDev, int, int, int);
 static int hist_ft4(const GbdtDev& d) {
   return ((d.stride == 32 || d.packed) && d.F <= 24 && d.feat_tile >= d.F) ? (d.F + 3) / 4 * 4 : 0;
 }
-static HistKernel hist_kernel(int ft4, bool pair, bool packed = false) {
+static HistKernel hist_kernel(int ft4, bool pair, bool packed = false, bool wide = false) {
+  if (wide) switch (ft4) {
+    case 4: return k_hist<4, false, false, true>;
+    case 8: return k_hist<8, false, false, true>;
+    case 12: return k_hist<12, false, false, true>;
+    case 16: return k_hist<16, false, false, true>;
+    case 20: return k_hist<20, false, false, true>;
+    case 24: return k_hist<24, false, false, true>;
+    default: return nullptr;
+  }
   if (packed) switch (ft4) {
     case 4: return k_hist<4, false, true>;
     case 8: return k_hist<8, false, true>;
@@ -2633,7 +2773,16 @@ static HistKernel hist_kernel(int ft4, bool pair, bool packed = false) {
     default: return k_hist<0, false>;
   }
 }
-static GradHistKernel grad_hist_kernel(int ft4, bool packed = false) {
+static GradHistKernel grad_hist_kernel(int ft4, bool packed = false, bool wide = false) {
+  if (wide) switch (ft4) {
+    case 4: return k_grad_hist<2, 4, false, true>;
+    case 8: return k_grad_hist<2, 8, false, true>;
+    case 12: return k_grad_hist<2, 12, false, true>;
+    case 16: return k_grad_hist<2, 16, false, true>;
+    case 20: return k_grad_hist<2, 20, false, true>;
+    case 24: return k_grad_hist<2, 24, false, true>;
+    default: return nullptr;
+  }
   if (packed) switch (ft4) {
     case 4: return k_grad_hist<2, 4, true>;
     case 8: return k_grad_hist<2, 8, true>;
@@ -2679,13 +2828,20 @@ static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
 COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if (cfg->max_depth < 1 || cfg->max_depth > 10) return -1;
   if (cfg->chunk < 64 || cfg->chunk > 16384) return -2;
-  // row_stride 16: packed 16-byte records (<= 24 features; the layout comes with cobalt_gbdt_set_pack)
-  const bool packed = cfg->row_stride == 16;
+  // packed 16-byte records (<= 24 features; the layout comes with cobalt_gbdt_set_pack). (A 16-byte
+  // stride alone does not say it: 32-byte-layout records of <= 8 features are 16 bytes wide too.)
+  const bool packed = cfg->packed != 0;
+  if (packed && cfg->row_stride != 16) return -3;
   if (packed ? (cfg->n_feat > 24 || cfg->feat_tile < cfg->n_feat)
              : (cfg->row_stride % 16 != 0 || cfg->row_stride < ((cfg->n_feat + 7) / 8) * 8 + 8))
     return -3;
   if (cfg->feat_tile % 4 != 0 || cfg->feat_tile <= 0 || cfg->feat_tile > 64) return -4;
   if (cfg->n_rows >= (int64_t)INT32_MAX) return -5;
+  // wide gradients: 32-byte records with one feature tile (the fast histogram path) only
+  const int gbits = cfg->grad_bits > 0 ? cfg->grad_bits : 17;
+  if (gbits != 17 && gbits != 25) return -6;
+  const bool wide = gbits == 25;
+  if (wide && (packed || cfg->row_stride != 32 || cfg->n_feat > 24 || cfg->feat_tile < cfg->n_feat)) return -6;
   GbdtCtx* c = new GbdtCtx();
   c->cfg = *cfg;
   const int F = cfg->n_feat;
@@ -2734,8 +2890,9 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.by_hess = cfg->comm ? 1 : 0;
   // lane-pair record gathers in the histogram levels (16 < F <= 24): default on (10M rows: 260.4 ->
   // 252.0 ms per fit, 1M: 90.9 -> 87.9 ms); COBALT_HIST_PAIR=0 selects the one-lane-per-row kernel
-  d.hist_pair = knob_int(Knob::HistPair, 1);
-  c->lds_hist = (size_t)cfg->feat_tile * kMaxBins * sizeof(uint64_t);
+  d.hist_pair = wide ? 0 : knob_int(Knob::HistPair, 1);
+  d.wide = wide ? 1 : 0;
+  c->lds_hist = (size_t)cfg->feat_tile * kMaxBins * sizeof(uint64_t) * (wide ? 2 : 1);
   int rc = 0;
   const size_t hist_bytes = (size_t)c->pairs_max * d.slot_elems * sizeof(int64_t);
   if ((rc = dev_alloc(c, (void**)&d.ridx[0], N * sizeof(int32_t)))) return rc;
@@ -2762,8 +2919,11 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
     memset(c->err_pinned, 0, 64);
     CK(hipHostGetDevicePointer((void**)&d.err_host, c->err_pinned, 0));
     d.world = cfg->world_size;
+    if ((rc = dev_alloc(c, (void**)&d.dec, c->max_nodes * sizeof(uint64_t)))) return rc;
+    CK(hipMemset(d.dec, 0, c->max_nodes * sizeof(uint64_t)));  // (tags start at 1)
   }
-  if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t) * (wide ? 2 : 1))))
+    return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
@@ -2881,27 +3041,29 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   c->d.ncells = hoff[F];
   c->d.slot_elems = (int64_t)(hoff[F] + 1) * 2;
   CK(hipMemcpy(c->d.tile_entries, ent.data(), ntiles * sizeof(int32_t), hipMemcpyHostToDevice));
-  c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t);
+  const bool wide = c->d.wide != 0;
+  c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t) * (wide ? 2 : 1);
   if (c->lds_hist > 64 * 1024) {
-    for (int pair = 0; pair < 3; ++pair)
-      if (HistKernel k = hist_kernel(hist_ft4(c->d), pair == 1, pair == 2))
+    for (int v = 0; v < 4; ++v)
+      if (HistKernel k = hist_kernel(hist_ft4(c->d), v == 1, v == 2, v == 3))
         CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
   const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
-  if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0))
-    CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0),
+  if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0, wide))
+    CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0, wide),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
   return 0;
 }
 
-static void launch_eval_part(int steps, bool dp, dim3 grid, hipStream_t stream, const GbdtDev& d, int parity,
-                             int64_t zero_next, int level, int chunk, int tree, const EvalSlots& es) {
+static void launch_eval_part(int steps, int mode, dim3 grid, size_t lds, hipStream_t stream, const GbdtDev& d,
+                             int parity, int64_t zero_next, int level, int chunk, int tree, const EvalSlots& es,
+                             uint32_t tag) {
 #define EP_LAUNCH(S, M) \
-  hipLaunchKernelGGL((k_eval_part<S, M>), grid, dim3(1024), 0, stream, d, parity, zero_next, level, chunk, tree, es)
+  hipLaunchKernelGGL((k_eval_part<S, M>), grid, dim3(1024), lds, stream, d, parity, zero_next, level, chunk, tree, es, tag)
   if (steps <= 4) {
-    if (dp) EP_LAUNCH(4, true); else EP_LAUNCH(4, false);
+    if (mode == 0) EP_LAUNCH(4, 0); else if (mode == 1) EP_LAUNCH(4, 1); else EP_LAUNCH(4, 2);
   } else {
-    if (dp) EP_LAUNCH(8, true); else EP_LAUNCH(8, false);
+    if (mode == 0) EP_LAUNCH(8, 0); else if (mode == 1) EP_LAUNCH(8, 1); else EP_LAUNCH(8, 2);
   }
 #undef EP_LAUNCH
 }
@@ -2938,6 +3100,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // (packed records have no unfused root pass: k_grad reads the 32-byte layout)
   const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.packed || d.ablate == 0 || d.ablate >= 10);
   if (d.packed && (!fuse_root || sampled)) return -15;
+  if (d.wide && sampled) return -15;  // (the sampled pages carry 17-bit pairs)
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
   static const int env_fg = knob_int(Knob::EvalFg, -1);
@@ -2978,10 +3141,20 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // (1M rows: 248.0 -> 239.3 us per tree in the stamps; 1.25M: 87.0 -> 96.3 ms per fit, 2.5M 112 -> 130:
   // two evaluations per CU). COBALT_EVAL_PART=0 / 2 disables / forces it. Under data parallelism it needs
   // the level's global histograms in hist_b before it runs (RCCL, or the separate IPC exchange kernel);
-  // the fused IPC exchange evaluates in k_eval (one block per node; node ownership on the deep levels).
+  // over the fused IPC exchange its evaluator-block form (k_eval_part<.., 2>: one evaluating block per
+  // node, the exchange and node ownership exactly as k_eval, the items wait for their node's decision)
+  // while the whole grid -- evaluators + items -- fits one block per CU (COBALT_DP_EVAL_PART=0: k_eval +
+  // k_partition).
   static const int env_ep = knob_int(Knob::EvalPart, 1);
+  static const int env_dp_ep = knob_int(Knob::DpEvalPart, 1);
   const int ep_steps = ceil_div(chunk_part(d), 16 * kWave);
-  // node ownership (see node_owner): over the fused exchange with separate k_eval / k_partition passes,
+  bool ep_split = false;  // k_eval_part<.., 2> fits a CU with the fused exchange's LDS
+  if (ipc_fused && env_dp_ep) {
+    int per_cu = 0;
+    ep_split = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_eval_part<8, 2>, 1024, fused_lds) ==
+                   hipSuccess && per_cu >= 1;
+  }
+  // node ownership (see node_owner): over the fused exchange (k_eval, or k_eval_part's evaluator blocks),
   // on the three deepest split levels (where the exchange volume is: 56 of a depth-7 tree's 64 pairs;
   // the copy costs the other ranks one more remote round trip, not worth it for a level's few nodes),
   // and never before a level with a node per rank. COBALT_DP_OWNER=0: every rank evaluates every node
@@ -2993,7 +3166,9 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     l0 = std::max(l0, D - 3);
     d.own_level = l0 < D ? l0 : -1;
   }
-  const bool eval_part = env_ep != 0 && !ipc_fused && eval_fg == 0 && ep_steps <= 8 && d.F <= 32;
+  const bool eval_part = env_ep != 0 && (!ipc_fused || ep_split) && eval_fg == 0 && ep_steps <= 8 && d.F <= 32;
+  const int ep_mode = ipc_fused ? 2 : (dp ? 1 : 0);
+  const int ep_extra = ep_mode == 2 ? 2 : 1;  // grid beyond the items: one partial item (+ one evaluator) per node
   c->plan[0] = ipc_fused ? 1 : 0;
   c->plan[1] = d.own_level;
   c->plan[2] = d.packed;
@@ -3003,7 +3178,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     if (eval_part) {
       const int cus = device_cu_count();
       for (int ch = std::min(4096, chunk_part(d)); ch <= 8192; ch += 1024)
-        if (ceil_div(d.n, ch) + (1 << level) <= cus) { c->plan[4] |= 1 << level; break; }
+        if (ceil_div(d.n, ch) + (ep_extra << level) <= cus) { c->plan[4] |= 1 << level; break; }
     }
   // Item size of a level's fused pass: the grid (items + one partial item per node) fits one 1024-thread
   // block per CU -- beyond that a second round of blocks doubles the level (1M rows with 4096-row items:
@@ -3015,7 +3190,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     if (!eval_part) return 0;
     const int cus = device_cu_count();
     for (int ch = std::min(4096, chunk_part(d)); ch <= 8192; ch += 1024)
-      if (ceil_div(d.n, ch) + (1 << level) <= cus) return ch;
+      if (ceil_div(d.n, ch) + (ep_extra << level) <= cus) return ch;
     return (env_ep == 2 && !dp) ? 8192 : 0;
   };
   d.zero_red = nullptr;
@@ -3054,7 +3229,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
               stream, d);
     else if (fuse_root)
-      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.packed != 0), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
+      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.packed != 0, d.wide != 0), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
               stream, d, t, apply, root_chunk);
     else
       GLAUNCH("k_grad", k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
@@ -3076,7 +3251,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       const int ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
                                                : ceil_div(d.n, chh) + (1 << level);
       if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0, d.packed != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
+        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0, d.packed != 0, d.wide != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
                 stream, d, parity, t, level, chh);
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       const dim3 rgrid(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256));
@@ -3137,7 +3312,9 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         const int steps = ceil_div(chp, 16 * kWave);  // <= 8 (chunk_part's cap)
         if (ep_level) {
           c->d.seq = stamp_next(c, "k_eval_part");
-          launch_eval_part(steps, dp, dim3(ubp), stream, d, parity, zero_next, level, chp, t, c->eval_slots);
+          const int evals = ep_mode == 2 ? (1 << level) : 0;
+          launch_eval_part(steps, ep_mode, dim3(ubp + evals), ep_mode == 2 ? fused_lds : 0, stream, d, parity, zero_next,
+                           level, chp, t, c->eval_slots, ++c->dec_tag);
         } else if (steps <= 4)
           GLAUNCH("k_partition", (k_partition<16, 4>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
                   level, chp);
@@ -3351,6 +3528,7 @@ __global__ __launch_bounds__(256) void k_ox_reduce(GbdtDev d, int64_t* __restric
 COBALT_API int cobalt_gbdt_ox_init(void* h, int64_t n, float* margin, const float* label, const float* weight) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   if (c->d.F > kMaxFeatTile || c->max_nodes > 256 || c->d.F > 32) return -15;  // depth <= 7, <= 32 features
+  if (c->d.wide) return -15;  // (the out-of-core passes accumulate 17-bit packed pairs)
   if (c->ox_pos) return -16;
   c->ox_n = n;
   int rc;
@@ -3549,7 +3727,8 @@ COBALT_API int cobalt_gbdt_reuse(void* h, const GbdtConfig* cfg) {
   const GbdtConfig& o = c->cfg;
   if (o.n_rows != cfg->n_rows || o.n_feat != cfg->n_feat || o.row_stride != cfg->row_stride ||
       o.max_depth != cfg->max_depth || o.max_trees != cfg->max_trees || o.chunk != cfg->chunk ||
-      o.feat_tile != cfg->feat_tile || o.world_size != cfg->world_size || o.comm != cfg->comm)
+      o.feat_tile != cfg->feat_tile || o.world_size != cfg->world_size || o.comm != cfg->comm ||
+      (o.grad_bits > 17) != (cfg->grad_bits > 17) || o.packed != cfg->packed)
     return 1;
   c->cfg = *cfg;
   GbdtDev& d = c->d;

@@ -65,6 +65,10 @@ class GBDTParams:
     # instead of all-gathering the global sample (see models/sketch.py)
     sketch_weight: str = "sample"
     sketch_mode: str = "sample"
+    # fixed-point gradient precision: 17 bits (default; one packed u64 LDS atomic per cell) or 25 bits
+    # ("wide": g and h summed in separate int64 cells, 256x finer steps; 32-byte records, <= 24 features
+    # on the GPU; the CPU trainer implements both exactly -- docs/PERF.md "Gradient precision")
+    grad_bits: int = 17
 
     @classmethod
     def from_kwargs(cls, **kw) -> "GBDTParams":
@@ -221,7 +225,7 @@ def resolve_sketch_rows(sketch_rows: int | None, dev, n_rows_global: int | None 
 
 def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO, device=None, dist=None,
                 n_rows_global: int | None = None, row_offset: int = 0, sketch_weights=None,
-                sketch_mode: str = "sample") -> BinnedData:
+                sketch_mode: str = "sample", packed: bool = True) -> BinnedData:
     """Weighted quantile sketch (K12) on a global strided sample + binning (K13).
 
     ``sketch_rows`` None / 0: every row (XGBoost ``hist`` sketches all rows), exact weighted quantiles.
@@ -231,7 +235,8 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     rank summarises its shard and the summaries are merged (``sketch_mode="summary"``).
     ``sketch_weights`` ([N_local], optional): per-row sketch weights (see models/sketch.py).
     A feature gets 256 bins only if it has no missing value in the FULL data (all ranks).
-    ``SKETCH_AUTO``: every row on a GPU, the 2^18-row sample on the CPU."""
+    ``SKETCH_AUTO``: every row on a GPU, the 2^18-row sample on the CPU. ``packed=False``: 32-byte
+    row records even where the packed 16-byte form fits (wide gradients need them)."""
     dev = _resolve_device(device, X)
     world = dist.world if dist is not None else 1
     Xt = _to_tensor(X, dev)
@@ -254,7 +259,7 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
         t_sketch = time.perf_counter() - ts
         tb = time.perf_counter()
         bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
-        _bin_device(bd, Xt, cuts, nbins)
+        _bin_device(bd, Xt, cuts, nbins, packed)
         torch.cuda.synchronize(dev)
         bd.t_bin = time.perf_counter() - tb
         return bd
@@ -279,7 +284,7 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     tb = time.perf_counter()
     bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
     if dev.type == "cuda":
-        _bin_device(bd, Xt, cuts, nbins)
+        _bin_device(bd, Xt, cuts, nbins, packed)
         torch.cuda.synchronize(dev)
     else:
         bd.bins_host = sketch.bin_matrix_host(Xt.cpu().numpy(), cuts.cpu().numpy(), nbins.cpu().numpy())
@@ -287,12 +292,13 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     return bd
 
 
-def _bin_device(bd: BinnedData, Xt: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> None:
+def _bin_device(bd: BinnedData, Xt: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor,
+                packed: bool = True) -> None:
     """Binning on the GPU: packed 16-byte row records where the codes fit (the gradient pass and the
     histogram gathers move half the bytes), else 32-byte records; feature-major bins either way."""
     from ..ops import gbdt_ops
 
-    pk = gbdt_ops.bin_matrix_packed(Xt, cuts, nbins)
+    pk = gbdt_ops.bin_matrix_packed(Xt, cuts, nbins) if packed else None
     if pk is not None:
         bd.records, bd.binsT, bd.pack = pk
     else:
@@ -408,7 +414,7 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
     bd = bin_dataset(X, max_bin=params.max_bin, sketch_rows=params.sketch_rows, device=device, dist=dist,
                      n_rows_global=n_rows_global, row_offset=row_offset,
                      sketch_weights=sketch_weights_for(params, y, sample_weight, dev),
-                     sketch_mode=params.sketch_mode)
+                     sketch_mode=params.sketch_mode, packed=int(params.grad_bits) <= gbdt_host.QBITS)
     bst = train_binned(bd, y, params, sample_weight=sample_weight, feature_names=feature_names,
                        feature_types=feature_types, dist=dist, report=report, init_booster=init_booster,
                        init_margin=init_margin, total_trees=total, checkpoint=ckpt, exact_fp64=exact_fp64)
@@ -433,6 +439,11 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         params = GBDTParams.from_kwargs(**params)
     dev = bd.device
     world = dist.world if dist is not None else 1
+    grad_bits = int(params.grad_bits)
+    if grad_bits not in gbdt_host.GRAD_BITS:
+        raise ValueError(f"grad_bits must be one of {gbdt_host.GRAD_BITS}")
+    if grad_bits > gbdt_host.QBITS and bd.pack is not None:  # wide gradients: 32-byte records
+        bd = subset_features(bd, range(bd.n_features))
     N, F = bd.n_rows, bd.n_features
     rep = report if report is not None else FitReport()
     tp = rep.mark("pre", time.perf_counter(), dev)
@@ -477,7 +488,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         base_score = float(params.base_score)
     base_score = float(np.float32(base_score))
     base_margin = Booster([], base_score=base_score, num_feature=F).base_margin
-    gscale, hscale = gbdt_host.quant_scales(wmax)
+    gscale, hscale = gbdt_host.quant_scales(wmax, grad_bits)
 
     T_new = (int(total_trees) - T0) if total_trees is not None else int(params.n_estimators)
     if T_new < 0:
@@ -525,7 +536,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                                   gamma=float(params.gamma), min_child_weight=float(params.min_child_weight),
                                   subsample=float(params.subsample), seed=int(params.random_state),
                                   gscale=1.0 if exact_fp64 else gscale, hscale=1.0 if exact_fp64 else hscale,
-                                  quant=not exact_fp64)
+                                  quant=not exact_fp64, qbits=grad_bits)
     if exact_fp64 and dev.type != "cpu":
         raise ValueError("exact_fp64 is the host (CPU) reference trainer")
     tp = rep.mark("labels_weights", tp, dev)
@@ -543,7 +554,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                                      min_child_weight=hp.min_child_weight, subsample=hp.subsample,
                                      gscale=gscale, hscale=hscale, base_margin=base_margin,
                                      seed=hp.seed, row_offset=bd.row_offset, world_size=world, comm=comm,
-                                     packed=bd.pack is not None)
+                                     packed=bd.pack is not None, grad_bits=grad_bits)
         fm = torch.as_tensor(fmask_np, device=dev).contiguous()
         tr.set_data(bd.records, bd.binsT, bd.cuts.contiguous(), bd.nbins.to(torch.int32).contiguous(),
                     yt.contiguous(), wt, margin, fm)

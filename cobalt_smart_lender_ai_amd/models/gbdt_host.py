@@ -28,6 +28,8 @@ MASK64 = (1 << 64) - 1
 QBITS = 17          # |g_q| < 2^17, h_q <= 2^17: a <= 16384-row histogram block sums to < 2^31
 G_CLIP = (1 << QBITS) - 1
 H_CLIP = 1 << QBITS
+QBITS_WIDE = 25     # wide gradients (grad_bits=25): int64 histogram cells on the GPU
+GRAD_BITS = (QBITS, QBITS_WIDE)
 
 
 def splitmix64_np(x: np.ndarray) -> np.ndarray:
@@ -82,14 +84,18 @@ class HostGbdtParams:
     gscale: float
     hscale: float
     quant: bool = True   # False: unquantised fp64 gradients and histograms (accuracy reference)
+    qbits: int = QBITS   # quantised magnitude bits: 17, or 25 (wide gradients)
 
 
-def quant_scales(w_max: float) -> tuple[float, float]:
-    """Fixed-point scales: |g| <= w and h <= w/4, so both quantised magnitudes stay <= 2^17 and a
-    16384-row histogram block sums to < 2^31 -- the packed-u64 LDS accumulation on the GPU keeps h in
-    the low 32 bits (no carry into g) and g as a signed 32-bit high half."""
+def quant_scales(w_max: float, bits: int = QBITS) -> tuple[float, float]:
+    """Fixed-point scales: |g| <= w and h <= w/4, so both quantised magnitudes stay <= 2^bits. At 17
+    bits a 16384-row histogram block sums to < 2^31 -- the packed-u64 LDS accumulation on the GPU keeps
+    h in the low 32 bits (no carry into g) and g as a signed 32-bit high half; at 25 bits (wide
+    gradients) the GPU sums g and h in separate int64 cells."""
+    if bits not in GRAD_BITS:
+        raise ValueError(f"grad_bits must be one of {GRAD_BITS}")
     w_max = float(w_max) if w_max > 0 else 1.0
-    return float(2 ** QBITS) / w_max, float(2 ** (QBITS + 2)) / w_max
+    return float(2 ** bits) / w_max, float(2 ** (bits + 2)) / w_max
 
 
 def _thresh_l1(g, alpha):
@@ -137,8 +143,9 @@ def gradients_host(margin: np.ndarray, label: np.ndarray, weight: np.ndarray, p:
     # E[q] = x * scale exactly -- small hessians are not flushed to 0 and the rounding error of a sum
     # averages out instead of accumulating a bias; deterministic (same on every device / rank count)
     ug, uh = dither_uniforms(p.seed, tree, row_offset + np.arange(len(m), dtype=np.int64))
-    gq = np.clip(np.floor(g * p.gscale + ug), -G_CLIP, G_CLIP).astype(np.int64)
-    hq = np.clip(np.floor(h * p.hscale + uh), 0, H_CLIP).astype(np.int64)
+    gclip, hclip = (1 << p.qbits) - 1, 1 << p.qbits
+    gq = np.clip(np.floor(g * p.gscale + ug), -gclip, gclip).astype(np.int64)
+    hq = np.clip(np.floor(h * p.hscale + uh), 0, hclip).astype(np.int64)
     return gq, hq
 
 

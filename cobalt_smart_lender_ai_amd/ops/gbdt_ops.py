@@ -42,10 +42,12 @@ class GbdtConfig(ctypes.Structure):
         ("world_size", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("comm", ctypes.c_void_p),
+        ("grad_bits", ctypes.c_int32),  # 17 (packed u64 LDS cells) or 25 (wide int64 cells)
+        ("packed", ctypes.c_int32),     # 1: packed 16-byte row records (set_pack)
     ]
 
 
-assert ctypes.sizeof(GbdtConfig) == 128
+assert ctypes.sizeof(GbdtConfig) == 136
 
 
 def row_stride(n_feat: int) -> int:
@@ -184,7 +186,7 @@ class GpuGbdtTrainer:
                  reg_lambda: float, reg_alpha: float, gamma: float, min_child_weight: float, subsample: float,
                  gscale: float, hscale: float, base_margin: float, seed: int, row_offset: int = 0,
                  world_size: int = 1, comm: int | None = None, chunk: int | None = None,
-                 feat_tile: int | None = None, packed: bool = False):
+                 feat_tile: int | None = None, packed: bool = False, grad_bits: int = 17):
         self.lib = _native.lib()
         cfg = GbdtConfig()
         cfg.n_rows = n_rows
@@ -207,9 +209,12 @@ class GpuGbdtTrainer:
         cfg.world_size = world_size
         cfg.seed = seed & ((1 << 64) - 1)
         cfg.comm = comm
+        cfg.grad_bits = int(grad_bits)
+        cfg.packed = 1 if packed else 0
         self.cfg = cfg
         self._key = (torch.cuda.current_device(), cfg.n_rows, cfg.n_feat, cfg.row_stride, cfg.max_depth,
-                     cfg.max_trees, cfg.chunk, cfg.feat_tile, cfg.world_size, cfg.comm or 0)
+                     cfg.max_trees, cfg.chunk, cfg.feat_tile, cfg.world_size, cfg.comm or 0, cfg.grad_bits,
+                     cfg.packed)
         h = None
         if _cache_on():
             with _PARKED_LOCK:

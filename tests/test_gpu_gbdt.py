@@ -70,6 +70,8 @@ def test_bin_matrix_packed_matches_host(F):
 
     X, _ = _data(30_011, seed=F)
     X = X[:, :F].contiguous() if F <= X.shape[1] else torch.cat([X, X[:, : F - X.shape[1]] * 1.5], 1).contiguous()
+    if F == 24:  # 24 codes fit the 91 bits only at <= 3 bits each: low-cardinality columns (NaNs kept)
+        X = torch.clamp(torch.floor(X * 1.5), -3, 2)
     cuts, nb = sketch.compute_cuts(X, 256)
     got = gbdt_ops.bin_matrix_packed(X.cuda(), cuts.cuda(), nb.cuda())
     assert got is not None, "the layout fits these features"
@@ -98,6 +100,19 @@ def test_gpu_packed_records_fit_equals_32byte_fit_and_oracle(env, monkeypatch):
     wide = gbdt.train(X.cuda(), y.cuda(), p, device="cuda").save_raw("ubj")
     assert packed == wide
     assert packed == gbdt.train(X, y, p, device="cpu").save_raw("ubj")
+
+
+def test_gpu_wide_gradients_equal_oracle():
+    """grad_bits=25 (int64 LDS cells, 32-byte records even where the packed form fits): the GPU trees
+    equal the NumPy oracle's at 25 bits byte for byte, with row and column sampling; a 17-bit fit of
+    the same data grows different trees (the precision is really used)."""
+    X, y = _data(120_000, seed=13)
+    p = gbdt.GBDTParams(n_estimators=5, max_depth=7, learning_rate=0.2, gamma=0.5, subsample=0.8,
+                        colsample_bytree=0.7, scale_pos_weight=6.7, random_state=9, grad_bits=25)
+    wide = gbdt.train(X.cuda(), y.cuda(), p, device="cuda").save_raw("ubj")
+    assert wide == gbdt.train(X, y, p, device="cpu").save_raw("ubj")
+    p17 = gbdt.GBDTParams(**{**p.__dict__, "grad_bits": 17})
+    assert wide != gbdt.train(X.cuda(), y.cuda(), p17, device="cuda").save_raw("ubj")
 
 
 def test_sketch_gpu_equals_cpu():
