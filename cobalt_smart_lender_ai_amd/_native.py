@@ -62,10 +62,6 @@ _SIGS: dict[str, tuple] = {
                                 ctypes.c_uint64, c_int64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "cobalt_ooc_bins": (c_int, []),
-    "cobalt_pack_layout": (c_int, [c_void_p, c_int, c_void_p]),
-    "cobalt_bin_matrix_pk": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                     c_int64, c_void_p]),
-    "cobalt_gbdt_set_pack": (c_int, [c_void_p, c_void_p]),
     "cobalt_gbdt_plan": (c_int, [c_void_p, c_void_p]),
     "cobalt_knob_count": (c_int, []),
     "cobalt_bin_matrix": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int,

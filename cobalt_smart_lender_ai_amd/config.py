@@ -157,7 +157,7 @@ KNOBS: dict[str, Knob] = {
     # -- data parallelism --
     "COBALT_IPC_FUSED": Knob("1", "native", "IPC exchange fused into the split evaluation (0: separate exchange kernel + fused eval/partition)"),
     "COBALT_DP_OWNER": Knob("1", "native", "node ownership on the three deepest levels over the fused IPC exchange"),
-    "COBALT_DP_EVAL_PART": Knob("1", "native", "fused IPC exchange: evaluator blocks + partition items in one pass while the grid fits the CUs (0 off)"),
+    "COBALT_EVAL_BLOCKS": Knob("1", "native", "fused evaluation + partition with one evaluator block per node where the items exceed the CUs, and over the fused IPC exchange (0 off)"),
     "COBALT_CU_BUDGET": Knob("", "native", "CUs of this rank's CU-masked stream (set by parallel/cumask.py)"),
     "COBALT_DP_TRANSPORT": Knob("auto", "python", "native communicator: auto (IPC within a node), ipc or rccl"),
     "COBALT_DIST_BACKEND": Knob("auto", "python", "torch.distributed backend override (gloo for ranks sharing one GPU)"),
@@ -170,7 +170,6 @@ KNOBS: dict[str, Knob] = {
     "COBALT_CU_MASK_LAYOUT": Knob("interleaved", "python", "CU masks of ranks sharing one GPU: interleaved (CU rank + k world) or blocked"),
     "COBALT_BENCH_SHARED_DEVICE": Knob("0", "python", "bench.py: every rank on cuda:0 (the 1-GPU multi-rank rehearsal)"),
     # -- trainer / serving (python) --
-    "COBALT_PACKED_RECORDS": Knob("1", "python", "packed 16-byte row records where the bin codes fit 91 bits (0: 32-byte records)"),
     "COBALT_LABEL_IN_RECORD": Knob("1", "python", "0/1 labels ride in the row records' padding (weights derived from them)"),
     "COBALT_TRAINER_CACHE": Knob("1", "python", "keep one trainer context per process for back-to-back fits of the same shapes"),
     "COBALT_SEARCH_STREAMS": Knob("4", "python", "HIP streams of the randomized search's concurrent fits"),

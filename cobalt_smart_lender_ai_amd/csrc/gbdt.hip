@@ -133,7 +133,7 @@ struct GbdtConfig {
   uint64_t seed;
   void* comm;            // native RCCL communicator (cobalt_comm_*) or nullptr
   int32_t grad_bits;     // quantised (g, h) magnitude bits: 17 (packed u64 LDS cells) or 25 (wide cells)
-  int32_t packed;        // 1: packed 16-byte row records (row_stride 16, the layout via cobalt_gbdt_set_pack)
+  int32_t reserved0;
 };
 
 struct GbdtDev {
@@ -217,10 +217,6 @@ struct GbdtDev {
   // node ownership (fused IPC exchange): from level own_level on, a node is evaluated only by the rank
   // owning its level-own_level ancestor; the others copy its decision (-1: every rank evaluates all)
   int32_t own_level;
-  // packed 16-byte row records (stride 16, cobalt_pack_layout): pk[f] = bit offset | width << 8 of
-  // feature f's code (device memory; the histogram kernels fold it into their per-feature metadata word)
-  int32_t packed;
-  const uint32_t* pk;
   // k_eval_part<.., 2>: per-node decision granules {launch tag, decision} (decision_word)
   uint64_t* dec;
   // wide gradients (grad_bits 25): |g_q| < 2^25, h_q <= 2^25, and the LDS histograms hold a cell as two
@@ -406,39 +402,6 @@ __device__ __forceinline__ uint32_t node_meta(const Node& nd) {
 }
 __device__ __forceinline__ bool meta_left(uint32_t m, uint32_t b) {
   return (b == kMissingBin) ? ((m >> 25) & 1u) : (b < ((m >> 16) & 0x1FFu));
-}
-
-// ------------------------------------------------------------------------------------------
-// Packed 16-byte row records (the default for <= 24 features whose codes fit 91 bits; cobalt_pack_layout).
-// Dwords 0, 1 and bits 0..26 of dword 2 hold the F bin codes, each `width` bits at its bit `offset`, no
-// code crossing a dword; width = ceil(log2(nbins + 1)) -- room for the all-ones missing code -- and 8 for a
-// 256-bin feature, whose code 255 is a real bin exactly as in the uint8 layout. Bit 27 of dword 2: the
-// 0/1 label (binary-label fits). The quantised pair: g in dword 3 bits 0..17 (two's complement, |g| <
-// 2^17), h (0 .. 2^17) in dword 3 bits 18..31 (low 14 bits) and dword 2 bits 28..31 (high 4). Half the
-// bytes of the 32-byte record per row: the gradient pass streams 16 B in and out instead of a 32-byte
-// read + a dirtied 32-byte sector, and a histogram gather moves one 16-byte record per lane.
-// ------------------------------------------------------------------------------------------
-constexpr int kPkBinBits = 91;
-constexpr uint32_t kPkLabelBit = 27;
-__device__ __forceinline__ uint32_t pk_code(const uint4& r, uint32_t pk) {
-  const uint32_t off = pk & 0x7Fu, word = off >> 5;
-  const uint32_t w = word == 0 ? r.x : (word == 1 ? r.y : r.z);
-  return __builtin_amdgcn_ubfe(w, off & 31u, (pk >> 8) & 0xFu);
-}
-// The code as the uint8 layout has it (missing -> 255), for the tree walks.
-__device__ __forceinline__ uint32_t pk_bin8(const uint4& r, uint32_t pk) {
-  const uint32_t c = pk_code(r, pk);
-  return c == (1u << ((pk >> 8) & 0xFu)) - 1u ? 255u : c;
-}
-__device__ __forceinline__ int32_t pk_g(const uint4& r) { return ((int32_t)(r.w << 14)) >> 14; }
-__device__ __forceinline__ uint32_t pk_h(const uint4& r) { return (r.w >> 18) | ((r.z >> 28) << 14); }
-__device__ __forceinline__ uint64_t pk_gh(const uint4& r) {  // packed (g, h) as the LDS histograms add it
-  return ((uint64_t)(uint32_t)pk_g(r) << 32) | pk_h(r);
-}
-__device__ __forceinline__ void pk_set_gh(uint4& r, int64_t gq, int64_t hq) {
-  const uint32_t h = (uint32_t)hq;
-  r.w = ((uint32_t)(int32_t)gq & 0x3FFFFu) | (h << 18);
-  r.z = (r.z & 0x0FFFFFFFu) | ((h >> 14) << 28);
 }
 
 // Stage tree `t` (heap-ordered node records) into LDS as {meta, leaf value}.
@@ -842,7 +805,6 @@ struct HistLanes {
 struct HistLaneRaw {
   bool on;
   int sh, nb;
-  uint32_t pk;  // packed records: the feature's code layout (0 otherwise)
 };
 
 __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tree, int f0, int ft) {
@@ -854,8 +816,6 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   const uint8_t fmv = d.fmask[(int64_t)tree * d.F + f];
   const int ly0 = d.layout[f].y;
   const int nb0 = d.nbins[f];
-  const uint32_t pk0 = d.packed ? d.pk[f] : 0u;
-  r.pk = in ? pk0 : 0u;
   r.on = in && fmv != 0;
   const int ly = in ? ly0 : 0;
   r.sh = ly & 7;
@@ -863,12 +823,11 @@ __device__ __forceinline__ HistLaneRaw hist_lanes_load(const GbdtDev& d, int tre
   return r;
 }
 
-// Per-feature histogram metadata of lane fl's feature: nbins | (copy shift + cs) << 16 | packed-code
-// width << 20 | packed-code bit offset << 24 (cs = log2 of the LDS cell bytes: 3, or 4 for wide cells);
-// a feature past the tile or masked out by colsample gets nbins 0 (it adds into a trash cell).
+// Per-feature histogram metadata of lane fl's feature: nbins | (copy shift + cs) << 16 (cs = log2 of the
+// LDS cell bytes: 3, or 4 for wide cells); a feature past the tile or masked out by colsample gets
+// nbins 0 (it adds into a trash cell).
 __device__ __forceinline__ uint32_t hist_meta(const HistLaneRaw& raw, uint32_t cs = 3) {
-  const uint32_t pkm = ((raw.pk >> 8) & 0xFu) << 20 | (raw.pk & 0x7Fu) << 24;
-  return (raw.on ? ((uint32_t)raw.nb | ((uint32_t)raw.sh + cs) << 16) : (cs << 16)) | pkm;
+  return raw.on ? ((uint32_t)raw.nb | ((uint32_t)raw.sh + cs) << 16) : (cs << 16);
 }
 
 // Stage the metadata of the tile's features in LDS (s_fm[64], lane fl = feature fl) from ONE wave: the
@@ -929,23 +888,6 @@ __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes
         atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
       }
     }
-  }
-}
-
-// The same for one packed 16-byte record (d.pk: the features' bit offsets / widths, uniform kernel
-// arguments): per feature one bit-field extract from the record word, then hist_add_rec32's clamp /
-// shift-add / ds_add_u64. Padding features (pk = 0: a 0-bit field) add into the trash cell.
-template <int FT4>
-__device__ __forceinline__ void hist_add_pk(uint64_t* s_hist, const HistLanes& hl, const uint4& r) {
-  static_assert(FT4 % 4 == 0 && FT4 > 0 && FT4 <= 24, "packed records hold <= 24 features");
-  const uint64_t gp = pk_gh(r);
-  char* base = reinterpret_cast<char*>(s_hist);
-#pragma unroll
-  for (int fl = 0; fl < FT4; ++fl) {
-    const uint32_t m = hl.fm[fl];  // nbins | copy shift | code width << 20 | code offset << 24
-    const uint32_t bb = pk_code(r, (m >> 24) | (((m >> 20) & 15u) << 8));
-    const uint32_t off = hl.lb8[fl] + (min(bb, m & 0xffffu) << ((m >> 16) & 15u));
-    atomicAdd(reinterpret_cast<unsigned long long*>(base + off), (unsigned long long)gp);
   }
 }
 
@@ -1029,11 +971,9 @@ __device__ void hist_flush(const GbdtDev& d, const uint64_t* s_hist, const HistL
 // holding the freshly quantised (g, h) and the bins -- the separate root histogram pass (a full
 // 32 B/row re-read) disappears. Block b = root work item b: rows [b*chunk, (b+1)*chunk).
 // Also: previous-tree margin update + archive and node-table init, as k_grad.
-// kPk: packed 16-byte records (one 16-byte load and store per row; the walk extracts the split
-// feature's code with its layout entry, staged in LDS because the walk indexes it per lane).
-template <int U, int FT4, bool kPk, bool kWide>
+// kWide: wide gradients (16-byte LDS cells {g, h}, 25-bit quantisation).
+template <int U, int FT4, bool kWide>
 __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int apply_tree, int chunk) {
-  static_assert(!(kPk && kWide), "wide gradients use 32-byte records");
   constexpr int kW = kWide ? 2 : 1;            // u64 words per LDS cell
   constexpr uint32_t kCs = kWide ? 4u : 3u;    // log2 of the cell bytes
   BlockStamp stamp_(d);
@@ -1049,8 +989,6 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
   uint64_t* s_hist = s_dyn;
   uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries * kW);
   float* s_leaf = reinterpret_cast<float*>(s_meta + d.max_nodes);
-  __shared__ uint32_t s_pk[kPk ? 24 : 1];  // the features' packed-code layout (the walk indexes it per lane)
-  if (kPk && threadIdx.x < d.F) s_pk[threadIdx.x] = d.pk[threadIdx.x];
   {  // zero the root histogram slot (k_hist_reduce accumulates into it)
     int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[0]);
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
@@ -1092,14 +1030,9 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + (int64_t)u * B;
       const int64_t ii = i < end ? i : begin;
-      if constexpr (kPk) {
-        ra[u] = reinterpret_cast<const uint4*>(d.bins)[ii];
-        rb[u] = make_uint4(0, 0, 0, 0);
-      } else {
-        const uint4* rec = reinterpret_cast<const uint4*>(d.bins + ii * 32);
-        ra[u] = rec[0];
-        rb[u] = rec[1];
-      }
+      const uint4* rec = reinterpret_cast<const uint4*>(d.bins + ii * 32);
+      ra[u] = rec[0];
+      rb[u] = rec[1];
       mf[u] = d.margin[ii];
       yl[u] = 0.0f;
       wt[u] = 0.0f;
@@ -1117,14 +1050,9 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
         uint32_t m = s_meta[0];
         while (m & kMetaSplit) {
           const int f = m & 0xFFFF, q = f >> 2;
-          uint32_t b;
-          if constexpr (kPk) {
-            b = pk_bin8(ra[u], s_pk[f]);
-          } else {
-            const uint32_t word = q == 0 ? ra[u].x : q == 1 ? ra[u].y : q == 2 ? ra[u].z : q == 3 ? ra[u].w
-                                : q == 4 ? rb[u].x : rb[u].y;
-            b = (word >> (8 * (f & 3))) & 0xffu;
-          }
+          const uint32_t word = q == 0 ? ra[u].x : q == 1 ? ra[u].y : q == 2 ? ra[u].z : q == 3 ? ra[u].w
+                              : q == 4 ? rb[u].x : rb[u].y;
+          const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
           const bool left = meta_left(m, b);
           nidx = 2 * nidx + (left ? 1 : 2);
           m = s_meta[nidx];
@@ -1135,7 +1063,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       const double mm = (double)mf[u];
       const double p = d.ablate == 20 ? 0.5 + 0.01 * mm : 1.0 / (1.0 + exp(-mm));  // (20: timing-only, no exp)
       if (d.ylab) {
-        yl[u] = kPk ? (float)((ra[u].z >> kPkLabelBit) & 1u) : (float)(rb[u].y >> 24);
+        yl[u] = (float)(rb[u].y >> 24);
         wt[u] = yl[u] != 0.0f ? d.spw : 1.0f;
       }
       const double y = (double)yl[u];
@@ -1150,16 +1078,10 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq, kWide);
       tg += gq;
       th += hq;
-      if constexpr (kPk) {
-        pk_set_gh(ra[u], gq, hq);
-        reinterpret_cast<uint4*>(d.bins)[i] = ra[u];  // the whole 16-byte record: full lines per wave
-        if (d.ablate != 21) hist_add_pk<FT4>(s_hist, hl, ra[u]);
-      } else {
-        rb[u].z = (uint32_t)hq;
-        rb[u].w = (uint32_t)(int32_t)gq;
-        reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
-        if (d.ablate != 21) hist_add_rec32<FT4, kWide>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
-      }
+      rb[u].z = (uint32_t)hq;
+      rb[u].w = (uint32_t)(int32_t)gq;
+      reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
+      if (d.ablate != 21) hist_add_rec32<FT4, kWide>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
     }
   }
   __syncthreads();
@@ -1169,9 +1091,9 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
 
 // U rows in flight per thread; 2 per CU of 512 threads at 95 VGPRs (no waves-per-EU bound: capping U = 2
 // at 80 VGPRs spills, 276.5 vs 269.7 ms per 10M fit)
-template <int U, int FT4, bool kPk, bool kWide = false>
+template <int U, int FT4, bool kWide = false>
 __global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
-  grad_hist_body<U, FT4, kPk, kWide>(d, tree, apply_tree, chunk);
+  grad_hist_body<U, FT4, kWide>(d, tree, apply_tree, chunk);
 }
 
 
@@ -1259,58 +1181,17 @@ __device__ __forceinline__ void hist_rows_pair(const GbdtDev& d, uint64_t* s_his
   }
 }
 
-// Packed 16-byte records: one lane per row, one 16-byte load per row (a wave-instruction gathers 64
-// whole records), U rows in flight per lane with the next rows' ids prefetched one iteration ahead.
-template <int FT4>
-__device__ __forceinline__ void hist_rows_pk(const GbdtDev& d, uint64_t* s_hist, const HistLanes& hl,
-                                             const int32_t* rix, bool identity, int begin, int end, int64_t& tg,
-                                             int64_t& th) {
-  constexpr int U = 6;
-  const int B = (int)blockDim.x;
-  const uint4* recs = reinterpret_cast<const uint4*>(d.bins);
-  const int ilast = max(end - 1, begin);
-  int rn[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = begin + (int)threadIdx.x + u * B;
-    const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
-    rn[u] = i < end ? rv : -1;
-  }
-  for (int i0 = begin + (int)threadIdx.x; i0 < end; i0 += U * B) {
-    int r[U];
-    uint4 x[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) r[u] = rn[u];
-#pragma unroll
-    for (int u = 0; u < U; ++u) x[u] = recs[r[u] >= 0 ? r[u] : r[0]];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + U * B + u * B;
-      const int rv = identity ? min(i, ilast) : rix[min(i, ilast)];
-      rn[u] = i < end ? rv : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (r[u] < 0) { x[u].w = 0u; x[u].z &= 0x0FFFFFFFu; }  // no row: a zero pair
-      tg += (int64_t)pk_g(x[u]);
-      th += (int64_t)pk_h(x[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) hist_add_pk<FT4>(s_hist, hl, x[u]);
-  }
-}
-
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
 
 // FT4 > 0: 32-byte records with one tile of <= FT4 features (FT4 = F rounded up to 4); 0: generic rows.
 // (6 waves per SIMD = the 3 blocks per CU that the LDS tile allows: keeps the kernel within 80 VGPRs)
-// PAIR: the lane-pair record gathers of hist_rows_pair (FT4 >= 16); kPk: packed 16-byte records.
+// PAIR: the lane-pair record gathers of hist_rows_pair (FT4 >= 16).
 // kWide: wide gradients (16-byte LDS cells; the one-lane-per-row 32-byte path only).
 // (wide cells: one block per CU by LDS, 2 waves per SIMD -- twice the rows in flight per thread instead)
-template <int FT4, bool PAIR, bool kPk = false, bool kWide = false>
+template <int FT4, bool PAIR, bool kWide = false>
 __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(kWide ? 2 : 6))) void k_hist(
     GbdtDev d, int parity, int tree, int level, int chunk) {
-  static_assert(!kWide || (FT4 > 0 && !PAIR && !kPk), "wide cells: 32-byte records, one lane per row");
+  static_assert(!kWide || (FT4 > 0 && !PAIR), "wide cells: 32-byte records, one lane per row");
   constexpr int kW = kWide ? 2 : 1;
   constexpr uint32_t kCs = kWide ? 4u : 3u;
   BlockStamp stamp_(d);
@@ -1357,9 +1238,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(kW
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
   constexpr int U = kWide ? 8 : 4;  // rows in flight per thread
-  if constexpr (kPk) {
-    hist_rows_pk<FT4>(d, s_hist, hl, rix, identity, w.begin, w.end, tg, th);
-  } else if constexpr (PAIR) {
+  if constexpr (PAIR) {
     hist_rows_pair<FT4>(d, s_hist, hl, rix, identity, w.begin, w.end, tg, th);
   } else if constexpr (FT4 > 0) {
     // 32-byte records (bins | pad | (g,h)): one pair of 16-byte loads per row
@@ -2402,30 +2281,33 @@ __device__ __forceinline__ bool split_decision(const GbdtDev& d, const Cand& bes
   return ok;
 }
 
-// A node's split decision as ONE 8-byte granule {tag, decision} (kMode 2): written by the node's
-// evaluator block with a write-through store, polled by the node's partition blocks.
+// A node's split decision as ONE 8-byte granule {tag, decision} (evaluator-block modes): written by the
+// node's evaluator block with a write-through store, polled by the node's partition blocks.
 __device__ __forceinline__ uint64_t decision_word(uint32_t tag, bool ok, bool fail, int f, int j, bool dl) {
   const uint32_t v = (ok ? 1u : 0u) | (fail ? 2u : 0u) | (dl ? 4u : 0u) | ((uint32_t)(j + 1) & 0x3FFu) << 3 |
                      (uint32_t)f << 13;
   return ((uint64_t)tag << 32) | v;
 }
 
-// kMode 0: one GPU. 1: data parallel with the level's global histograms already in hist_b (RCCL / the
-// separate IPC exchange kernel): every block evaluates its node. In both, every active node gets an
-// item (possibly empty, kMode 1), so each rank finalises every node of the level, also those it holds no
-// rows of.
-// kMode 2: data parallel over the fused IPC exchange. Blocks 0 .. 2^level - 1 are the level's EVALUATOR
-// blocks -- one per node position, exactly k_eval<false, true, true>: the exchange (block 0 publishes,
-// every evaluator sums its node's cells over the ranks), node ownership on the deep levels, the replica
-// digest -- and each publishes its node's decision granule; the blocks after them are the partition
-// items, which plan and load their row ids while the evaluation runs and then poll their node's granule
-// (one lane, bounded by the group's deadline). One evaluation per node (no xGMI traffic multiplied by the
-// items) and no k_eval -> k_partition boundary. The host launches it only while the whole grid is
-// resident at once (evaluators + items <= CUs): a waiting item never holds a CU its evaluator needs.
+// Every block evaluates its node (the items fit one block per CU):
+//   kMode 0: one GPU. 1: data parallel with the level's global histograms already in hist_b (RCCL / the
+//   separate IPC exchange kernel); every active node gets an item (possibly empty), so each rank
+//   finalises every node of the level, also those it holds no rows of.
+// EVALUATOR blocks: blocks 0 .. 2^level - 1 evaluate one node position each, exactly as k_eval does,
+// finalise it and publish its decision granule; the blocks after them are the partition items, which
+// plan and load their row ids while the evaluation runs and then poll their node's granule (one lane,
+// bounded). One evaluation per node and no k_eval -> k_partition boundary, at any item count:
+//   kMode 2: data parallel over the fused IPC exchange (k_eval<false, true, true>: block 0 publishes the
+//   epoch, every evaluator sums its node's cells over the ranks; node ownership on the deep levels; the
+//   replica digest); 3: one GPU, the level's items exceed the CUs; 4: data parallel over hist_b, ditto.
+// Forward progress does not need the grid resident: blocks are dispatched in index order on every XCD,
+// so the evaluators hold CUs before any item does, and no evaluator waits on an item.
 template <int kSteps, int kMode>
 __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64_t zero_next, int level, int chunk,
                                                     int tree, EvalSlots es, uint32_t tag) {
-  constexpr bool kDP = kMode != 0;
+  constexpr bool kDP = kMode == 1 || kMode == 2 || kMode == 4;
+  constexpr bool kEvalBlocks = kMode >= 2;
+  constexpr bool kIpc = kMode == 2;
   constexpr int kPW = 16;  // waves
   BlockStamp stamp_(d);
   __shared__ int32_t s_cnt[2][kPW];
@@ -2435,12 +2317,26 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   // kMode 2: the evaluators do, see below)
   int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
   const int64_t nz = zero_next / 2;
-  if (kMode != 2)
+  if (!kIpc)
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
       zp[e] = make_int4(0, 0, 0, 0);
   const int nlev = 1 << level;
   const int first = nlev - 1;
-  if (kMode == 2 && (int)blockIdx.x < nlev) {  // the evaluator of node first + blockIdx.x
+  if (kEvalBlocks && !kIpc && (int)blockIdx.x < nlev) {  // the evaluator of node first + blockIdx.x
+    const int pos = blockIdx.x, n = first + pos;
+    const bool good = eval_core<false, false, kDP>(d, level, parity, tree, d.F, es, pos, stamp_, &s_out);
+    if (threadIdx.x == 0 && good) {  // (an inactive node has no partition items)
+      int f = 0, j = -1;
+      bool dl = false;
+      const bool ok = split_decision(d, s_out.best, s_out.nb, f, j, dl);
+      eval_finalize<kDP>(d, level, n, s_out.G, s_out.H, s_out.best, s_out.cut, s_out.nb);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(d.dec) + n,
+                         (unsigned long long)decision_word(tag, ok, false, f, j, dl), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (kIpc && (int)blockIdx.x < nlev) {  // the evaluator of node first + blockIdx.x
     const int pos = blockIdx.x, n = first + pos;
     const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
     const bool owned = d.own_level >= 0 && level >= d.own_level;
@@ -2480,7 +2376,7 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
       zp[e] = make_int4(0, 0, 0, 0);
     return;
   }
-  const int item = kMode == 2 ? (int)blockIdx.x - nlev : (int)blockIdx.x;
+  const int item = kEvalBlocks ? (int)blockIdx.x - nlev : (int)blockIdx.x;
   // this block's item: the root's rows are fixed slices; deeper levels' items are planned by every
   // block (block_plan over the level's node table)
   PlanOut pl;
@@ -2521,19 +2417,21 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   int f, j;
   bool dlb, ok;
   load_rows();
-  if constexpr (kMode == 2) {  // the node's evaluator decides; the row ids are in flight meanwhile
+  if constexpr (kEvalBlocks) {  // the node's evaluator decides; the row ids are in flight meanwhile
     if (len == 0) return;
     __shared__ uint32_t s_dec;
     if (threadIdx.x == 0) {
-      const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
+      // (bounded: the exchange's deadline; without an exchange 20 s, which no evaluator approaches)
+      const IpcFusedView* iv = kIpc ? d.ipcv + (d.ipc_epoch & 1u) : nullptr;
+      const uint64_t limit = kIpc ? iv->timeout : 2000000000ull;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t v = 2u;  // failed unless the evaluator's granule arrives
       for (;;) {
         const uint64_t w = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(d.dec) + node,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((uint32_t)(w >> 32) == tag) { v = (uint32_t)w; break; }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > iv->timeout) {
-          ipc_fail(iv->myflag, iv->err_host);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
+          if (kIpc) ipc_fail(iv->myflag, iv->err_host);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -2627,11 +2525,10 @@ struct GbdtCtx {
   std::vector<int32_t> hoff_h;  // host copy of d.hoff (sizes k_eval's fused-exchange LDS)
   int fit_first = 0;            // first tree this context grows in the current fit (no replica check)
   int fault_tree = -1;          // fault injection: tree whose root totals are perturbed on this rank
-  uint32_t* pk_buf = nullptr;   // packed records: the code layout (cobalt_gbdt_set_pack)
   uint32_t dec_tag = 0;         // k_eval_part<.., 2>: the launch tag of the decision granules (d.dec)
-  // the last grow call's plan (cobalt_gbdt_plan): fused IPC exchange, ownership level, packed records,
+  // the last grow call's plan (cobalt_gbdt_plan): fused IPC exchange, ownership level, wide gradients,
   // resident blocks of the fused k_eval, levels run by the fused evaluation + partition pass
-  int32_t plan[5] = {0, -1, 0, 0, 0};
+  int32_t plan[6] = {0, -1, 0, 0, 0, 0};
   unsigned* err_pinned = nullptr;  // mapped host word behind d.err_host
   // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
   const char* stamp_path = nullptr;
@@ -2742,19 +2639,10 @@ static int chunk_part(const GbdtDev& d) {
 typedef void (*HistKernel)(GbdtDev, int, int, int, int);
 typedef void (*GradHistKernel)(GbdtDev, int, int, int);
 static int hist_ft4(const GbdtDev& d) {
-  return ((d.stride == 32 || d.packed) && d.F <= 24 && d.feat_tile >= d.F) ? (d.F + 3) / 4 * 4 : 0;
+  return (d.stride == 32 && d.F <= 24 && d.feat_tile >= d.F) ? (d.F + 3) / 4 * 4 : 0;
 }
-static HistKernel hist_kernel(int ft4, bool pair, bool packed = false, bool wide = false) {
+static HistKernel hist_kernel(int ft4, bool pair, bool wide = false) {
   if (wide) switch (ft4) {
-    case 4: return k_hist<4, false, false, true>;
-    case 8: return k_hist<8, false, false, true>;
-    case 12: return k_hist<12, false, false, true>;
-    case 16: return k_hist<16, false, false, true>;
-    case 20: return k_hist<20, false, false, true>;
-    case 24: return k_hist<24, false, false, true>;
-    default: return nullptr;
-  }
-  if (packed) switch (ft4) {
     case 4: return k_hist<4, false, true>;
     case 8: return k_hist<8, false, true>;
     case 12: return k_hist<12, false, true>;
@@ -2773,17 +2661,8 @@ static HistKernel hist_kernel(int ft4, bool pair, bool packed = false, bool wide
     default: return k_hist<0, false>;
   }
 }
-static GradHistKernel grad_hist_kernel(int ft4, bool packed = false, bool wide = false) {
+static GradHistKernel grad_hist_kernel(int ft4, bool wide = false) {
   if (wide) switch (ft4) {
-    case 4: return k_grad_hist<2, 4, false, true>;
-    case 8: return k_grad_hist<2, 8, false, true>;
-    case 12: return k_grad_hist<2, 12, false, true>;
-    case 16: return k_grad_hist<2, 16, false, true>;
-    case 20: return k_grad_hist<2, 20, false, true>;
-    case 24: return k_grad_hist<2, 24, false, true>;
-    default: return nullptr;
-  }
-  if (packed) switch (ft4) {
     case 4: return k_grad_hist<2, 4, true>;
     case 8: return k_grad_hist<2, 8, true>;
     case 12: return k_grad_hist<2, 12, true>;
@@ -2828,20 +2707,14 @@ static int dev_alloc(GbdtCtx* c, void** p, size_t bytes) {
 COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   if (cfg->max_depth < 1 || cfg->max_depth > 10) return -1;
   if (cfg->chunk < 64 || cfg->chunk > 16384) return -2;
-  // packed 16-byte records (<= 24 features; the layout comes with cobalt_gbdt_set_pack). (A 16-byte
-  // stride alone does not say it: 32-byte-layout records of <= 8 features are 16 bytes wide too.)
-  const bool packed = cfg->packed != 0;
-  if (packed && cfg->row_stride != 16) return -3;
-  if (packed ? (cfg->n_feat > 24 || cfg->feat_tile < cfg->n_feat)
-             : (cfg->row_stride % 16 != 0 || cfg->row_stride < ((cfg->n_feat + 7) / 8) * 8 + 8))
-    return -3;
+  if (cfg->row_stride % 16 != 0 || cfg->row_stride < ((cfg->n_feat + 7) / 8) * 8 + 8) return -3;
   if (cfg->feat_tile % 4 != 0 || cfg->feat_tile <= 0 || cfg->feat_tile > 64) return -4;
   if (cfg->n_rows >= (int64_t)INT32_MAX) return -5;
   // wide gradients: 32-byte records with one feature tile (the fast histogram path) only
   const int gbits = cfg->grad_bits > 0 ? cfg->grad_bits : 17;
   if (gbits != 17 && gbits != 25) return -6;
   const bool wide = gbits == 25;
-  if (wide && (packed || cfg->row_stride != 32 || cfg->n_feat > 24 || cfg->feat_tile < cfg->n_feat)) return -6;
+  if (wide && (cfg->row_stride != 32 || cfg->n_feat > 24 || cfg->feat_tile < cfg->n_feat)) return -6;
   GbdtCtx* c = new GbdtCtx();
   c->cfg = *cfg;
   const int F = cfg->n_feat;
@@ -2861,7 +2734,6 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   d.row_offset = cfg->row_offset;
   d.F = F;
   d.stride = cfg->row_stride;
-  d.packed = packed ? 1 : 0;
   d.goff = ((F + 7) / 8) * 8;
   d.max_depth = cfg->max_depth;
   d.max_nodes = c->max_nodes;
@@ -2919,17 +2791,14 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
     memset(c->err_pinned, 0, 64);
     CK(hipHostGetDevicePointer((void**)&d.err_host, c->err_pinned, 0));
     d.world = cfg->world_size;
-    if ((rc = dev_alloc(c, (void**)&d.dec, c->max_nodes * sizeof(uint64_t)))) return rc;
-    CK(hipMemset(d.dec, 0, c->max_nodes * sizeof(uint64_t)));  // (tags start at 1)
   }
+  if ((rc = dev_alloc(c, (void**)&d.dec, c->max_nodes * sizeof(uint64_t)))) return rc;
+  CK(hipMemset(d.dec, 0, c->max_nodes * sizeof(uint64_t)));  // (tags start at 1)
   if ((rc = dev_alloc(c, (void**)&d.slab, (size_t)c->items_cap * F * kMaxBins * sizeof(uint64_t) * (wide ? 2 : 1))))
     return rc;
   if ((rc = dev_alloc(c, (void**)&d.slab_tot, (size_t)c->items_cap * 2 * sizeof(int64_t)))) return rc;
   const int ntiles = ceil_div(F, cfg->feat_tile);
   if ((rc = dev_alloc(c, (void**)&d.layout, F * sizeof(int2)))) return rc;
-  if ((rc = dev_alloc(c, (void**)&c->pk_buf, 24 * sizeof(uint32_t)))) return rc;
-  CK(hipMemset(c->pk_buf, 0, 24 * sizeof(uint32_t)));
-  d.pk = c->pk_buf;
   if ((rc = dev_alloc(c, (void**)&d.hoff, (F + 1) * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, (void**)&d.tile_entries, ntiles * sizeof(int32_t)))) return rc;
   d.stamps = nullptr;
@@ -3044,13 +2913,13 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   const bool wide = c->d.wide != 0;
   c->lds_hist = (size_t)(max_ent + kWave) * sizeof(uint64_t) * (wide ? 2 : 1);
   if (c->lds_hist > 64 * 1024) {
-    for (int v = 0; v < 4; ++v)
-      if (HistKernel k = hist_kernel(hist_ft4(c->d), v == 1, v == 2, v == 3))
+    for (int v = 0; v < 3; ++v)
+      if (HistKernel k = hist_kernel(hist_ft4(c->d), v == 1, v == 2))
         CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
   const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
-  if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0, wide))
-    CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d), c->d.packed != 0, wide),
+  if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d), wide))
+    CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d), wide),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
   return 0;
 }
@@ -3061,9 +2930,23 @@ static void launch_eval_part(int steps, int mode, dim3 grid, size_t lds, hipStre
 #define EP_LAUNCH(S, M) \
   hipLaunchKernelGGL((k_eval_part<S, M>), grid, dim3(1024), lds, stream, d, parity, zero_next, level, chunk, tree, es, tag)
   if (steps <= 4) {
-    if (mode == 0) EP_LAUNCH(4, 0); else if (mode == 1) EP_LAUNCH(4, 1); else EP_LAUNCH(4, 2);
+    switch (mode) {
+      case 0: EP_LAUNCH(4, 0); break;
+      case 1: EP_LAUNCH(4, 1); break;
+      case 2: EP_LAUNCH(4, 2); break;
+      case 3: EP_LAUNCH(4, 3); break;
+      default: EP_LAUNCH(4, 4); break;
+    }
+  } else if (steps <= 6 && mode <= 1) {  // (1.25M rows: 6144-row items; the 8-step form spills 2 VGPRs)
+    if (mode == 0) EP_LAUNCH(6, 0); else EP_LAUNCH(6, 1);
   } else {
-    if (mode == 0) EP_LAUNCH(8, 0); else if (mode == 1) EP_LAUNCH(8, 1); else EP_LAUNCH(8, 2);
+    switch (mode) {
+      case 0: EP_LAUNCH(8, 0); break;
+      case 1: EP_LAUNCH(8, 1); break;
+      case 2: EP_LAUNCH(8, 2); break;
+      case 3: EP_LAUNCH(8, 3); break;
+      default: EP_LAUNCH(8, 4); break;
+    }
   }
 #undef EP_LAUNCH
 }
@@ -3097,9 +2980,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   }
   // gradients + root histogram in one pass (32-byte records, one feature tile)
   const int ft4 = hist_ft4(d);
-  // (packed records have no unfused root pass: k_grad reads the 32-byte layout)
-  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.packed || d.ablate == 0 || d.ablate >= 10);
-  if (d.packed && (!fuse_root || sampled)) return -15;
+  const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.ablate == 0 || d.ablate >= 10);
   if (d.wide && sampled) return -15;  // (the sampled pages carry 17-bit pairs)
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
@@ -3136,23 +3017,23 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const bool ipc_fused = ipc && env_ipc_fused != 0 && fused_lds <= 65536 && resident >= deepest_grid;
   d.ipc_epoch = 0;
   d.ipcv = ipc_fused ? ipc_device_views(cc) : nullptr;
-  // split evaluation fused into the partition pass (k_eval_part): one launch per level fewer, but every
-  // partition block repeats its node's evaluation, so only while the level's items fit one block per CU
-  // (1M rows: 248.0 -> 239.3 us per tree in the stamps; 1.25M: 87.0 -> 96.3 ms per fit, 2.5M 112 -> 130:
-  // two evaluations per CU). COBALT_EVAL_PART=0 / 2 disables / forces it. Under data parallelism it needs
-  // the level's global histograms in hist_b before it runs (RCCL, or the separate IPC exchange kernel);
-  // over the fused IPC exchange its evaluator-block form (k_eval_part<.., 2>: one evaluating block per
-  // node, the exchange and node ownership exactly as k_eval, the items wait for their node's decision)
-  // while the whole grid -- evaluators + items -- fits one block per CU (COBALT_DP_EVAL_PART=0: k_eval +
-  // k_partition).
+  // Split evaluation fused into the partition pass (k_eval_part): one launch per level fewer.
+  //  * While a level's items fit one 1024-thread block per CU, every partition block evaluates its node
+  //    itself (modes 0 / 1; 1M rows: 248.0 -> 239.3 us per tree in the stamps). Under data parallelism
+  //    that needs the level's global histograms in hist_b first (RCCL, or the separate IPC exchange).
+  //  * Beyond that (a second evaluation per CU cost more than it saved: 1.25M 87.0 -> 96.3 ms per fit in
+  //    round 3), and always over the fused IPC exchange, the evaluator-block form (modes 3 / 4 / 2): one
+  //    evaluating block per node, the items wait for their node's decision granule.
+  // COBALT_EVAL_PART=0 disables both (k_eval + k_partition), 2 forces the every-block form on one GPU;
+  // COBALT_EVAL_BLOCKS=0 disables the evaluator-block form.
   static const int env_ep = knob_int(Knob::EvalPart, 1);
-  static const int env_dp_ep = knob_int(Knob::DpEvalPart, 1);
+  static const int env_eb = knob_int(Knob::EvalBlocks, 1);
   const int ep_steps = ceil_div(chunk_part(d), 16 * kWave);
-  bool ep_split = false;  // k_eval_part<.., 2> fits a CU with the fused exchange's LDS
-  if (ipc_fused && env_dp_ep) {
+  bool eb_ok = env_eb != 0;  // (over the fused exchange: a CU holds the kernel with the exchange's LDS)
+  if (ipc_fused && eb_ok) {
     int per_cu = 0;
-    ep_split = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_eval_part<8, 2>, 1024, fused_lds) ==
-                   hipSuccess && per_cu >= 1;
+    eb_ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_eval_part<8, 2>, 1024, fused_lds) ==
+                hipSuccess && per_cu >= 1;
   }
   // node ownership (see node_owner): over the fused exchange (k_eval, or k_eval_part's evaluator blocks),
   // on the three deepest split levels (where the exchange volume is: 56 of a depth-7 tree's 64 pairs;
@@ -3166,33 +3047,39 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     l0 = std::max(l0, D - 3);
     d.own_level = l0 < D ? l0 : -1;
   }
-  const bool eval_part = env_ep != 0 && (!ipc_fused || ep_split) && eval_fg == 0 && ep_steps <= 8 && d.F <= 32;
-  const int ep_mode = ipc_fused ? 2 : (dp ? 1 : 0);
-  const int ep_extra = ep_mode == 2 ? 2 : 1;  // grid beyond the items: one partial item (+ one evaluator) per node
+  const bool eval_part = env_ep != 0 && (!ipc_fused || eb_ok) && eval_fg == 0 && ep_steps <= 8 && d.F <= 32;
+  // A level's fused pass: {item rows (0: separate k_eval + k_partition), mode}. Every-block form: the
+  // smallest item (1024-row steps from 4096) whose grid -- items + one partial item per node -- is one
+  // block per CU (a second round of blocks doubles the level; 1.25M rows: 6144 at every level).
+  // Evaluator-block form: the same rule with one more block per node while it fits, else chunk_part.
+  auto ep_plan = [&](int level, int& mode) -> int {
+    mode = 0;
+    if (!eval_part || level + 1 >= D) return 0;
+    const int cus = device_cu_count();
+    const int extra = (ipc_fused ? 2 : 1) << level;
+    for (int ch = std::min(4096, chunk_part(d)); ch <= 8192; ch += 1024)
+      if (ceil_div(d.n, ch) + extra <= cus) {
+        mode = ipc_fused ? 2 : (dp ? 1 : 0);
+        return ch;
+      }
+    if (ipc_fused) { mode = 2; return chunk_part(d); }
+    if (env_ep == 2 && !dp) return 8192;
+    if (eb_ok) { mode = dp ? 4 : 3; return chunk_part(d); }
+    return 0;
+  };
   c->plan[0] = ipc_fused ? 1 : 0;
   c->plan[1] = d.own_level;
-  c->plan[2] = d.packed;
+  c->plan[2] = d.wide;
   c->plan[3] = resident;
-  c->plan[4] = 0;  // levels run by the fused evaluation + partition pass (bit mask, set below)
-  for (int level = 0; level + 1 < D; ++level)
-    if (eval_part) {
-      const int cus = device_cu_count();
-      for (int ch = std::min(4096, chunk_part(d)); ch <= 8192; ch += 1024)
-        if (ceil_div(d.n, ch) + (ep_extra << level) <= cus) { c->plan[4] |= 1 << level; break; }
+  c->plan[4] = 0;  // levels run by the fused evaluation + partition pass (bit mask)
+  c->plan[5] = 0;  // ... of them in the evaluator-block form
+  for (int level = 0; level + 1 < D; ++level) {
+    int m = 0;
+    if (ep_plan(level, m) > 0) {
+      c->plan[4] |= 1 << level;
+      if (m >= 2) c->plan[5] |= 1 << level;
     }
-  // Item size of a level's fused pass: the grid (items + one partial item per node) fits one 1024-thread
-  // block per CU -- beyond that a second round of blocks doubles the level (1M rows with 4096-row items:
-  // levels 4-5 launched 261 / 277 blocks on 256 CUs). The smallest item (in 1024-row steps from 4096)
-  // whose grid is one block per CU (a level whose 4096-row items overflow the CUs takes 5120 / 6144 / 7168
-  // instead of jumping to 8192: 1.25M rows: 6144 at every level), else the level runs the separate
-  // evaluation + partition (0). COBALT_EVAL_PART=2 forces the fusion on one GPU (8192-row items).
-  auto ep_chunk = [&](int level) -> int {
-    if (!eval_part) return 0;
-    const int cus = device_cu_count();
-    for (int ch = std::min(4096, chunk_part(d)); ch <= 8192; ch += 1024)
-      if (ceil_div(d.n, ch) + (ep_extra << level) <= cus) return ch;
-    return (env_ep == 2 && !dp) ? 8192 : 0;
-  };
+  }
   d.zero_red = nullptr;
   // root items of the fused pass: <= 8192 rows (more blocks in flight than the 16384-row k_hist items);
   // COBALT_ROOT_CHUNK overrides (tuning experiments; multiple of 64 in [1024, 16384])
@@ -3229,7 +3116,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
               stream, d);
     else if (fuse_root)
-      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.packed != 0, d.wide != 0), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
+      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.wide != 0), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
               stream, d, t, apply, root_chunk);
     else
       GLAUNCH("k_grad", k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
@@ -3238,7 +3125,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     for (int level = 0; level < D; ++level) {
       const int parity = level & 1;
       // this level's evaluation runs in the partition pass (k_eval_part) with items of ep_ch rows
-      const int ep_ch = level + 1 < D ? ep_chunk(level) : 0;
+      int ep_mode = 0;
+      const int ep_ch = ep_plan(level, ep_mode);
       const bool ep_level = ep_ch > 0;
       d.ep_chunk = ep_ch;
       d.ep_zero = dp ? 1 : 0;
@@ -3251,7 +3139,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       const int ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
                                                : ceil_div(d.n, chh) + (1 << level);
       if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0, d.packed != 0, d.wide != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
+        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0, d.wide != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
                 stream, d, parity, t, level, chh);
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       const dim3 rgrid(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256));
@@ -3312,7 +3200,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         const int steps = ceil_div(chp, 16 * kWave);  // <= 8 (chunk_part's cap)
         if (ep_level) {
           c->d.seq = stamp_next(c, "k_eval_part");
-          const int evals = ep_mode == 2 ? (1 << level) : 0;
+          const int evals = ep_mode >= 2 ? (1 << level) : 0;  // the evaluator blocks come first
           launch_eval_part(steps, ep_mode, dim3(ubp + evals), ep_mode == 2 ? fused_lds : 0, stream, d, parity, zero_next,
                            level, chp, t, c->eval_slots, ++c->dec_tag);
         } else if (steps <= 4)
@@ -3651,37 +3539,17 @@ __global__ __launch_bounds__(256) void k_put_label(uint8_t* bins, const float* l
     bins[i * 32 + 23] = label[i] != 0.0f ? 1 : 0;
 }
 
-__global__ __launch_bounds__(256) void k_put_label_pk(uint4* recs, const float* label, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    uint4 r = recs[i];
-    r.z = (r.z & ~(1u << kPkLabelBit)) | ((label[i] != 0.0f ? 1u : 0u) << kPkLabelBit);
-    recs[i] = r;
-  }
-}
-
 COBALT_API int cobalt_gbdt_set_binary_labels(void* h, float spw, hipStream_t stream) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   GbdtDev& d = c->d;
-  if (!d.bins || !d.label || (!d.packed && (d.stride != 32 || d.F > 23))) return -13;
+  if (!d.bins || !d.label || d.stride != 32 || d.F > 23) return -13;
   if (d.n > 0) {
     const int grid = std::min(ceil_div(d.n, 256), 4096);
-    if (d.packed)
-      hipLaunchKernelGGL(k_put_label_pk, dim3(grid), dim3(256), 0, stream, reinterpret_cast<uint4*>(d.bins), d.label, d.n);
-    else
-      hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
+    hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
     CK(hipGetLastError());
   }
   d.ylab = 1;
   d.spw = spw;
-  return 0;
-}
-
-// The packed-record layout (cobalt_pack_layout's out, host memory) of a context created with row_stride 16.
-COBALT_API int cobalt_gbdt_set_pack(void* h, const int32_t* layout) {
-  GbdtCtx* c = static_cast<GbdtCtx*>(h);
-  if (!c->d.packed || !c->pk_buf) return -3;
-  CK(hipMemcpy(c->pk_buf, layout, c->d.F * sizeof(int32_t), hipMemcpyHostToDevice));
-  c->d.pk = c->pk_buf;
   return 0;
 }
 
@@ -3695,11 +3563,11 @@ COBALT_API int cobalt_gbdt_set_start(void* h, int t0) {
 }
 
 // The last grow call's launch plan (GbdtCtx::plan): out[0] fused IPC exchange, [1] node-ownership level
-// (-1 off), [2] packed records, [3] blocks of the fused k_eval this rank's CUs hold at once, [4] bit mask of
-// the levels run by the fused evaluation + partition pass.
+// (-1 off), [2] wide gradients, [3] blocks of the fused k_eval this rank's CUs hold at once, [4] bit mask of
+// the levels run by the fused evaluation + partition pass, [5] of them in the evaluator-block form.
 COBALT_API int cobalt_gbdt_plan(void* h, int32_t* out) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
-  for (int k = 0; k < 5; ++k) out[k] = c->plan[k];
+  for (int k = 0; k < 6; ++k) out[k] = c->plan[k];
   return 0;
 }
 
@@ -3728,7 +3596,7 @@ COBALT_API int cobalt_gbdt_reuse(void* h, const GbdtConfig* cfg) {
   if (o.n_rows != cfg->n_rows || o.n_feat != cfg->n_feat || o.row_stride != cfg->row_stride ||
       o.max_depth != cfg->max_depth || o.max_trees != cfg->max_trees || o.chunk != cfg->chunk ||
       o.feat_tile != cfg->feat_tile || o.world_size != cfg->world_size || o.comm != cfg->comm ||
-      (o.grad_bits > 17) != (cfg->grad_bits > 17) || o.packed != cfg->packed)
+      (o.grad_bits > 17) != (cfg->grad_bits > 17))
     return 1;
   c->cfg = *cfg;
   GbdtDev& d = c->d;
@@ -3812,106 +3680,6 @@ __global__ __launch_bounds__(256) void k_bin_rec32(const float* __restrict__ X, 
     rec[0] = make_uint4(w[0], w[1], w[2], w[3]);
     rec[1] = make_uint4(w[4], w[5], 0u, 0u);
   }
-}
-
-// Packed 16-byte records (see pk_code): the layout of F features from their bin counts -- each code
-// ceil(log2(nbins + 1)) bits (8 for 256 bins), placed first-fit in order of decreasing width into
-// dword 0, dword 1 and the low 27 bits of dword 2, never across a dword. out[f] = bit offset | width << 8.
-// Returns 1 when every feature fits (F <= 24), else 0 (the caller keeps 32-byte records).
-COBALT_API int cobalt_pack_layout(const int32_t* nbins, int F, int32_t* out) {
-  if (F < 1 || F > 24) return 0;
-  int cap[3] = {32, 32, (int)kPkLabelBit}, used[3] = {0, 0, 0};
-  std::vector<int> order(F), width(F);
-  for (int f = 0; f < F; ++f) {
-    const int nb = std::max(1, std::min(256, (int)nbins[f]));
-    int w = 1;
-    if (nb >= 256) w = 8;
-    else while ((1 << w) < nb + 1) ++w;
-    width[f] = w;
-    order[f] = f;
-  }
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return width[a] > width[b]; });
-  for (int f : order) {
-    int k = 0;
-    while (k < 3 && used[k] + width[f] > cap[k]) ++k;
-    if (k == 3) return 0;
-    out[f] = (k * 32 + used[k]) | (width[f] << 8);
-    used[k] += width[f];
-  }
-  return 1;
-}
-
-template <int F4>
-__global__ __launch_bounds__(256) void k_bin_pk(const float* __restrict__ X, int64_t n, const float* __restrict__ cuts,
-                                                const int32_t* __restrict__ nbins, const int32_t* __restrict__ pack,
-                                                uint4* __restrict__ recs, uint8_t* __restrict__ binsT, int64_t ldt) {
-  constexpr int F = 4 * F4;
-  __shared__ float s_cuts[F * kMaxBins];
-  __shared__ int s_nb[F];
-  __shared__ uint32_t s_pk[F];
-  for (int i = threadIdx.x; i < F * kMaxBins; i += blockDim.x) s_cuts[i] = cuts[i];
-  if (threadIdx.x < F) {
-    s_nb[threadIdx.x] = nbins[threadIdx.x];
-    s_pk[threadIdx.x] = (uint32_t)pack[threadIdx.x];
-  }
-  __syncthreads();
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < n;
-       row += (int64_t)gridDim.x * blockDim.x) {
-    const float4* x4 = reinterpret_cast<const float4*>(X + row * F);
-    float v[F];
-#pragma unroll
-    for (int q = 0; q < F4; ++q) {
-      const float4 t = x4[q];
-      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
-    }
-    uint32_t w[3] = {0, 0, 0};
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-      const int nb = s_nb[f];
-      const uint32_t pk = s_pk[f];
-      const uint32_t width = (pk >> 8) & 0xFu, off = pk & 0x7Fu;
-      uint32_t b, code;
-      if (v[f] != v[f]) {
-        b = kMissingBin;
-        code = (1u << width) - 1u;
-      } else {  // upper_bound over cuts[f][0..nb), clamped to nb - 1
-        const float* c = s_cuts + f * kMaxBins;
-        int lo = 0, hi = nb;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (c[mid] <= v[f]) lo = mid + 1; else hi = mid;
-        }
-        b = code = lo >= nb ? (uint32_t)(nb - 1) : (uint32_t)lo;
-      }
-      binsT[(int64_t)f * ldt + row] = (uint8_t)b;
-      const uint32_t k = off >> 5;
-      const uint32_t sh = code << (off & 31u);
-      w[0] |= k == 0 ? sh : 0u;
-      w[1] |= k == 1 ? sh : 0u;
-      w[2] |= k == 2 ? sh : 0u;
-    }
-    recs[row] = make_uint4(w[0], w[1], w[2], 0u);
-  }
-}
-
-// Quantise n rows into packed 16-byte records (layout from cobalt_pack_layout, a device int32 [F]) and the
-// feature-major bins (row pitch ldt). X: 16-byte aligned fp32 rows, F % 4 == 0.
-COBALT_API int cobalt_bin_matrix_pk(const float* X, int64_t n, int F, const float* cuts, const int32_t* nbins,
-                                    const int32_t* pack, void* recs, uint8_t* binsT, int64_t ldt, hipStream_t stream) {
-  if (F % 4 != 0 || F < 4 || F > 24 || ldt < n || (reinterpret_cast<uintptr_t>(X) & 15) != 0 ||
-      (reinterpret_cast<uintptr_t>(recs) & 15) != 0)
-    return -3;
-  if (n == 0) return 0;
-  const int grid = std::max(1, std::min(ceil_div(n, 256), 256 * 8));
-  switch (F / 4) {
-#define BINPK_CASE(K)                                                                                       \
-    case K: hipLaunchKernelGGL(k_bin_pk<K>, dim3(grid), dim3(256), 0, stream, X, n, cuts, nbins, pack,       \
-                               static_cast<uint4*>(recs), binsT, ldt); break;
-    BINPK_CASE(1) BINPK_CASE(2) BINPK_CASE(3) BINPK_CASE(4) BINPK_CASE(5) BINPK_CASE(6)
-#undef BINPK_CASE
-  }
-  CK_LAUNCH();
-  return 0;
 }
 
 COBALT_API int cobalt_bin_matrix_ld(const float* X, int64_t n, int F, int64_t ldx, const float* cuts,

@@ -156,7 +156,6 @@ class BinnedData:
     nbins: torch.Tensor
     records: torch.Tensor | None = None
     binsT: torch.Tensor | None = None
-    pack: np.ndarray | None = None          # packed 16-byte records: the code layout (ops/gbdt_ops.pack_layout)
     bins_host: np.ndarray | None = None
     t_sketch: float = 0.0
     t_bin: float = 0.0
@@ -225,7 +224,7 @@ def resolve_sketch_rows(sketch_rows: int | None, dev, n_rows_global: int | None 
 
 def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO, device=None, dist=None,
                 n_rows_global: int | None = None, row_offset: int = 0, sketch_weights=None,
-                sketch_mode: str = "sample", packed: bool = True) -> BinnedData:
+                sketch_mode: str = "sample") -> BinnedData:
     """Weighted quantile sketch (K12) on a global strided sample + binning (K13).
 
     ``sketch_rows`` None / 0: every row (XGBoost ``hist`` sketches all rows), exact weighted quantiles.
@@ -235,8 +234,7 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     rank summarises its shard and the summaries are merged (``sketch_mode="summary"``).
     ``sketch_weights`` ([N_local], optional): per-row sketch weights (see models/sketch.py).
     A feature gets 256 bins only if it has no missing value in the FULL data (all ranks).
-    ``SKETCH_AUTO``: every row on a GPU, the 2^18-row sample on the CPU. ``packed=False``: 32-byte
-    row records even where the packed 16-byte form fits (wide gradients need them)."""
+    ``SKETCH_AUTO``: every row on a GPU, the 2^18-row sample on the CPU."""
     dev = _resolve_device(device, X)
     world = dist.world if dist is not None else 1
     Xt = _to_tensor(X, dev)
@@ -259,7 +257,7 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
         t_sketch = time.perf_counter() - ts
         tb = time.perf_counter()
         bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
-        _bin_device(bd, Xt, cuts, nbins, packed)
+        _bin_device(bd, Xt, cuts, nbins)
         torch.cuda.synchronize(dev)
         bd.t_bin = time.perf_counter() - tb
         return bd
@@ -284,7 +282,7 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     tb = time.perf_counter()
     bd = BinnedData(dev, N, n_glob, F, row_offset, cuts, nbins, t_sketch=t_sketch)
     if dev.type == "cuda":
-        _bin_device(bd, Xt, cuts, nbins, packed)
+        _bin_device(bd, Xt, cuts, nbins)
         torch.cuda.synchronize(dev)
     else:
         bd.bins_host = sketch.bin_matrix_host(Xt.cpu().numpy(), cuts.cpu().numpy(), nbins.cpu().numpy())
@@ -292,17 +290,13 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     return bd
 
 
-def _bin_device(bd: BinnedData, Xt: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor,
-                packed: bool = True) -> None:
-    """Binning on the GPU: packed 16-byte row records where the codes fit (the gradient pass and the
-    histogram gathers move half the bytes), else 32-byte records; feature-major bins either way."""
+def _bin_device(bd: BinnedData, Xt: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> None:
+    """Binning on the GPU: row records (32 bytes for <= 24 features) + feature-major bins.
+    (Packed 16-byte records were measured slower in round 5 -- the per-feature bit-field extracts cost
+    the histogram gathers more than the halved bytes saved: profiles/round5/packed_vs_32byte.txt.)"""
     from ..ops import gbdt_ops
 
-    pk = gbdt_ops.bin_matrix_packed(Xt, cuts, nbins) if packed else None
-    if pk is not None:
-        bd.records, bd.binsT, bd.pack = pk
-    else:
-        bd.records, bd.binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
+    bd.records, bd.binsT = gbdt_ops.bin_matrix(Xt, cuts, nbins)
 
 
 def sketch_weights_for(params: "GBDTParams", y, sample_weight=None, device=None):
@@ -321,7 +315,7 @@ def sketch_weights_for(params: "GBDTParams", y, sample_weight=None, device=None)
 def subset_rows(bd: BinnedData, rows: np.ndarray) -> BinnedData:
     """Rows ``rows`` of a binned matrix with the same cuts (CV folds re-use one binning)."""
     idx = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=bd.device)
-    out = BinnedData(bd.device, len(rows), len(rows), bd.n_features, 0, bd.cuts, bd.nbins, pack=bd.pack)
+    out = BinnedData(bd.device, len(rows), len(rows), bd.n_features, 0, bd.cuts, bd.nbins)
     if bd.records is not None:
         out.records = bd.records.index_select(0, idx).contiguous()
         out.binsT = bd.binsT.index_select(1, idx).contiguous()
@@ -344,10 +338,7 @@ def subset_features(bd: BinnedData, feats) -> BinnedData:
         from ..ops import gbdt_ops
 
         rec = torch.zeros((bd.n_rows, gbdt_ops.row_stride(len(f))), dtype=torch.uint8, device=bd.device)
-        if bd.pack is not None:  # packed records: the narrower 32-byte records from the feature-major bins
-            rec[:, : len(f)] = bd.binsT.index_select(0, idx).t()
-        else:
-            rec[:, : len(f)] = bd.records.index_select(1, idx)
+        rec[:, : len(f)] = bd.records.index_select(1, idx)
         out.records = rec
         out.binsT = bd.binsT.index_select(0, idx).contiguous()
     else:
@@ -414,7 +405,7 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
     bd = bin_dataset(X, max_bin=params.max_bin, sketch_rows=params.sketch_rows, device=device, dist=dist,
                      n_rows_global=n_rows_global, row_offset=row_offset,
                      sketch_weights=sketch_weights_for(params, y, sample_weight, dev),
-                     sketch_mode=params.sketch_mode, packed=int(params.grad_bits) <= gbdt_host.QBITS)
+                     sketch_mode=params.sketch_mode)
     bst = train_binned(bd, y, params, sample_weight=sample_weight, feature_names=feature_names,
                        feature_types=feature_types, dist=dist, report=report, init_booster=init_booster,
                        init_margin=init_margin, total_trees=total, checkpoint=ckpt, exact_fp64=exact_fp64)
@@ -442,8 +433,6 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     grad_bits = int(params.grad_bits)
     if grad_bits not in gbdt_host.GRAD_BITS:
         raise ValueError(f"grad_bits must be one of {gbdt_host.GRAD_BITS}")
-    if grad_bits > gbdt_host.QBITS and bd.pack is not None:  # wide gradients: 32-byte records
-        bd = subset_features(bd, range(bd.n_features))
     N, F = bd.n_rows, bd.n_features
     rep = report if report is not None else FitReport()
     tp = rep.mark("pre", time.perf_counter(), dev)
@@ -554,16 +543,14 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                                      min_child_weight=hp.min_child_weight, subsample=hp.subsample,
                                      gscale=gscale, hscale=hscale, base_margin=base_margin,
                                      seed=hp.seed, row_offset=bd.row_offset, world_size=world, comm=comm,
-                                     packed=bd.pack is not None, grad_bits=grad_bits)
+                                     grad_bits=grad_bits)
         fm = torch.as_tensor(fmask_np, device=dev).contiguous()
         tr.set_data(bd.records, bd.binsT, bd.cuts.contiguous(), bd.nbins.to(torch.int32).contiguous(),
                     yt.contiguous(), wt, margin, fm)
-        if bd.pack is not None:
-            tr.set_pack(bd.pack)
         # 0/1 labels and no sample weights: the labels ride in the row records' padding and the weights
         # follow from them (8 fewer bytes per row in every gradient pass); COBALT_LABEL_IN_RECORD=0 off
         if (sample_weight is None and os.environ.get("COBALT_LABEL_IN_RECORD", "1") != "0"
-                and (bd.pack is not None or (bd.records.shape[1] == 32 and F <= 23))
+                and bd.records.shape[1] == 32 and F <= 23
                 and bool(((yt == 0) | (yt == 1)).all())):
             tr.set_binary_labels(float(np.float32(spw)))
         tp = rep.mark("trainer_setup", tp, dev)

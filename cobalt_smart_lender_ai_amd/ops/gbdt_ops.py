@@ -43,7 +43,7 @@ class GbdtConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("comm", ctypes.c_void_p),
         ("grad_bits", ctypes.c_int32),  # 17 (packed u64 LDS cells) or 25 (wide int64 cells)
-        ("packed", ctypes.c_int32),     # 1: packed 16-byte row records (set_pack)
+        ("reserved0", ctypes.c_int32),
     ]
 
 
@@ -94,50 +94,6 @@ def bin_matrix(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> tupl
     return bins, binsT
 
 
-def packed_records_on() -> bool:
-    """Packed 16-byte row records (csrc/gbdt.hip pk_code) where the layout fits: the default;
-    COBALT_PACKED_RECORDS=0 keeps the 32-byte records (A/B)."""
-    return os.environ.get("COBALT_PACKED_RECORDS", "1") != "0"
-
-
-def pack_layout(nbins: torch.Tensor) -> np.ndarray | None:
-    """The packed-record code layout of features with these bin counts (cobalt_pack_layout: each code
-    ceil(log2(nbins + 1)) bits, first-fit into 91 bits, no code across a dword), int32 [F] = bit offset |
-    width << 8; None when the features do not fit (> 24 of them, or more than 91 bits)."""
-    fn = getattr(_native.lib(), "cobalt_pack_layout", None)
-    if fn is None:  # an older library (same-box A/B builds): 32-byte records
-        return None
-    nb = np.ascontiguousarray(nbins.detach().to("cpu", torch.int32).numpy())
-    F = int(nb.shape[0])
-    out = np.zeros(max(F, 1), dtype=np.int32)
-    ok = fn(nb.ctypes.data, F, out.ctypes.data)
-    return out[:F] if ok else None
-
-
-def bin_matrix_packed(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor):
-    """Quantise ``X`` [N, F] float32 (CUDA) into packed 16-byte row records [N, 16] + binsT [F, N]:
-    ``(records, binsT, layout)``, or None when the packed form does not apply (layout does not fit,
-    F % 4 != 0, unaligned rows, COBALT_PACKED_RECORDS=0) -- the caller then uses :func:`bin_matrix`."""
-    if X.device.type != "cuda" or not packed_records_on():
-        return None
-    X = X.contiguous()
-    N, F = X.shape
-    if F % 4 != 0 or F > 24 or X.data_ptr() % 16 != 0:
-        return None
-    lay = pack_layout(nbins)
-    if lay is None:
-        return None
-    dev = X.device
-    rec = torch.empty((N, 16), dtype=torch.uint8, device=dev)
-    binsT = torch.empty((F, N), dtype=torch.uint8, device=dev)
-    lay_d = torch.from_numpy(lay).to(dev)
-    rc = _native.lib().cobalt_bin_matrix_pk(X.data_ptr(), N, F, cuts.contiguous().data_ptr(),
-                                            nbins.to(torch.int32).contiguous().data_ptr(), lay_d.data_ptr(),
-                                            rec.data_ptr(), binsT.data_ptr(), N, _native.stream_handle())
-    _native.check(rc, "cobalt_bin_matrix_pk")
-    return rec, binsT, lay
-
-
 def bin_matrix_into(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor, records: torch.Tensor,
                     binsT: torch.Tensor, row0: int) -> None:
     """Quantise the chunk ``X`` [n, F] (CUDA) in place into rows ``row0 .. row0+n`` of preallocated
@@ -186,13 +142,13 @@ class GpuGbdtTrainer:
                  reg_lambda: float, reg_alpha: float, gamma: float, min_child_weight: float, subsample: float,
                  gscale: float, hscale: float, base_margin: float, seed: int, row_offset: int = 0,
                  world_size: int = 1, comm: int | None = None, chunk: int | None = None,
-                 feat_tile: int | None = None, packed: bool = False, grad_bits: int = 17):
+                 feat_tile: int | None = None, grad_bits: int = 17):
         self.lib = _native.lib()
         cfg = GbdtConfig()
         cfg.n_rows = n_rows
         cfg.row_offset = row_offset
         cfg.n_feat = n_feat
-        cfg.row_stride = 16 if packed else row_stride(n_feat)  # 16: packed records (set_pack)
+        cfg.row_stride = row_stride(n_feat)
         cfg.max_depth = max_depth
         cfg.max_trees = max_trees
         cfg.chunk = chunk or pick_chunk(n_rows)
@@ -210,11 +166,9 @@ class GpuGbdtTrainer:
         cfg.seed = seed & ((1 << 64) - 1)
         cfg.comm = comm
         cfg.grad_bits = int(grad_bits)
-        cfg.packed = 1 if packed else 0
         self.cfg = cfg
         self._key = (torch.cuda.current_device(), cfg.n_rows, cfg.n_feat, cfg.row_stride, cfg.max_depth,
-                     cfg.max_trees, cfg.chunk, cfg.feat_tile, cfg.world_size, cfg.comm or 0, cfg.grad_bits,
-                     cfg.packed)
+                     cfg.max_trees, cfg.chunk, cfg.feat_tile, cfg.world_size, cfg.comm or 0, cfg.grad_bits)
         h = None
         if _cache_on():
             with _PARKED_LOCK:
@@ -245,14 +199,9 @@ class GpuGbdtTrainer:
         rc = self.lib.cobalt_gbdt_set_data(self.h, *[t.data_ptr() for t in ts])
         _native.check(rc, "cobalt_gbdt_set_data")
 
-    def set_pack(self, layout: np.ndarray) -> None:
-        """The packed-record code layout (:func:`pack_layout`) of a trainer created with ``packed``."""
-        lay = np.ascontiguousarray(layout, dtype=np.int32)
-        _native.check(self.lib.cobalt_gbdt_set_pack(self.h, lay.ctypes.data), "cobalt_gbdt_set_pack")
-
     def set_binary_labels(self, spw: float) -> bool:
         """After :meth:`set_data`: hold the 0/1 labels in the row records (byte 23 of a 32-byte record,
-        F <= 23; bit 27 of dword 2 of a packed record) and derive each row's weight from its label (``spw`` for positives, 1 otherwise), so
+        F <= 23) and derive each row's weight from its label (``spw`` for positives, 1 otherwise), so
         the gradient pass reads neither array. The caller guarantees binary labels and no sample
         weights. False (nothing changed) when the record layout has no room."""
         rc = self.lib.cobalt_gbdt_set_binary_labels(self.h, ctypes.c_float(spw), _native.stream_handle())
@@ -266,11 +215,12 @@ class GpuGbdtTrainer:
         fn = getattr(self.lib, "cobalt_gbdt_plan", None)
         if fn is None or not self.h:
             return {}
-        out = (ctypes.c_int32 * 5)()
+        out = (ctypes.c_int32 * 6)()
         fn(self.h, out)
-        return {"ipc_fused": bool(out[0]), "own_level": int(out[1]), "packed": bool(out[2]),
+        return {"ipc_fused": bool(out[0]), "own_level": int(out[1]), "wide_gradients": bool(out[2]),
                 "fused_eval_resident_blocks": int(out[3]),
-                "eval_part_levels": [lv for lv in range(16) if (out[4] >> lv) & 1]}
+                "eval_part_levels": [lv for lv in range(16) if (out[4] >> lv) & 1],
+                "eval_block_levels": [lv for lv in range(16) if (out[5] >> lv) & 1]}
 
     def replica_error(self) -> int:
         """Data-parallel replica check (csrc/gbdt.hip GbdtDev::dig): 0 = healthy, 2 = this rank's trees

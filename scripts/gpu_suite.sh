@@ -12,7 +12,8 @@
 #   prof       rocprofv3 kernel trace of one 10M fit -> per-kernel summary
 #   multirank  the driver's 2- and 4-rank bench commands rehearsed on one GPU
 #   dpdiag     N processes sharing the GPU through the IPC exchange (DP_SET: a configuration set of dp8_diag.py)
-# Environment passes through (e.g. COBALT_NATIVE_LIB=abref/libcobalt_hip_r4.so for a same-box A/B).
+# Environment passes through (e.g. COBALT_NATIVE_LIB=abref/libcobalt_hip_r4.so for a same-box A/B);
+# BENCH_ARGS: extra bench.py arguments of the bench / shards steps (e.g. --grad-bits 25).
 set -o pipefail
 S=scripts/gpu_step.sh
 mkdir -p gpurun_out
@@ -33,11 +34,11 @@ for step in "$@"; do
       bash $S ${tag}_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
       echo "$tag smoke: $(grep -c 'smoke ok' gpurun_out/${tag}_smoke.log)" >> $OUT ;;
     bench)
-      bash $S ${tag}_bench 300 python bench.py --steps 5 --warmup 2 || exit $?
+      bash $S ${tag}_bench 300 python bench.py --steps 5 --warmup 2 $BENCH_ARGS || exit $?
       echo "$tag bench10M: $(ms gpurun_out/${tag}_bench.log) ms auc $(auc gpurun_out/${tag}_bench.log)" >> $OUT ;;
     shards)
       for r in ${SHARD_ROWS:-5000000 2500000 1250000 1000000}; do
-        bash $S ${tag}_shard_$r 300 python bench.py --rows $r --steps 5 --warmup 2 --test-rows 100000 || exit $?
+        bash $S ${tag}_shard_$r 300 python bench.py --rows $r --steps 5 --warmup 2 --test-rows 100000 $BENCH_ARGS || exit $?
         echo "$tag shard rows=$r: $(ms gpurun_out/${tag}_shard_$r.log) ms" >> $OUT
       done ;;
     dpprobe)

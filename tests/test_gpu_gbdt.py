@@ -50,60 +50,8 @@ def test_bin_matrix_other_widths_match_host(F):
     assert np.array_equal(binsT.cpu().numpy(), ref.T)
 
 
-def _unpack_records(rec: torch.Tensor, lay, nb) -> np.ndarray:
-    """Host decoder of packed 16-byte records (csrc/gbdt.hip pk_code): uint8 bins with missing = 255."""
-    words = rec.cpu().contiguous().view(torch.int32).numpy().view(np.uint32)
-    out = np.zeros((words.shape[0], len(lay)), dtype=np.uint8)
-    for f, p in enumerate(lay):
-        off, w = int(p) & 127, int(p) >> 8
-        code = (words[:, off >> 5] >> np.uint32(off & 31)) & np.uint32((1 << w) - 1)
-        miss = (code == (1 << w) - 1) & (int(nb[f]) < 256)
-        out[:, f] = np.where(miss, 255, code).astype(np.uint8)
-    return out
-
-
-@pytest.mark.parametrize("F", [8, 20, 24])
-def test_bin_matrix_packed_matches_host(F):
-    """Packed 16-byte records (k_bin_pk): every code decodes to the host bin, NaN to the missing code;
-    the pair / label bits start at zero; binsT as the 32-byte binning writes it."""
-    from cobalt_smart_lender_ai_amd.ops import gbdt_ops
-
-    X, _ = _data(30_011, seed=F)
-    X = X[:, :F].contiguous() if F <= X.shape[1] else torch.cat([X, X[:, : F - X.shape[1]] * 1.5], 1).contiguous()
-    if F == 24:  # 24 codes fit the 91 bits only at <= 3 bits each: low-cardinality columns (NaNs kept)
-        X = torch.clamp(torch.floor(X * 1.5), -3, 2)
-    cuts, nb = sketch.compute_cuts(X, 256)
-    got = gbdt_ops.bin_matrix_packed(X.cuda(), cuts.cuda(), nb.cuda())
-    assert got is not None, "the layout fits these features"
-    rec, binsT, lay = got
-    ref = sketch.bin_matrix_host(X.numpy(), cuts.numpy(), nb.numpy())
-    assert np.array_equal(_unpack_records(rec, lay, nb.numpy()), ref)
-    assert np.array_equal(binsT.cpu().numpy(), ref.T)
-    words = rec.cpu().contiguous().view(torch.int32).numpy().view(np.uint32)
-    assert not (words[:, 3].any() or (words[:, 2] >> np.uint32(27)).any())
-
-
-@pytest.mark.parametrize("env", [{}, {"COBALT_LABEL_IN_RECORD": "0"}])
-def test_gpu_packed_records_fit_equals_32byte_fit_and_oracle(env, monkeypatch):
-    """The packed-record trainer (16-byte records: root pass, tree walk, histogram gathers) grows the
-    32-byte trainer's and the NumPy oracle's trees byte for byte, with row and column sampling, with the
-    labels in the records and without."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    X, y = _data(120_000, seed=12)
-    p = gbdt.GBDTParams(n_estimators=5, max_depth=7, learning_rate=0.2, gamma=0.5, subsample=0.8,
-                        colsample_bytree=0.7, scale_pos_weight=6.7, random_state=9)
-    bd = gbdt.bin_dataset(X.cuda(), max_bin=256, device="cuda")
-    assert bd.pack is not None and bd.records.shape[1] == 16
-    packed = gbdt.train(X.cuda(), y.cuda(), p, device="cuda").save_raw("ubj")
-    monkeypatch.setenv("COBALT_PACKED_RECORDS", "0")
-    wide = gbdt.train(X.cuda(), y.cuda(), p, device="cuda").save_raw("ubj")
-    assert packed == wide
-    assert packed == gbdt.train(X, y, p, device="cpu").save_raw("ubj")
-
-
 def test_gpu_wide_gradients_equal_oracle():
-    """grad_bits=25 (int64 LDS cells, 32-byte records even where the packed form fits): the GPU trees
+    """grad_bits=25 (int64 LDS cells): the GPU trees
     equal the NumPy oracle's at 25 bits byte for byte, with row and column sampling; a 17-bit fit of
     the same data grows different trees (the precision is really used)."""
     X, y = _data(120_000, seed=13)
