@@ -84,6 +84,7 @@ _SIGS: dict[str, tuple] = {
     "cobalt_ipc_epoch": (ctypes.c_uint, [c_void_p]),
     "cobalt_ipc_set_timeout": (ctypes.c_int, [c_void_p, ctypes.c_double]),
     "cobalt_ipc_dtab_selftest": (c_int, [c_void_p, ctypes.c_uint, c_void_p]),
+    "cobalt_hw_ids": (c_int, [c_void_p, c_int, c_void_p]),
     # loopcomm.hip
     "cobalt_comm_loop_group": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "cobalt_comm_loop_rank": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),

@@ -157,7 +157,7 @@ KNOBS: dict[str, Knob] = {
     # -- data parallelism --
     "COBALT_IPC_FUSED": Knob("1", "native", "IPC exchange fused into the split evaluation (0: separate exchange kernel + fused eval/partition)"),
     "COBALT_DP_OWNER": Knob("1", "native", "node ownership on the three deepest levels over the fused IPC exchange"),
-    "COBALT_EVAL_BLOCKS": Knob("1", "native", "fused evaluation + partition with one evaluator block per node where the items exceed the CUs, and over the fused IPC exchange (0 off)"),
+    "COBALT_EVAL_BLOCKS": Knob("1", "native", "over the fused IPC exchange: the fused evaluation + partition pass with one evaluator block per node (0: k_eval + k_partition)"),
     "COBALT_CU_BUDGET": Knob("", "native", "CUs of this rank's CU-masked stream (set by parallel/cumask.py)"),
     "COBALT_DP_TRANSPORT": Knob("auto", "python", "native communicator: auto (IPC within a node), ipc or rccl"),
     "COBALT_DIST_BACKEND": Knob("auto", "python", "torch.distributed backend override (gloo for ranks sharing one GPU)"),
@@ -168,6 +168,7 @@ KNOBS: dict[str, Knob] = {
     "COBALT_COLLECTIVE_TIMEOUT_S": Knob("1800", "python", "host watchdog deadline for one enqueued segment of trees"),
     "COBALT_SHARED_CU_MASK": Knob("auto", "python", "CU-masked streams for ranks sharing one GPU (default up to 5 ranks)"),
     "COBALT_CU_MASK_LAYOUT": Knob("interleaved", "python", "CU masks of ranks sharing one GPU: interleaved (CU rank + k world) or blocked"),
+    "COBALT_TEST_PLACEMENT": Knob("0", "test", "parallel/dp_check.py: record the XCCs / CUs a rank's masked stream runs on"),
     "COBALT_BENCH_SHARED_DEVICE": Knob("0", "python", "bench.py: every rank on cuda:0 (the 1-GPU multi-rank rehearsal)"),
     # -- trainer / serving (python) --
     "COBALT_LABEL_IN_RECORD": Knob("1", "python", "0/1 labels ride in the row records' padding (weights derived from them)"),

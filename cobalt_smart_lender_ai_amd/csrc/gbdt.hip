@@ -1665,11 +1665,16 @@ __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pa
   const char* sp[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r) sp[r] = iv->slot[r] + pair_bytes;
+  const int me = __builtin_amdgcn_readfirstlane(iv->me);
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
     const int cell = i < mt ? cb + i : ncells + (i - mt);
     longlong2 t[NR];
+    // (this rank's own slot: plain 16-byte loads -- an earlier kernel of this device wrote it)
 #pragma unroll
-    for (int r = 0; r < NR; ++r) t[r] = ipc_load_cell(sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2));
+    for (int r = 0; r < NR; ++r) {
+      const char* p = sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2);
+      t[r] = r == me ? *reinterpret_cast<const longlong2*>(p) : ipc_load_cell(p);
+    }
     longlong2 acc = t[0];
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
@@ -2293,20 +2298,22 @@ __device__ __forceinline__ uint64_t decision_word(uint32_t tag, bool ok, bool fa
 //   kMode 0: one GPU. 1: data parallel with the level's global histograms already in hist_b (RCCL / the
 //   separate IPC exchange kernel); every active node gets an item (possibly empty), so each rank
 //   finalises every node of the level, also those it holds no rows of.
-// EVALUATOR blocks: blocks 0 .. 2^level - 1 evaluate one node position each, exactly as k_eval does,
-// finalise it and publish its decision granule; the blocks after them are the partition items, which
-// plan and load their row ids while the evaluation runs and then poll their node's granule (one lane,
-// bounded). One evaluation per node and no k_eval -> k_partition boundary, at any item count:
-//   kMode 2: data parallel over the fused IPC exchange (k_eval<false, true, true>: block 0 publishes the
-//   epoch, every evaluator sums its node's cells over the ranks; node ownership on the deep levels; the
-//   replica digest); 3: one GPU, the level's items exceed the CUs; 4: data parallel over hist_b, ditto.
-// Forward progress does not need the grid resident: blocks are dispatched in index order on every XCD,
-// so the evaluators hold CUs before any item does, and no evaluator waits on an item.
+// kMode 2, EVALUATOR blocks (data parallel over the fused IPC exchange): blocks 0 .. 2^level - 1
+// evaluate one node position each, exactly as k_eval<false, true, true> does (block 0 publishes the
+// epoch, every evaluator sums its node's cells over the ranks; node ownership on the deep levels; the
+// replica digest), publish its decision granule and finalise it; the blocks after them are the
+// partition items, which plan and load their row ids while the evaluation runs and then poll their
+// node's granule (one lane, bounded by the group's deadline). One evaluation per node -- no xGMI
+// traffic multiplied by the items -- and no k_eval -> k_partition boundary, at any item count: blocks
+// are dispatched in index order on every XCD, so the evaluators hold CUs before any item does, and no
+// evaluator waits on an item. (The same form for one GPU beyond one block per CU measured slower than
+// k_eval + k_partition -- 10M rows 238.6 vs 231.9 ms: the fused kernel's 110 VGPRs hold the partition
+// to one block per CU; profiles/round5/eval_blocks_10M.txt.)
 template <int kSteps, int kMode>
 __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64_t zero_next, int level, int chunk,
                                                     int tree, EvalSlots es, uint32_t tag) {
-  constexpr bool kDP = kMode == 1 || kMode == 2 || kMode == 4;
-  constexpr bool kEvalBlocks = kMode >= 2;
+  constexpr bool kDP = kMode != 0;
+  constexpr bool kEvalBlocks = kMode == 2;
   constexpr bool kIpc = kMode == 2;
   constexpr int kPW = 16;  // waves
   BlockStamp stamp_(d);
@@ -2322,20 +2329,6 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
       zp[e] = make_int4(0, 0, 0, 0);
   const int nlev = 1 << level;
   const int first = nlev - 1;
-  if (kEvalBlocks && !kIpc && (int)blockIdx.x < nlev) {  // the evaluator of node first + blockIdx.x
-    const int pos = blockIdx.x, n = first + pos;
-    const bool good = eval_core<false, false, kDP>(d, level, parity, tree, d.F, es, pos, stamp_, &s_out);
-    if (threadIdx.x == 0 && good) {  // (an inactive node has no partition items)
-      int f = 0, j = -1;
-      bool dl = false;
-      const bool ok = split_decision(d, s_out.best, s_out.nb, f, j, dl);
-      eval_finalize<kDP>(d, level, n, s_out.G, s_out.H, s_out.best, s_out.cut, s_out.nb);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(d.dec) + n,
-                         (unsigned long long)decision_word(tag, ok, false, f, j, dl), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
   if (kIpc && (int)blockIdx.x < nlev) {  // the evaluator of node first + blockIdx.x
     const int pos = blockIdx.x, n = first + pos;
     const IpcFusedView* iv = d.ipcv + (d.ipc_epoch & 1u);
@@ -2344,13 +2337,15 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
     const bool good = eval_core<false, true, true>(d, level, parity, tree, d.F, es, pos, stamp_, &s_out);
     if (threadIdx.x == 0) {
       uint64_t w = 0;
-      if (good) {
+      if (good) {  // the decision first (the items wait on it; they need nothing else of the finalisation)
         int f = 0, j = -1;
         bool dl = false;
         const bool ok = split_decision(d, s_out.best, s_out.nb, f, j, dl);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(d.dec) + n,
+                           (unsigned long long)decision_word(tag, ok, false, f, j, dl), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
         eval_finalize<true>(d, level, n, s_out.G, s_out.H, s_out.best, s_out.cut, s_out.nb);
         if (owned) own_publish(d, iv, n);
-        w = decision_word(tag, ok, false, f, j, dl);
       } else {
         const Node nd = d.nodes[n];  // a non-owner's copy of the owner's record (own_copy), or inactive
         if (owned && mine && nd.status != kActive) own_publish(d, iv, n);  // (as k_eval: a diverged peer learns)
@@ -2933,9 +2928,7 @@ static void launch_eval_part(int steps, int mode, dim3 grid, size_t lds, hipStre
     switch (mode) {
       case 0: EP_LAUNCH(4, 0); break;
       case 1: EP_LAUNCH(4, 1); break;
-      case 2: EP_LAUNCH(4, 2); break;
-      case 3: EP_LAUNCH(4, 3); break;
-      default: EP_LAUNCH(4, 4); break;
+      default: EP_LAUNCH(4, 2); break;
     }
   } else if (steps <= 6 && mode <= 1) {  // (1.25M rows: 6144-row items; the 8-step form spills 2 VGPRs)
     if (mode == 0) EP_LAUNCH(6, 0); else EP_LAUNCH(6, 1);
@@ -2943,9 +2936,7 @@ static void launch_eval_part(int steps, int mode, dim3 grid, size_t lds, hipStre
     switch (mode) {
       case 0: EP_LAUNCH(8, 0); break;
       case 1: EP_LAUNCH(8, 1); break;
-      case 2: EP_LAUNCH(8, 2); break;
-      case 3: EP_LAUNCH(8, 3); break;
-      default: EP_LAUNCH(8, 4); break;
+      default: EP_LAUNCH(8, 2); break;
     }
   }
 #undef EP_LAUNCH
@@ -3021,9 +3012,11 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   //  * While a level's items fit one 1024-thread block per CU, every partition block evaluates its node
   //    itself (modes 0 / 1; 1M rows: 248.0 -> 239.3 us per tree in the stamps). Under data parallelism
   //    that needs the level's global histograms in hist_b first (RCCL, or the separate IPC exchange).
-  //  * Beyond that (a second evaluation per CU cost more than it saved: 1.25M 87.0 -> 96.3 ms per fit in
-  //    round 3), and always over the fused IPC exchange, the evaluator-block form (modes 3 / 4 / 2): one
-  //    evaluating block per node, the items wait for their node's decision granule.
+  //  * Beyond that k_eval + k_partition (a second evaluation per CU cost more than it saved: 1.25M
+  //    87.0 -> 96.3 ms per fit in round 3; the evaluator-block form below, 10M 238.6 vs 231.9 ms).
+  //  * Over the fused IPC exchange, at every level: the evaluator-block form (mode 2): one evaluating
+  //    block per node, the items wait for their node's decision granule (1.25M through a 1-rank IPC
+  //    group: 86.3 vs 89.0 ms with k_eval + k_partition).
   // COBALT_EVAL_PART=0 disables both (k_eval + k_partition), 2 forces the every-block form on one GPU;
   // COBALT_EVAL_BLOCKS=0 disables the evaluator-block form.
   static const int env_ep = knob_int(Knob::EvalPart, 1);
@@ -3063,9 +3056,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
         return ch;
       }
     if (ipc_fused) { mode = 2; return chunk_part(d); }
-    if (env_ep == 2 && !dp) return 8192;
-    if (eb_ok) { mode = dp ? 4 : 3; return chunk_part(d); }
-    return 0;
+    return (env_ep == 2 && !dp) ? 8192 : 0;
   };
   c->plan[0] = ipc_fused ? 1 : 0;
   c->plan[1] = d.own_level;

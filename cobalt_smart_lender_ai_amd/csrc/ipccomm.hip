@@ -363,3 +363,26 @@ COBALT_API unsigned cobalt_ipc_epoch(void* comm) {
   CobaltComm* c = static_cast<CobaltComm*>(comm);
   return (c && c->kind == 2) ? c->ipc->epoch : 0u;
 }
+
+// ------------------------------------------------------------------------------------------
+// Placement probe for ranks sharing one device through CU-masked streams (parallel/cumask.py):
+// thread 0 of each block records where the block ran -- the XCC (HW_REG_XCC_ID) and the shader
+// engine / array / CU fields of HW_REG_HW_ID -- as xcc << 16 | se << 8 | sh << 4 | cu. A stream whose
+// mask leaves an XCC without CUs can never run that XCC's share of a grid (every XCC takes blocks
+// round-robin), which is what the probe exposes on the configurations that complete.
+namespace {
+__global__ __launch_bounds__(64) void k_hw_ids(uint32_t* out) {
+  if (threadIdx.x != 0) return;
+  uint32_t xcc, hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  const uint32_t cu = (hw >> 8) & 0xFu, sh = (hw >> 12) & 0x1u, se = (hw >> 13) & 0x7u;
+  out[blockIdx.x] = (xcc & 0xFu) << 16 | se << 8 | sh << 4 | cu;
+}
+}  // namespace
+
+COBALT_API int cobalt_hw_ids(hipStream_t stream, int blocks, uint32_t* out) {
+  if (blocks <= 0 || !out) return -3;
+  hipLaunchKernelGGL(k_hw_ids, dim3(blocks), dim3(64), 0, stream, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

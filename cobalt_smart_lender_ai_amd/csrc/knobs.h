@@ -24,7 +24,7 @@ enum class Knob : int {
   CuBudget,      // COBALT_CU_BUDGET: CUs of this rank's CU-masked stream (parallel/cumask.py sets it)
   BinScalar,     // COBALT_BIN_SCALAR: the generic binning kernel for 32-byte records too (tests)
   PredWalk,      // COBALT_PRED_WALK: trees walked at once per predictor thread (2 / 4 / 8)
-  EvalBlocks,    // COBALT_EVAL_BLOCKS: the evaluator-block form of the fused evaluation + partition pass
+  EvalBlocks,    // COBALT_EVAL_BLOCKS: the evaluator-block fused pass over the fused IPC exchange
   Count
 };
 

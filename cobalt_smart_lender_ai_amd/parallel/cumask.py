@@ -75,6 +75,22 @@ def shared_device_stream(rank: int, world: int, device: torch.device) -> torch.c
     return torch.cuda.ExternalStream(h.value, device=device)
 
 
+def placement(stream: torch.cuda.ExternalStream | None, device: torch.device, blocks: int = 1024) -> dict:
+    """Where a grid launched on ``stream`` runs (csrc/ipccomm.hip ``cobalt_hw_ids``): the XCCs and the
+    number of distinct CUs its blocks landed on. Only call on a mask that covers every XCC (a mask that
+    leaves one out never finishes the launch)."""
+    from .. import _native
+
+    out = torch.zeros(blocks, dtype=torch.int32, device=device)
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    rc = _native.lib().cobalt_hw_ids(ctypes.c_void_p(s.cuda_stream), blocks, ctypes.c_void_p(out.data_ptr()))
+    if rc != 0:
+        raise RuntimeError(f"cobalt_hw_ids failed ({rc})")
+    s.synchronize()
+    ids = out.cpu().numpy().astype("int64")
+    return {"xccs": sorted({int(v >> 16) for v in ids}), "cus": len({int(v) for v in ids})}
+
+
 MAX_MASKED_RANKS = 5
 
 

@@ -62,6 +62,8 @@ def rank_main(rank: int, world: int, port: int, out_dir: str, rows: int, params:
             # ranks sharing the device each get their own 1/world of the CUs (see parallel/cumask.py)
             stream = cumask.shared_device_stream(rank, world, dev)
             res["cu_budget"] = int(os.environ["COBALT_CU_BUDGET"])
+            if os.environ.get("COBALT_TEST_PLACEMENT") == "1":
+                res["placement"] = cumask.placement(stream, dev)
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             if world > 1:
                 backend = "nccl" if (one_gpu_per_rank and transport == "rccl") else "gloo"

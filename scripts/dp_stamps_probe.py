@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """In-kernel stamps (COBALT_STAMPS) of one 1.25M-row fit per data-parallel protocol variant on ONE GPU,
-1-rank groups: single GPU / IPC fused k_eval + k_partition / IPC lead-decides k_eval_part
-(COBALT_DP_EVAL_PART=1) / RCCL (k_eval_part mode 1). Writes gpurun_out/dpst_<name>.txt (raw stamps,
-summarised by scripts/stamp_summary.py)."""
+1-rank groups: single GPU / IPC fused exchange (k_eval_part's evaluator blocks; with COBALT_EVAL_BLOCKS=0
+k_eval + k_partition) / RCCL (k_eval_part mode 1). The caller sets COBALT_STAMPS (raw stamps, summarised
+by scripts/stamp_summary.py). usage: dp_stamps_probe.py ROWS single|ipc|rccl"""
 import ctypes
 import os
 import sys
@@ -30,10 +30,10 @@ assert lib.cobalt_comm_init(uid, 1, 0, ctypes.byref(h)) == 0
 rccl = DistContext(rank=0, world=1, local_rank=0, backend="none", native_comm=h.value, transport="rccl")
 ipc = DistContext(rank=0, world=1, local_rank=0, backend="none", transport="ipc")
 ipc.native_comm = create_ipc_comm(ipc)
-# COBALT_STAMPS / COBALT_DP_EVAL_PART are read when a trainer context is created / per process: one
+# COBALT_STAMPS / COBALT_EVAL_BLOCKS are read when a trainer context is created / per process: one
 # variant per process invocation (argv[2])
 name = sys.argv[2]
-kw = {"single": {}, "ipc": {"dist": ipc}, "ipc_ep": {"dist": ipc}, "rccl": {"dist": rccl}}[name]
+kw = {"single": {}, "ipc": {"dist": ipc}, "rccl": {"dist": rccl}}[name]
 gbdt.train(X, y, p, device=dev, **kw)
 torch.cuda.synchronize()
 print(f"{name} done", flush=True)

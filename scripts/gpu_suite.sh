@@ -8,10 +8,12 @@
 #   bench      bench.py (10M rows, 5 timed fits)
 #   shards     single-GPU fits at the strong-scaling shard sizes (5M / 2.5M / 1.25M / 1M rows)
 #   dpprobe    data-parallel protocol cost at the 1.25M shard with 1-rank RCCL / IPC groups
+#   dpstamps   in-kernel stamps of the 1.25M shard: single GPU / 1-rank IPC / 1-rank RCCL
 #   stamps     in-kernel stamps at 1M and 10M rows (STAMP_ROWS overrides)
 #   prof       rocprofv3 kernel trace of one 10M fit -> per-kernel summary
 #   multirank  the driver's 2- and 4-rank bench commands rehearsed on one GPU
 #   dpdiag     N processes sharing the GPU through the IPC exchange (DP_SET: a configuration set of dp8_diag.py)
+#   qdiag      N CU-masked rank processes: outcome, KFD queues, where each rank's blocks run (dp_queue_diag.py)
 # Environment passes through (e.g. COBALT_NATIVE_LIB=abref/libcobalt_hip_r4.so for a same-box A/B);
 # BENCH_ARGS: extra bench.py arguments of the bench / shards steps (e.g. --grad-bits 25).
 set -o pipefail
@@ -44,6 +46,15 @@ for step in "$@"; do
     dpprobe)
       bash $S ${tag}_dpprobe 400 python -u scripts/dp_overhead_probe.py --rows ${DP_ROWS:-1250000} || exit $?
       echo "$tag dpprobe: $(grep '^{' gpurun_out/${tag}_dpprobe.log | tail -1)" >> $OUT ;;
+    dpstamps)
+      for v in ${DPST_VARIANTS:-single ipc rccl}; do
+        rm -f gpurun_out/dpst_raw.txt
+        COBALT_STAMPS=gpurun_out/dpst_raw.txt bash $S ${tag}_dpst_$v 200 python -u scripts/dp_stamps_probe.py \
+          ${DP_ROWS:-1250000} $v || exit $?
+        python scripts/stamp_summary.py gpurun_out/dpst_raw.txt > gpurun_out/${tag}_dpst_$v.txt || exit $?
+        rm -f gpurun_out/dpst_raw.txt
+        echo "$tag dpstamps $v: $(grep 'per tree' gpurun_out/${tag}_dpst_$v.txt)" >> $OUT
+      done ;;
     stamps)
       for rows in ${STAMP_ROWS:-1000000 10000000}; do
         rm -f gpurun_out/stamps_raw_$rows.txt
@@ -64,6 +75,9 @@ for step in "$@"; do
     dpdiag)
       bash $S ${tag}_dpdiag 900 python -u scripts/dp8_diag.py ${DP_SET:-width} || exit $?
       echo "$tag dpdiag: $(tail -3 gpurun_out/${tag}_dpdiag.log)" >> $OUT ;;
+    qdiag)
+      bash $S ${tag}_qdiag 900 python -u scripts/dp_queue_diag.py $QDIAG_CFGS || exit $?
+      echo "$tag qdiag: see ${tag}_qdiag.log" >> $OUT ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
