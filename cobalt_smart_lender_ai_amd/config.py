@@ -166,8 +166,8 @@ KNOBS: dict[str, Knob] = {
     "COBALT_IPC_TIMEOUT_S": Knob("120", "python", "in-kernel exchange deadline before the group fails on every rank"),
     "COBALT_IPC_CONNECT_TIMEOUT_S": Knob("30", "python", "deadline of the IPC connect self-test"),
     "COBALT_COLLECTIVE_TIMEOUT_S": Knob("1800", "python", "host watchdog deadline for one enqueued segment of trees"),
-    "COBALT_SHARED_CU_MASK": Knob("auto", "python", "CU-masked streams for ranks sharing one GPU (default up to 5 ranks)"),
-    "COBALT_CU_MASK_LAYOUT": Knob("interleaved", "python", "CU masks of ranks sharing one GPU: interleaved (CU rank + k world) or blocked"),
+    "COBALT_SHARED_CU_MASK": Knob("auto", "python", "CU-masked streams for ranks sharing one GPU (default for 2-8 ranks)"),
+    "COBALT_CU_MASK_LAYOUT": Knob("blocked", "python", "CU masks of ranks sharing one GPU: blocked (contiguous bits, every XCC covered) or interleaved"),
     "COBALT_TEST_PLACEMENT": Knob("0", "test", "parallel/dp_check.py: record the XCCs / CUs a rank's masked stream runs on"),
     "COBALT_BENCH_SHARED_DEVICE": Knob("0", "python", "bench.py: every rank on cuda:0 (the 1-GPU multi-rank rehearsal)"),
     # -- trainer / serving (python) --

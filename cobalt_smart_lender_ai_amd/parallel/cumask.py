@@ -3,22 +3,22 @@ parallelism).
 
 On an 8-GPU node every rank owns a whole device. When N rank processes share one device instead,
 their kernels compete for the same compute units, and the data-parallel exchange waits inside
-kernels (the fused IPC exchange of ``csrc/gbdt.hip``): with 8 ranks the blocks of 7 ranks that are
-already waiting can occupy every CU while the 8th rank's publishing block never gets one -- observed
-as a 120 s group deadline at 8 processes (round 4), while 2-4 processes ran. A GPU does not preempt a
-running wave for another process's queue, so the fix is the hardware's own partitioning: each rank
-launches on a stream whose CU mask (``hipExtStreamCreateWithCUMask``) holds a disjoint 1/N of the
-CUs, like a small GPU of its own. The mask interleaves the ranks (CU ``rank + k * N``), so every rank
-has CUs in every XCD whichever way the runtime maps mask bits onto the XCDs. ``COBALT_CU_BUDGET``
-tells the trainer's launch heuristics how many CUs it has (e.g. the fused evaluation + partition
-pass only runs while its whole grid is resident).
+kernels (the fused IPC exchange of ``csrc/gbdt.hip``): unpartitioned, the GPU time-slices the
+processes' queues (8 ranks: 12.6 s for one tree, round 4). A GPU does not preempt a running wave for
+another process's queue, so the fix is the hardware's own partitioning: each rank launches on a
+stream whose CU mask (``hipExtStreamCreateWithCUMask``) holds a disjoint 1/N of the CUs, like a
+small GPU of its own. ``COBALT_CU_BUDGET`` tells the trainer's launch heuristics how many CUs it has.
 
-Measured on one MI355X (scripts/dp8_diag.py, profiles/round4/dp_shared_gpu.txt): with masks, 2-5
-processes run at full speed (5 ranks: 0.14 s per 1-tree fit, the 1-process model); from 6 processes
-on, the masked fits deadlock at the in-kernel exchange (every rank times out). Unmasked, 6 and 8
-processes are time-sliced by the GPU's queue scheduler -- slow (8 ranks: 12.6 s for one tree) but
-every rank finishes with the 1-process model, byte for byte. So the masks are the default only up
-to 5 ranks per device. None of this applies to the production layout (one process per GPU).
+The mask must give the rank CUs in EVERY XCC: a dispatch hands each of the 8 XCCs its round-robin
+share of the grid, and the share of an XCC with no CU in the mask never runs. Measured on one MI355X
+(round 5, ``scripts/dp_queue_diag.py`` with the ``cobalt_hw_ids`` placement probe,
+``profiles/round5/qdiag_masks.txt``): the mask bits go to the XCCs round-robin (bit i -> XCC i mod 8),
+so the former default layout -- CU ``rank + k * N`` -- gave rank r of 6 only the XCCs of r's parity and
+every 6-rank fit deadlocked, while a BLOCKED layout -- a contiguous range of N-th of the bits, >= 8
+consecutive bits for any N <= 32 -- covers all 8 XCCs: 6 and 8 masked ranks run at full speed (8 ranks:
+32 CUs each, 4 per XCC, the 1-process model byte for byte). (With 2 and 4 ranks the interleaved masks
+were not applied at all -- the probe saw every rank's blocks on all 256 CUs -- so those runs had been
+time-sliced rather than partitioned.) The blocked layout is the default for 2-8 sharing ranks.
 """
 from __future__ import annotations
 
@@ -60,11 +60,12 @@ def blocked_mask(rank: int, world: int, n_cu: int) -> list[int]:
 
 def shared_device_stream(rank: int, world: int, device: torch.device) -> torch.cuda.ExternalStream:
     """A stream of ``device`` restricted to this rank's 1/world of the CUs; sets ``COBALT_CU_BUDGET``
-    (call before the first fit: the trainer reads it once). ``COBALT_CU_MASK_LAYOUT``: ``interleaved``
-    (default: CU rank + k * world) or ``blocked`` (a contiguous range; scripts/dp_queue_diag.py)."""
+    (call before the first fit: the trainer reads it once). ``COBALT_CU_MASK_LAYOUT``: ``blocked``
+    (default: a contiguous range of mask bits, every XCC covered) or ``interleaved`` (CU rank + k * world;
+    leaves XCCs empty when world and 8 share a factor -- scripts/dp_queue_diag.py)."""
     n_cu = torch.cuda.get_device_properties(device).multi_processor_count
-    layout = os.environ.get("COBALT_CU_MASK_LAYOUT", "interleaved")
-    words = blocked_mask(rank, world, n_cu) if layout == "blocked" else interleaved_mask(rank, world, n_cu)
+    layout = os.environ.get("COBALT_CU_MASK_LAYOUT", "blocked")
+    words = interleaved_mask(rank, world, n_cu) if layout == "interleaved" else blocked_mask(rank, world, n_cu)
     arr = (ctypes.c_uint32 * len(words))(*words)
     h = ctypes.c_void_p()
     with torch.cuda.device(device):
@@ -91,7 +92,7 @@ def placement(stream: torch.cuda.ExternalStream | None, device: torch.device, bl
     return {"xccs": sorted({int(v >> 16) for v in ids}), "cus": len({int(v) for v in ids})}
 
 
-MAX_MASKED_RANKS = 5
+MAX_MASKED_RANKS = 8
 
 
 def want_shared_mask(world: int) -> bool:

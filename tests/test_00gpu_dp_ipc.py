@@ -55,26 +55,32 @@ def test_ipc_data_parallel_processes_equal_single_process():
             assert g["ok"] and g["model_sha256"] == ref3["model_sha256"], (procs, g)
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.skipif(os.environ.get("COBALT_TEST_DP8") != "1", reason="opt-in (COBALT_TEST_DP8=1): time-sliced, "
-                    "12.6 s to several minutes per run on a shared GPU")
+@pytest.mark.timeout(300)
 def test_ipc_eight_ranks_share_one_gpu():
     """8 processes on one GPU -- the rank count of an 8-GPU node, so the fused exchange sums 8 ranks'
-    cells (ipc_sum_cells<8>). Unmasked (parallel/cumask.py: masks deadlock from 6 sharing ranks), the
-    GPU time-slices the ranks' queues: slow, one tree, but byte-identical to 1 process. Its recorded
-    runs: profiles/round4/dp_shared_gpu.txt (scripts/dp8_diag.py)."""
+    cells (ipc_sum_cells<8>) and node ownership deals the deep levels over 8 owners -- each on its own
+    CU-masked 1/8 of the device (parallel/cumask.py, blocked layout): every rank's blocks land in all 8
+    XCCs on exactly its 32 CUs (the placement probe), and every rank grows the 1-process model byte for
+    byte, in seconds (rounds 4-5 before the layout fix: a deadlock masked, 12.6 s per tree time-sliced)."""
+    import time
+
     from cobalt_smart_lender_ai_amd.parallel import dp_check
 
     _check_clean(torch.cuda.is_initialized())
-    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=1)
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=3)
     ref = dp_check.run(1, 240_000, params)[0]
     assert ref["ok"], ref
-    got = dp_check.run(8, 240_000, params, timeout_s=300, env={"COBALT_IPC_TIMEOUT_S": "200"})
+    t0 = time.monotonic()
+    got = dp_check.run(8, 240_000, params, timeout_s=120,
+                       env={"COBALT_IPC_TIMEOUT_S": "30", "COBALT_TEST_PLACEMENT": "1"})
+    wall = time.monotonic() - t0
     for g in got:
         assert g["ok"], g
-        assert g["transport"] == "ipc" and g.get("cu_budget") is None
-        assert g["ipc_epochs"] == 4 + 1 + 7 + 1  # (240k rows: the 2^18-row sample sketch, gathered over gloo)
+        assert g["transport"] == "ipc" and g["cu_budget"] == 32, g
+        assert g["placement"]["xccs"] == list(range(8)) and g["placement"]["cus"] == 32, g["placement"]
+        assert g["ipc_epochs"] == 4 + 1 + 7 * 3 + 1  # (240k rows: the 2^18-row sample sketch, gathered over gloo)
         assert g["model_sha256"] == ref["model_sha256"], g["rank"]
+    assert wall < 60, wall
 
 
 @pytest.mark.timeout(600)
