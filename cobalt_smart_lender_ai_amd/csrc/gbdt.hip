@@ -2336,7 +2336,6 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
     const bool mine = !owned || node_owner(d, level, n, iv->n) == iv->me;
     const bool good = eval_core<false, true, true>(d, level, parity, tree, d.F, es, pos, stamp_, &s_out);
     if (threadIdx.x == 0) {
-      uint64_t w = 0;
       if (good) {  // the decision first (the items wait on it; they need nothing else of the finalisation)
         int f = 0, j = -1;
         bool dl = false;
@@ -2351,13 +2350,15 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
         if (owned && mine && nd.status != kActive) own_publish(d, iv, n);  // (as k_eval: a diverged peer learns)
         const bool failed =
             __hip_atomic_load(iv->myflag + kIpcStickyWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        // (no node here and no failure: no partition block waits for it)
-        if (nd.status != kNone || failed)
-          w = decision_word(tag, nd.status == kSplit, failed || nd.status == kActive, nd.feat, nd.bin,
-                            nd.default_left != 0);
+        // Always published: a node that is inactive here has no items, but one this rank planned items
+        // for can come back inactive from its owner's record (a diverged replica) -- its items then
+        // route no rows (and the replica digest reports the divergence at the next tree) instead of
+        // waiting for a decision that never comes.
+        const uint64_t w = decision_word(tag, nd.status == kSplit, failed || nd.status == kActive, nd.feat, nd.bin,
+                                         nd.default_left != 0);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(d.dec) + n, (unsigned long long)w, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (w) __hip_atomic_store(reinterpret_cast<unsigned long long*>(d.dec) + n, (unsigned long long)w,
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // The next send slot (this epoch - 1's) is zeroed once every peer has published this epoch: a peer
     // then has finished reading its previous contents. The evaluators that exchanged waited for that in

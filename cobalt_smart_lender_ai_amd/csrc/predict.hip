@@ -363,53 +363,89 @@ __global__ void k_shap_table(const PathElem* __restrict__ elems, const int32_t* 
   }
 }
 
-// Row-parallel kernel (batches): block = (256 rows, chunk); the chunk's path elements live in LDS
-// and are read as broadcasts, every thread walks the chunk's paths in order for ITS row: k interval
-// tests -> pattern -> k table values added to its private LDS column.
-constexpr int kShapRowsF = 48;  // row-parallel kernel: [F][256] doubles of per-row accumulators
+// Row-parallel kernel (batches): block = (kShapRowsB rows, chunk of paths); every thread walks the
+// chunk's paths in order for ITS row: k interval tests -> pattern -> k table values added to its
+// private LDS column. A path's elements are the same for every lane, so they come by scalar loads
+// (SGPRs) -- no LDS staging of the chunk's elements (which held a block to one per CU: 90 KB of LDS
+// for 256 rows, one wave per SIMD) -- and the block is 128 rows: 30 KB of LDS, several blocks per CU.
+// Two paths per step: the second path's tests and table loads are issued before the first's adds.
+constexpr int kShapRowsF = 48;  // row-parallel kernel: [F][kShapRowsB] doubles of per-row accumulators
+constexpr int kShapRowsB = 128;
+constexpr int kMaxTabK = 10;
 
-__global__ __launch_bounds__(256) void k_treeshap_rows(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
-                                                       const PathElem* __restrict__ elems,
-                                                       const int32_t* __restrict__ path_ptr, int n_paths,
-                                                       const int64_t* __restrict__ tab_ptr,
-                                                       const double* __restrict__ table, int max_len, int nchunks,
-                                                       double* __restrict__ out) {
+__device__ __forceinline__ int shap_pattern(const PathElem* __restrict__ el, int k, const float* x, int* fe) {
+  int pat = 0;
+#pragma unroll
+  for (int l = 0; l < kMaxTabK; ++l) {
+    if (l < k) {
+      const PathElem e = el[l];
+      const float v = x[e.feat];
+      const bool one = (v != v) ? (e.nan_ok != 0) : (v >= e.lo && v < e.hi);
+      pat |= (int)one << l;
+      fe[l] = e.feat;
+    }
+  }
+  return pat;
+}
+
+__global__ __launch_bounds__(kShapRowsB) void k_treeshap_rows(const float* __restrict__ X, int64_t n, int F, int64_t ldx,
+                                                              const PathElem* __restrict__ elems,
+                                                              const int32_t* __restrict__ path_ptr, int n_paths,
+                                                              const int64_t* __restrict__ tab_ptr,
+                                                              const double* __restrict__ table, int nchunks,
+                                                              double* __restrict__ out) {
   extern __shared__ double s_dyn[];
-  const int B = blockDim.x, tid = threadIdx.x;
+  constexpr int B = kShapRowsB;
+  const int tid = threadIdx.x;
   double* s_phi = s_dyn;                                              // [F][B]
   float* s_x = reinterpret_cast<float*>(s_phi + (size_t)F * B);        // [B][F|1]
   const int xs = F | 1;
-  PathElem* s_el = reinterpret_cast<PathElem*>(s_x + (size_t)B * xs + ((B * xs) & 1));  // chunk elements
   const int c = blockIdx.y;
   const int p0 = c * kShapChunk, p1 = min(n_paths, p0 + kShapChunk);
-  const int ebase = path_ptr[p0], eend = path_ptr[p1];
-  for (int i = tid; i < eend - ebase; i += B) s_el[i] = elems[ebase + i];
   const int64_t row0 = (int64_t)blockIdx.x * B;
   const int nrows = (int)min((int64_t)B, n - row0);
-  for (int e = tid; e < nrows * F; e += B) {
+  for (int e = tid; e < B * F; e += B) {  // (rows past the batch: zeros, computed and not stored)
     const int r = e / F, f = e - r * F;
-    s_x[r * xs + f] = X[(row0 + r) * ldx + f];
+    s_x[r * xs + f] = r < nrows ? X[(row0 + r) * ldx + f] : 0.0f;
   }
   for (int f = 0; f < F; ++f) s_phi[f * B + tid] = 0.0;
   __syncthreads();
-  if (tid < nrows) {
-    const float* x = s_x + tid * xs;
-    for (int p = p0; p < p1; ++p) {
-      const int e0 = path_ptr[p] - ebase, k = path_ptr[p + 1] - path_ptr[p];
-      int pat = 0;
-      for (int l = 0; l < k; ++l) {
-        const PathElem e = s_el[e0 + l];
-        const float v = x[e.feat];
-        const bool one = (v != v) ? (e.nan_ok != 0) : (v >= e.lo && v < e.hi);
-        pat |= (int)one << l;
-      }
-      const double* t = table + tab_ptr[p] + (int64_t)pat * k;
-      for (int l = 0; l < k; ++l) s_phi[s_el[e0 + l].feat * B + tid] += t[l];
+  const float* x = s_x + tid * xs;
+  int p = p0;
+  for (; p + 1 < p1; p += 2) {
+    const int e0 = path_ptr[p], e1 = path_ptr[p + 1], e2 = path_ptr[p + 2];
+    const int ka = e1 - e0, kb = e2 - e1;
+    int fa[kMaxTabK], fb[kMaxTabK];
+    const int pa = shap_pattern(elems + e0, ka, x, fa);
+    const int pb = shap_pattern(elems + e1, kb, x, fb);
+    const double* ta = table + tab_ptr[p] + (int64_t)pa * ka;
+    const double* tb = table + tab_ptr[p + 1] + (int64_t)pb * kb;
+    double va[kMaxTabK], vb[kMaxTabK];
+#pragma unroll
+    for (int l = 0; l < kMaxTabK; ++l) {
+      if (l < ka) va[l] = ta[l];
+      if (l < kb) vb[l] = tb[l];
     }
+#pragma unroll
+    for (int l = 0; l < kMaxTabK; ++l)
+      if (l < ka) s_phi[fa[l] * B + tid] += va[l];
+#pragma unroll
+    for (int l = 0; l < kMaxTabK; ++l)
+      if (l < kb) s_phi[fb[l] * B + tid] += vb[l];
+  }
+  if (p < p1) {
+    const int e0 = path_ptr[p], k = path_ptr[p + 1] - e0;
+    int fa[kMaxTabK];
+    const int pa = shap_pattern(elems + e0, k, x, fa);
+    const double* ta = table + tab_ptr[p] + (int64_t)pa * k;
+#pragma unroll
+    for (int l = 0; l < kMaxTabK; ++l)
+      if (l < k) s_phi[fa[l] * B + tid] += ta[l];
+  }
+  if (tid < nrows) {
     const int64_t row = row0 + tid;
     for (int f = 0; f < F; ++f) out[(row * nchunks + c) * F + f] = s_phi[f * B + tid];
   }
-  (void)max_len;
 }
 
 __global__ void k_shap_reduce(const double* __restrict__ slab, int64_t n, int F, int nchunks,
@@ -439,9 +475,7 @@ static int shap_reduce_launch(const double* work, int64_t n, int F, int nchunks,
   return 0;
 }
 
-// Table size (doubles) for paths with unique-feature counts given by path_ptr diffs; -1 if some
-// path is longer than kMaxTabK (the direct kernel is used then).
-constexpr int kMaxTabK = 10;
+// Pattern tables exist for paths of <= kMaxTabK unique features (longer: the direct kernel).
 
 COBALT_API int cobalt_shap_table_build(const void* elems, const int32_t* path_ptr, const double* path_val, int n_paths,
                                        int max_len, const int64_t* tab_ptr, double* table, hipStream_t stream) {
@@ -465,14 +499,12 @@ COBALT_API int cobalt_treeshap_tab(const float* X, int64_t n, int F, int64_t ldx
   if (F > kShapRowsF || max_len > kMaxTabK) return -5;
   if (nchunks != cobalt_treeshap_chunks(n, F, n_paths)) return -8;
   if (nchunks > 1 && work == nullptr) return -7;
-  const int B = 256;
-  const size_t lds = (size_t)F * B * sizeof(double) + (size_t)B * (F | 1) * sizeof(float) + 8 +
-                     (size_t)kShapChunk * max_len * sizeof(PathElem);
-  if (lds > 160 * 1024) return -3;
+  const int B = kShapRowsB;
+  const size_t lds = (size_t)F * B * sizeof(double) + (size_t)B * (F | 1) * sizeof(float);
   if (lds > 64 * 1024) CK(hipFuncSetAttribute((const void*)k_treeshap_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_treeshap_rows, dim3((unsigned)ceil_div(n, (int64_t)B), (unsigned)nchunks), dim3(B), lds, stream,
-                     X, n, F, ldx, static_cast<const PathElem*>(elems), path_ptr, n_paths, tab_ptr, table, max_len,
-                     nchunks, nchunks > 1 ? work : phi);
+                     X, n, F, ldx, static_cast<const PathElem*>(elems), path_ptr, n_paths, tab_ptr, table, nchunks,
+                     nchunks > 1 ? work : phi);
   CK_LAUNCH();
   return nchunks > 1 ? shap_reduce_launch(work, n, F, nchunks, phi, stream) : 0;
 }

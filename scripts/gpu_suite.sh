@@ -13,6 +13,8 @@
 #   prof       rocprofv3 kernel trace of one 10M fit -> per-kernel summary
 #   multirank  the driver's 2- and 4-rank bench commands rehearsed on one GPU
 #   dpdiag     N processes sharing the GPU through the IPC exchange (DP_SET: a configuration set of dp8_diag.py)
+#   shap       TreeSHAP kernel timings per batch size (pattern-table and direct kernels)
+#   serve      scoring engine / bulk scoring benchmark (scripts/bench_serve.py)
 #   qdiag      N CU-masked rank processes: outcome, KFD queues, where each rank's blocks run (dp_queue_diag.py)
 # Environment passes through (e.g. COBALT_NATIVE_LIB=abref/libcobalt_hip_r4.so for a same-box A/B);
 # BENCH_ARGS: extra bench.py arguments of the bench / shards steps (e.g. --grad-bits 25).
@@ -29,7 +31,7 @@ for step in "$@"; do
       bash $S ${tag}_tests 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit $?
       echo "$tag tests: $(grep -E 'passed|failed' gpurun_out/${tag}_tests.log | tail -1)" >> $OUT ;;
     gbdt)
-      bash $S ${tag}_gbdt 600 python -u -m pytest tests/test_gpu_gbdt.py tests/test_00gpu_dp_ipc.py -m gpu -x -q \
+      bash $S ${tag}_gbdt 600 python -u -m pytest tests/test_00gpu_dp_ipc.py tests/test_gpu_gbdt.py -m gpu -x -q -rs \
         --timeout 200 --timeout-method thread || exit $?
       echo "$tag gbdt: $(grep -E 'passed|failed' gpurun_out/${tag}_gbdt.log | tail -1)" >> $OUT ;;
     smoke)
@@ -78,6 +80,12 @@ for step in "$@"; do
     qdiag)
       bash $S ${tag}_qdiag 900 python -u scripts/dp_queue_diag.py $QDIAG_CFGS || exit $?
       echo "$tag qdiag: see ${tag}_qdiag.log" >> $OUT ;;
+    shap)
+      bash $S ${tag}_shap 300 python -u scripts/shap_probe.py || exit $?
+      echo "$tag shap: $(grep -c kernel gpurun_out/${tag}_shap.log) timings" >> $OUT ;;
+    serve)
+      bash $S ${tag}_serve 600 python -u scripts/bench_serve.py || exit $?
+      echo "$tag serve: see ${tag}_serve.log" >> $OUT ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

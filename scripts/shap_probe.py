@@ -1,0 +1,57 @@
+#!/usr/bin/env python
+"""TreeSHAP kernel timings on the reference model (300 trees, depth 7, 20 features): the row-parallel
+pattern-table kernel (batches >= 256 rows) and the direct path-parallel EXTEND / UNWIND kernel, per
+batch size, device-resident rows. One JSON line per (kernel, batch).
+
+usage: shap_probe.py [batch ...]   (default 64 512 4096 65535)"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from cobalt_smart_lender_ai_amd.dataio import synth  # noqa: E402
+from cobalt_smart_lender_ai_amd.models.booster import load_pickle_bytes  # noqa: E402
+from cobalt_smart_lender_ai_amd.ops import predict_ops  # noqa: E402
+
+
+def main() -> None:
+    sizes = [int(a) for a in sys.argv[1:]] or [64, 512, 4096, 65535]
+    b = load_pickle_bytes((ROOT / "tests" / "fixtures" / "xgb_model_tree.pkl").read_bytes())[1]
+    dev = torch.device("cuda", 0)
+    F = b.num_feature
+    X, _ = synth.make_lendingclub(max(sizes), seed=5, device=dev)
+    X = X[:, :F].contiguous()
+    gf = predict_ops.gpu_forest(b, dev, None, with_shap=True)
+    info = {"paths": int(gf.n_paths), "max_len": int(gf.max_len),
+            "table_mb": None if gf.table is None else round(gf.table.numel() * 8 / 2**20, 1)}
+    print(json.dumps(info), flush=True)
+    for n in sizes:
+        Xn = X[:n].contiguous()
+        phi = torch.zeros((n, F), dtype=torch.float64, device=dev)
+        for kind in ("table", "direct"):
+            if kind == "table" and n < predict_ops.SHAP_ROWS_MIN:
+                continue
+            predict_ops._FORCE_DIRECT_SHAP = kind == "direct"
+            try:
+                predict_ops.treeshap_gpu(b, Xn, phi)
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(5 if n <= 4096 else 2):
+                    t = time.perf_counter()
+                    predict_ops.treeshap_gpu(b, Xn, phi)
+                    torch.cuda.synchronize()
+                    ts.append(time.perf_counter() - t)
+            finally:
+                predict_ops._FORCE_DIRECT_SHAP = False
+            ms = float(np.median(ts)) * 1e3
+            print(json.dumps({"kernel": kind, "rows": n, "ms": round(ms, 3), "rows_per_s": round(n / ms * 1e3)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -102,9 +102,12 @@ def test_full_data_sketch_across_processes_equals_single_process():
 @pytest.mark.timeout(600)
 def test_ipc_replica_divergence_fails_every_rank():
     """Fault injection: rank 1 grows a different tree 1 (its root totals perturbed after the exchange,
-    as a stale peer read would). The in-flight digest check (csrc/gbdt.hip GbdtDev::dig) sees it at
-    level 0 of tree 2, on EVERY rank, and each raises ReplicaDivergence after that tree's segment --
-    not a silently divergent model at the end of the fit."""
+    as a stale peer read would). The replica digest (csrc/gbdt.hip GbdtDev::dig) is compared in flight
+    at level 0 of the next tree and by the digest all-reduce that closes every grow call -- here (one
+    tree per checkpoint segment) right after tree 1 -- on EVERY rank, and each raises ReplicaDivergence
+    for that segment, not a silently divergent model at the end of the fit. (The diverged rank's
+    partition items get their node's decision from the owner's record even when the owner found the
+    node inactive, so no rank waits for a decision that never comes.)"""
     from cobalt_smart_lender_ai_amd.parallel import dp_check
 
     _check_clean(torch.cuda.is_initialized())
@@ -115,7 +118,7 @@ def test_ipc_replica_divergence_fails_every_rank():
         for g in got:
             assert not g["ok"], g
             assert g.get("error") == "ReplicaDivergence", g
-            assert "before tree 3" in g.get("message", ""), g  # detected within one tree
+            assert "before tree 2" in g.get("message", ""), g  # detected with the diverged tree itself
     # the same fit without the fault: the check stays quiet
     got = dp_check.run(2, 200_000, params, checkpoint_every=1, timeout_s=300)
     assert all(g["ok"] for g in got), got
