@@ -1091,8 +1091,9 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
 
 // U rows in flight per thread; 2 per CU of 512 threads at 95 VGPRs (no waves-per-EU bound: capping U = 2
 // at 80 VGPRs spills, 276.5 vs 269.7 ms per 10M fit)
+// (wide cells: 1024-thread blocks -- the 16-byte-cell tile holds a CU to one block, so twice the waves)
 template <int U, int FT4, bool kWide = false>
-__global__ __launch_bounds__(512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
+__global__ __launch_bounds__(kWide ? 1024 : 512) void k_grad_hist(GbdtDev d, int tree, int apply_tree, int chunk) {
   grad_hist_body<U, FT4, kWide>(d, tree, apply_tree, chunk);
 }
 
@@ -1182,14 +1183,15 @@ __device__ __forceinline__ void hist_rows_pair(const GbdtDev& d, uint64_t* s_his
 }
 
 constexpr int kHistThreads = 512;  // (1024-thread blocks measured 3-8% slower)
+constexpr int kHistThreadsWide = 1024;  // wide cells: one block per CU by LDS, so the larger block
 
 // FT4 > 0: 32-byte records with one tile of <= FT4 features (FT4 = F rounded up to 4); 0: generic rows.
 // (6 waves per SIMD = the 3 blocks per CU that the LDS tile allows: keeps the kernel within 80 VGPRs)
 // PAIR: the lane-pair record gathers of hist_rows_pair (FT4 >= 16).
 // kWide: wide gradients (16-byte LDS cells; the one-lane-per-row 32-byte path only).
-// (wide cells: one block per CU by LDS, 2 waves per SIMD -- twice the rows in flight per thread instead)
+// (wide cells: one block per CU by LDS -- a 1024-thread block, 4 waves per SIMD)
 template <int FT4, bool PAIR, bool kWide = false>
-__global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(kWide ? 2 : 6))) void k_hist(
+__global__ __launch_bounds__(kWide ? kHistThreadsWide : kHistThreads) __attribute__((amdgpu_waves_per_eu(kWide ? 4 : 6))) void k_hist(
     GbdtDev d, int parity, int tree, int level, int chunk) {
   static_assert(!kWide || (FT4 > 0 && !PAIR), "wide cells: 32-byte records, one lane per row");
   constexpr int kW = kWide ? 2 : 1;
@@ -1237,7 +1239,7 @@ __global__ __launch_bounds__(kHistThreads) __attribute__((amdgpu_waves_per_eu(kW
   const int lane = lane_id();
   int64_t tg = 0, th = 0;
   const int B = blockDim.x;
-  constexpr int U = kWide ? 8 : 4;  // rows in flight per thread
+  constexpr int U = 4;  // rows in flight per thread
   if constexpr (PAIR) {
     hist_rows_pair<FT4>(d, s_hist, hl, rix, identity, w.begin, w.end, tg, th);
   } else if constexpr (FT4 > 0) {
@@ -1662,27 +1664,41 @@ __device__ __forceinline__ longlong2 ipc_load_cell(const char* p) {
 template <int NR>
 __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m, int ncells,
                                               longlong2* s_cells, longlong2* hbw, bool store, bool store_tot) {
+  // U cells per thread per round trip: all U x NR loads (clamped, unconditional) are issued before the
+  // first sum -- over xGMI every round trip is a remote latency, and a 1024-thread block sums ~5k cells
+  constexpr int U = NR <= 2 ? 4 : 2;
   const char* sp[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r) sp[r] = iv->slot[r] + pair_bytes;
   const int me = __builtin_amdgcn_readfirstlane(iv->me);
-  for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    const int cell = i < mt ? cb + i : ncells + (i - mt);
-    longlong2 t[NR];
-    // (this rank's own slot: plain 16-byte loads -- an earlier kernel of this device wrote it)
+  const int B = (int)blockDim.x;
+  for (int i0 = threadIdx.x; i0 < m; i0 += U * B) {
+    longlong2 t[U][NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const char* p = sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2);
-      t[r] = r == me ? *reinterpret_cast<const longlong2*>(p) : ipc_load_cell(p);
-    }
-    longlong2 acc = t[0];
+    for (int u = 0; u < U; ++u) {
+      const int ic = min(i0 + u * B, m - 1);
+      const int cell = ic < mt ? cb + ic : ncells + (ic - mt);
+      // (this rank's own slot: plain 16-byte loads -- an earlier kernel of this device wrote it)
 #pragma unroll
-    for (int r = 1; r < NR; ++r) {
-      acc.x += t[r].x;
-      acc.y += t[r].y;
+      for (int r = 0; r < NR; ++r) {
+        const char* p = sp[r] + (int64_t)cell * (int64_t)sizeof(longlong2);
+        t[u][r] = r == me ? *reinterpret_cast<const longlong2*>(p) : ipc_load_cell(p);
+      }
     }
-    s_cells[i] = acc;
-    if (i < mt ? store : store_tot) hbw[cell] = acc;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * B;
+      if (i >= m) break;
+      const int cell = i < mt ? cb + i : ncells + (i - mt);
+      longlong2 acc = t[u][0];
+#pragma unroll
+      for (int r = 1; r < NR; ++r) {
+        acc.x += t[u][r].x;
+        acc.y += t[u][r].y;
+      }
+      s_cells[i] = acc;
+      if (i < mt ? store : store_tot) hbw[cell] = acc;
+    }
   }
 }
 
@@ -1855,9 +1871,8 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
         for (int c = 0; c < 4; ++c) pv[s][c] = make_longlong2(0, 0);
     }
   };
-  // fused exchange: the parent's loads (local, independent of the peers) are in flight during the
-  // wait for the ranks, instead of one more round trip after it
-  if (kFused && !kGroups) load_parent();  // (the grouped form spilled holding them)
+  // (fused exchange: the parent's loads come after the ranks' sums -- holding them across the exchange
+  // cost the registers that keep two cells' remote loads in flight per round trip, see ipc_sum_cells)
   // round trip 1 (uniform scalar loads); unconditional (in-bounds) loads selected after
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
@@ -1936,7 +1951,7 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
         v[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c])
                            : make_longlong2(0, 0);
     }
-  if (!kFused || kGroups) load_parent();
+  load_parent();
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     EvalFeat& e = ef[s];
@@ -3108,7 +3123,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
               stream, d);
     else if (fuse_root)
-      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.wide != 0), dim3(ceil_div(d.n, root_chunk)), dim3(512), c->lds_hist + tree_lds,
+      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.wide != 0), dim3(ceil_div(d.n, root_chunk)), dim3(d.wide ? 1024 : 512), c->lds_hist + tree_lds,
               stream, d, t, apply, root_chunk);
     else
       GLAUNCH("k_grad", k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
@@ -3131,7 +3146,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       const int ub = (level > 0 && !d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1
                                                : ceil_div(d.n, chh) + (1 << level);
       if (!(level == 0 && fuse_root))  // the fused gradient kernel already built the root histogram
-        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0, d.wide != 0), dim3(ub, ftiles), dim3(kHistThreads), c->lds_hist,
+        GLAUNCH("k_hist", hist_kernel(ft4, d.hist_pair != 0, d.wide != 0), dim3(ub, ftiles), dim3(d.wide ? kHistThreadsWide : kHistThreads), c->lds_hist,
                 stream, d, parity, t, level, chh);
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       const dim3 rgrid(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256));

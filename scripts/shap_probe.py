@@ -3,8 +3,10 @@
 pattern-table kernel (batches >= 256 rows) and the direct path-parallel EXTEND / UNWIND kernel, per
 batch size, device-resident rows. One JSON line per (kernel, batch).
 
-usage: shap_probe.py [batch ...]   (default 64 512 4096 65535)"""
+usage: shap_probe.py [batch ...]   (default 64 512 4096 65535); SHAP_TABLE_MIN=n: the table kernel from n
+rows (default predict_ops.SHAP_ROWS_MIN)"""
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -21,6 +23,8 @@ from cobalt_smart_lender_ai_amd.ops import predict_ops  # noqa: E402
 
 def main() -> None:
     sizes = [int(a) for a in sys.argv[1:]] or [64, 512, 4096, 65535]
+    if os.environ.get("SHAP_TABLE_MIN"):
+        predict_ops.SHAP_ROWS_MIN = int(os.environ["SHAP_TABLE_MIN"])
     b = load_pickle_bytes((ROOT / "tests" / "fixtures" / "xgb_model_tree.pkl").read_bytes())[1]
     dev = torch.device("cuda", 0)
     F = b.num_feature
