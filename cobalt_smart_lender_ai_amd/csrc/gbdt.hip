@@ -1364,12 +1364,16 @@ constexpr int kRedItems = 16;
 
 // kDP: data parallel (the replica-digest cell of level 0); the single-GPU instantiation has none of it.
 template <bool kDP>
-__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int n_grid, int level) {
+// `likely`: items below it exist in all but rare levels (the row-count bound); a block starting past it
+// (the hessian build rule's all-rows grid under data parallelism) reads the item count first and
+// leaves without its loads when it has no items -- usually the upper half of that grid.
+__global__ __launch_bounds__(256) void k_hist_reduce(GbdtDev d, int parity, int n_grid, int level, int likely) {
   BlockStamp stamp_(d);
   const int i0 = blockIdx.x * kRedItems;
   const int ncell = d.ncells;
   const int cell = blockIdx.y * blockDim.x + threadIdx.x;
   if (cell > ncell) return;
+  if (i0 >= likely && i0 >= __builtin_amdgcn_readfirstlane(d.counters[0])) return;
   const bool tot = cell == ncell;
   // Issue every load of the run before the first add, in ONE round trip together with the item
   // count: the item indices are clamped to the launched work-item range (n_grid <= items_cap), not
@@ -3151,10 +3155,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       d.hist_red = ipc ? static_cast<int64_t*>(ipc_send_buffer(cc)) : nullptr;
       const dim3 rgrid(ceil_div(ub, kRedItems), ceil_div((int64_t)d.ncells + 1, 256));
       const int rn = std::min(ub, c->items_cap);
+      // (the row-count bound of the items, for the reduce blocks past it under the hessian rule)
+      const int likely = (level > 0 && d.by_hess) ? ceil_div((d.n + 1) / 2, chh) + (1 << (level - 1)) + 1 : rn;
       if (dp)
-        GLAUNCH("k_hist_reduce", k_hist_reduce<true>, rgrid, dim3(256), 0, stream, d, parity, rn, level);
+        GLAUNCH("k_hist_reduce", k_hist_reduce<true>, rgrid, dim3(256), 0, stream, d, parity, rn, level, likely);
       else
-        GLAUNCH("k_hist_reduce", k_hist_reduce<false>, rgrid, dim3(256), 0, stream, d, parity, rn, level);
+        GLAUNCH("k_hist_reduce", k_hist_reduce<false>, rgrid, dim3(256), 0, stream, d, parity, rn, level, likely);
       CK_LAUNCH();
       if (dp) {  // every rank built the globally chosen child (hessian rule): all-reduced as is
         int rc;
