@@ -216,6 +216,14 @@ struct PathElem {
 };
 static_assert(sizeof(PathElem) == 24, "PathElem");
 
+// EXTEND / UNWIND without per-step divisions: the integer ratios (j + 1) / (l + 1) fold to constants of
+// the unrolled loops, 1 / (k - j) comes from kShapInv and 1 / zero is taken once per element; both SHAP
+// kernels (and so the pattern tables) use the same operation order, so their values stay bit-identical
+// to each other (and within rounding of the division form and of the host oracle).
+__constant__ double kShapInv[18] = {0.0,       1.0,        1.0 / 2,  1.0 / 3,  1.0 / 4,  1.0 / 5,
+                                    1.0 / 6,   1.0 / 7,    1.0 / 8,  1.0 / 9,  1.0 / 10, 1.0 / 11,
+                                    1.0 / 12,  1.0 / 13,   1.0 / 14, 1.0 / 15, 1.0 / 16, 1.0 / 17};
+
 // Canonical summation order (shared by both SHAP kernels, so a row's values do not depend on the
 // batch size or on which kernel ran): paths are cut into fixed chunks of kShapChunk; within a chunk
 // contributions are added in path order; k_shap_reduce adds the chunk sums in chunk order. No
@@ -256,8 +264,8 @@ __global__ __launch_bounds__(kShapChunk) void k_treeshap(const float* __restrict
 #pragma unroll
         for (int j = P - 2; j >= 0; --j) {
           if (j <= l - 1) {
-            w[j + 1] += one * w[j] * (double)(j + 1) / (double)(l + 1);
-            w[j] = e.zero * w[j] * (double)(l - j) / (double)(l + 1);
+            w[j + 1] += one * w[j] * ((double)(j + 1) / (double)(l + 1));
+            w[j] = e.zero * w[j] * ((double)(l - j) / (double)(l + 1));
           }
         }
       }
@@ -269,20 +277,21 @@ __global__ __launch_bounds__(kShapChunk) void k_treeshap(const float* __restrict
       if (i <= k) {
         const double one = o[i], zero = z[i];
         double total = 0.0;
-        if (one != 0.0) {
+        if (one != 0.0) {  // (one is 1 here)
           double next = w[k];
 #pragma unroll
           for (int j = P - 2; j >= 0; --j) {
             if (j <= k - 1) {
-              const double tmp = next / ((double)(j + 1) * one);
+              const double tmp = next * (1.0 / (double)(j + 1));
               total += tmp;
               next = w[j] - tmp * zero * (double)(k - j);
             }
           }
         } else {
+          const double iz = 1.0 / zero;
 #pragma unroll
           for (int j = P - 2; j >= 0; --j) {
-            if (j <= k - 1) total += w[j] / (zero * (double)(k - j));
+            if (j <= k - 1) total += w[j] * (iz * kShapInv[k - j]);
           }
         }
         total *= (double)(k + 1);
@@ -328,8 +337,8 @@ __global__ void k_shap_table(const PathElem* __restrict__ elems, const int32_t* 
 #pragma unroll
         for (int j = P - 2; j >= 0; --j) {
           if (j <= l - 1) {
-            w[j + 1] += one * w[j] * (double)(j + 1) / (double)(l + 1);
-            w[j] = e.zero * w[j] * (double)(l - j) / (double)(l + 1);
+            w[j + 1] += one * w[j] * ((double)(j + 1) / (double)(l + 1));
+            w[j] = e.zero * w[j] * ((double)(l - j) / (double)(l + 1));
           }
         }
       }
@@ -340,20 +349,21 @@ __global__ void k_shap_table(const PathElem* __restrict__ elems, const int32_t* 
       if (i <= k) {
         const double one = o[i], zero = z[i];
         double total = 0.0;
-        if (one != 0.0) {
+        if (one != 0.0) {  // (one is 1 here)
           double next = w[k];
 #pragma unroll
           for (int j = P - 2; j >= 0; --j) {
             if (j <= k - 1) {
-              const double tmp = next / ((double)(j + 1) * one);
+              const double tmp = next * (1.0 / (double)(j + 1));
               total += tmp;
               next = w[j] - tmp * zero * (double)(k - j);
             }
           }
         } else {
+          const double iz = 1.0 / zero;
 #pragma unroll
           for (int j = P - 2; j >= 0; --j) {
-            if (j <= k - 1) total += w[j] / (zero * (double)(k - j));
+            if (j <= k - 1) total += w[j] * (iz * kShapInv[k - j]);
           }
         }
         total *= (double)(k + 1);

@@ -67,7 +67,7 @@ for step in "$@"; do
         echo "$tag stamps rows=$rows: $(grep 'per tree' gpurun_out/${tag}_stamps_$rows.txt)" >> $OUT
       done ;;
     prof)
-      bash scripts/gpu_prof.sh $tag 300 300 --steps 1 --warmup 1 --test-rows 1000 > gpurun_out/${tag}_prof.log 2>&1 || exit $?
+      bash scripts/gpu_prof.sh $tag 300 600 --steps 1 --warmup 1 --test-rows 1000 > gpurun_out/${tag}_prof.log 2>&1 || exit $?
       echo "$tag prof: see prof_$tag.summary.txt" >> $OUT ;;
     multirank)
       for n in 2 4; do
