@@ -190,7 +190,6 @@ KNOBS: dict[str, Knob] = {
     "COBALT_FAULT_STALL_S": Knob("0", "test", "the faulting rank stalls this long once instead of dying"),
     "COBALT_FAULT_CORRUPT_RANK": Knob("-1", "test", "this rank perturbs a tree's root totals (replica-divergence test)"),
     "COBALT_FAULT_CORRUPT_TREE": Knob("1", "test", "the tree COBALT_FAULT_CORRUPT_RANK perturbs"),
-    "COBALT_TEST_DP8": Knob("0", "test", "run the 8-process shared-GPU data-parallel test"),
     "COBALT_REFERENCE_PKL": Knob("", "test", "path of the reference's shipped model for the golden tests"),
     "COBALT_REFERENCE_UI": Knob("", "test", "path of the reference Streamlit script for the UI replay test"),
     "COBALT_RECORD_UI": Knob("", "test", "record the UI replay's exchanges"),
