@@ -1667,10 +1667,10 @@ __device__ __forceinline__ longlong2 ipc_load_cell(const char* p) {
 
 template <int NR>
 __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m, int ncells,
-                                              longlong2* s_cells, longlong2* hbw, bool store, bool store_tot) {
+                                              longlong2* s_cells, longlong2* hbw, bool store, bool store_tot, bool sub) {
   // U cells per thread per round trip: all U x NR loads (clamped, unconditional) are issued before the
   // first sum -- over xGMI every round trip is a remote latency, and a 1024-thread block sums ~5k cells
-  constexpr int U = NR <= 2 ? 4 : 2;
+  constexpr int U = NR <= 4 ? 4 : 2;
   const char* sp[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r) sp[r] = iv->slot[r] + pair_bytes;
@@ -1700,7 +1700,7 @@ __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pa
         acc.x += t[u][r].x;
         acc.y += t[u][r].y;
       }
-      s_cells[i] = acc;
+      s_cells[i] = sub && i < mt ? make_longlong2(s_cells[i].x - acc.x, s_cells[i].y - acc.y) : acc;
       if (i < mt ? store : store_tot) hbw[cell] = acc;
     }
   }
@@ -1711,7 +1711,7 @@ __device__ __forceinline__ void ipc_sum_cells(const IpcFusedView* iv, int64_t pa
 // histogram loads in flight across the exchange and spilled with 16)
 __device__ __forceinline__ void ipc_sum_cells_wide(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m,
                                                    int ncells, longlong2* s_cells, longlong2* hbw, bool store,
-                                                   bool store_tot) {
+                                                   bool store_tot, bool sub) {
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
     const int cell = i < mt ? cb + i : ncells + (i - mt);
     const int64_t off = pair_bytes + (int64_t)cell * (int64_t)sizeof(longlong2);
@@ -1728,21 +1728,21 @@ __device__ __forceinline__ void ipc_sum_cells_wide(int nr, const IpcFusedView* i
         acc.y += t[r].y;
       }
     }
-    s_cells[i] = acc;
+    s_cells[i] = sub && i < mt ? make_longlong2(s_cells[i].x - acc.x, s_cells[i].y - acc.y) : acc;
     if (i < mt ? store : store_tot) hbw[cell] = acc;
   }
 }
 
 __device__ __forceinline__ void ipc_sum_cells_n(int nr, const IpcFusedView* iv, int64_t pair_bytes, int cb, int mt, int m,
                                                 int ncells, longlong2* s_cells, longlong2* hbw, bool store,
-                                                bool store_tot) {
+                                                bool store_tot, bool sub) {
   switch (nr) {
 #define IPC_SUM_CASE(K) \
-    case K: ipc_sum_cells<K>(iv, pair_bytes, cb, mt, m, ncells, s_cells, hbw, store, store_tot); break;
+    case K: ipc_sum_cells<K>(iv, pair_bytes, cb, mt, m, ncells, s_cells, hbw, store, store_tot, sub); break;
     IPC_SUM_CASE(1) IPC_SUM_CASE(2) IPC_SUM_CASE(3) IPC_SUM_CASE(4) IPC_SUM_CASE(5) IPC_SUM_CASE(6)
     IPC_SUM_CASE(7) IPC_SUM_CASE(8)
 #undef IPC_SUM_CASE
-    default: ipc_sum_cells_wide(nr, iv, pair_bytes, cb, mt, m, ncells, s_cells, hbw, store, store_tot); break;
+    default: ipc_sum_cells_wide(nr, iv, pair_bytes, cb, mt, m, ncells, s_cells, hbw, store, store_tot, sub); break;
   }
 }
 
@@ -1875,8 +1875,10 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
         for (int c = 0; c < 4; ++c) pv[s][c] = make_longlong2(0, 0);
     }
   };
-  // (fused exchange: the parent's loads come after the ranks' sums -- holding them across the exchange
-  // cost the registers that keep two cells' remote loads in flight per round trip, see ipc_sum_cells)
+  // (fused exchange, per-node blocks: the subtracted sibling's parent histogram goes to LDS while wave 0
+  // waits for the peers, and the ranks' sums are subtracted from it there -- no global load after the
+  // exchange, and no parent registers held across it; grouped blocks load it after the exchange)
+  constexpr bool kParLds = kFused && !kGroups;
   // round trip 1 (uniform scalar loads); unconditional (in-bounds) loads selected after
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
@@ -1900,6 +1902,11 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
         return false;
       }
     }
+    const bool sub = kParLds && level > 0 && !built;  // block-uniform
+    if (sub && threadIdx.x >= kWave) {  // waves 1.. (wave 0 polls the peers' flags)
+      const longlong2* par = reinterpret_cast<const longlong2*>(parent) + cb;
+      for (int i = (int)threadIdx.x - kWave; i < ce - cb; i += (int)blockDim.x - kWave) s_cells[i] = par[i];
+    }
     if (!ipc_wait<kIpcAcquireFence>(iv->ftab, iv->n, iv->me, iv->myflag, d.ipc_epoch, iv->err_host, iv->timeout))
       return false;
     // the global root totals are stored at level 0 (k_eval_finish reads them)
@@ -1907,7 +1914,7 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
     ipc_sum_cells_n(__builtin_amdgcn_readfirstlane(iv->n), iv, (int64_t)pair * SE * (int64_t)sizeof(int64_t), cb,
                     ce - cb, ce - cb + 1 + (level == 0 ? 1 : 0), d.ncells, s_cells,
                     reinterpret_cast<longlong2*>(d.hist_b[parity] + pair * SE), built && status == kActive,
-                    level == 0 && blockIdx.y == 0);
+                    level == 0 && blockIdx.y == 0, sub);
     __syncthreads();
     const longlong2 tot = s_cells[ce - cb];
     rg = tot.x;
@@ -1955,15 +1962,16 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
         v[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c])
                            : make_longlong2(0, 0);
     }
-  load_parent();
+  if (!kParLds) load_parent();
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     EvalFeat& e = ef[s];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const bool in = e.on && c * kWave + lane < e.nb;
-      const int64_t g = built ? v[s][c].x : pv[s][c].x - v[s][c].x;
-      const int64_t h = built ? v[s][c].y : pv[s][c].y - v[s][c].y;
+      // (kParLds: the LDS cells already hold this node's own histogram)
+      const int64_t g = (kParLds || built) ? v[s][c].x : pv[s][c].x - v[s][c].x;
+      const int64_t h = (kParLds || built) ? v[s][c].y : pv[s][c].y - v[s][c].y;
       e.g[c] = in ? g : 0;
       e.h[c] = in ? h : 0;
     }
