@@ -131,6 +131,9 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
         params = GBDTParams.from_kwargs(**params)
     if not 0.0 < sample_rate <= 1.0:
         raise ValueError("sample_rate must be in (0, 1]")
+    if int(params.grad_bits) != 17:
+        # the page passes (cobalt_gbdt_ox_init / the sampled grow) keep the packed 17-bit (g, h) cells
+        raise ValueError(f"out-of-core training supports grad_bits=17 only (got {params.grad_bits})")
     exact = sample_rate >= 1.0  # every row every tree: level-wise page streaming (no sample)
     dev = _resolve_device(device, None)
     if exact and dev.type == "cuda":

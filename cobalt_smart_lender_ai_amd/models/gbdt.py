@@ -363,6 +363,16 @@ def expand_features(bst: Booster, feats, n_features: int, feature_names: Sequenc
                    bst.objective, dict(bst.train_params), dict(bst.attributes))
 
 
+def check_grad_bits(grad_bits: int, n_features: int, device_type: str) -> None:
+    """``grad_bits`` is 17 or 25; the GPU's wide (25-bit) cells need the 32-byte row records of <= 24
+    features (csrc/gbdt.hip cobalt_gbdt_create refuses the rest with -6)."""
+    if grad_bits not in gbdt_host.GRAD_BITS:
+        raise ValueError(f"grad_bits must be one of {gbdt_host.GRAD_BITS}")
+    if grad_bits > 17 and device_type == "cuda" and n_features > 24:
+        raise ValueError(f"grad_bits={grad_bits} on the GPU supports <= 24 features (32-byte row records); "
+                         f"got {n_features}: use grad_bits=17")
+
+
 def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, device=None,
           feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
           dist=None, n_rows_global: int | None = None, row_offset: int = 0,
@@ -431,9 +441,8 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     dev = bd.device
     world = dist.world if dist is not None else 1
     grad_bits = int(params.grad_bits)
-    if grad_bits not in gbdt_host.GRAD_BITS:
-        raise ValueError(f"grad_bits must be one of {gbdt_host.GRAD_BITS}")
     N, F = bd.n_rows, bd.n_features
+    check_grad_bits(grad_bits, F, dev.type)
     rep = report if report is not None else FitReport()
     tp = rep.mark("pre", time.perf_counter(), dev)
     yt = _to_tensor(y, dev).reshape(-1)

@@ -127,3 +127,18 @@ def test_wide_gradients_track_fp64_closer_than_17_bits():
     lw = _logloss(gbdt.train(X, y, gbdt.GBDTParams(**{**p30.__dict__, "grad_bits": 25}), device="cpu"), X, y)
     lf = _logloss(gbdt.train(X, y, p30, device="cpu", exact_fp64=True), X, y)
     assert abs(lw / lf - 1) < 0.002
+
+
+def test_wide_gradient_limits_are_named():
+    """grad_bits outside {17, 25}, 25 bits on the GPU with more than 24 features (no 32-byte records)
+    and 25 bits out of core are refused with a message naming the limit, not a native error code."""
+    gbdt.check_grad_bits(25, 24, "cuda")
+    gbdt.check_grad_bits(25, 106, "cpu")  # the host trainer has no record layout limit
+    with pytest.raises(ValueError, match="one of"):
+        gbdt.check_grad_bits(16, 20, "cpu")
+    with pytest.raises(ValueError, match="<= 24 features"):
+        gbdt.check_grad_bits(25, 25, "cuda")
+    from cobalt_smart_lender_ai_amd.models.external import train_external
+
+    with pytest.raises(ValueError, match="grad_bits=17 only"):
+        train_external(lambda: iter(()), gbdt.GBDTParams(grad_bits=25), sample_rate=1.0, device="cpu")
