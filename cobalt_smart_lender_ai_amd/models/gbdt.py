@@ -373,6 +373,16 @@ def check_grad_bits(grad_bits: int, n_features: int, device_type: str) -> None:
                          f"got {n_features}: use grad_bits=17")
 
 
+def check_gpu_shape(max_depth: int, n_rows: int) -> None:
+    """The GPU trainer's limits (csrc/gbdt.hip cobalt_gbdt_create: -1 / -5), named before any device work."""
+    if not 1 <= max_depth <= 10:
+        raise ValueError(f"the GPU trainer supports max_depth 1-10 (got {max_depth}); use the host trainer "
+                         "(device='cpu') for deeper trees")
+    if n_rows >= (1 << 31) - 1:
+        raise ValueError(f"{n_rows} rows exceed one GPU fit's int32 row ids: shard them over ranks "
+                         "(data parallel) or stream them (models.external.train_external)")
+
+
 def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, device=None,
           feature_names: Sequence[str] | None = None, feature_types: Sequence[str] | None = None,
           dist=None, n_rows_global: int | None = None, row_offset: int = 0,
@@ -443,6 +453,8 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     grad_bits = int(params.grad_bits)
     N, F = bd.n_rows, bd.n_features
     check_grad_bits(grad_bits, F, dev.type)
+    if dev.type == "cuda":
+        check_gpu_shape(int(params.max_depth), N)
     rep = report if report is not None else FitReport()
     tp = rep.mark("pre", time.perf_counter(), dev)
     yt = _to_tensor(y, dev).reshape(-1)

@@ -142,3 +142,11 @@ def test_wide_gradient_limits_are_named():
 
     with pytest.raises(ValueError, match="grad_bits=17 only"):
         train_external(lambda: iter(()), gbdt.GBDTParams(grad_bits=25), sample_rate=1.0, device="cpu")
+
+
+def test_gpu_shape_limits_are_named():
+    gbdt.check_gpu_shape(10, 10_000_000)
+    with pytest.raises(ValueError, match="max_depth 1-10"):
+        gbdt.check_gpu_shape(11, 1000)
+    with pytest.raises(ValueError, match="int32 row ids"):
+        gbdt.check_gpu_shape(7, 1 << 31)
