@@ -43,6 +43,8 @@ def rank_main(rank: int, world: int, port: int, out_dir: str, rows: int, params:
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank if one_gpu_per_rank else 0), LOCAL_WORLD_SIZE=str(world))
     os.environ.setdefault("OMP_NUM_THREADS", "2")
+    if "{rank}" in os.environ.get("COBALT_STAMPS", ""):  # per-rank stamp files (diagnostics)
+        os.environ["COBALT_STAMPS"] = os.environ["COBALT_STAMPS"].replace("{rank}", str(rank))
     res: dict = {"rank": rank, "world": world, "ok": False}
     t0 = time.monotonic()
     ctx = None

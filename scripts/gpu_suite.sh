@@ -77,6 +77,13 @@ for step in "$@"; do
     dpdiag)
       bash $S ${tag}_dpdiag 900 python -u scripts/dp8_diag.py ${DP_SET:-width} || exit $?
       echo "$tag dpdiag: $(tail -3 gpurun_out/${tag}_dpdiag.log)" >> $OUT ;;
+    rankstamps)
+      bash $S ${tag}_rankstamps 600 python -u scripts/dp_rank_stamps.py ${DP_ROWS:-1250000} ${RS_PROCS:-2 4 8} || exit $?
+      for n in ${RS_PROCS:-2 4 8}; do
+        python scripts/stamp_summary.py gpurun_out/dprs_${n}_rank0.txt > gpurun_out/${tag}_rankstamps_$n.txt || exit $?
+        echo "$tag rankstamps n=$n: $(grep 'per tree' gpurun_out/${tag}_rankstamps_$n.txt)" >> $OUT
+      done
+      rm -f gpurun_out/dprs_*_rank*.txt ;;
     qdiag)
       bash $S ${tag}_qdiag 900 python -u scripts/dp_queue_diag.py $QDIAG_CFGS || exit $?
       echo "$tag qdiag: see ${tag}_qdiag.log" >> $OUT ;;
