@@ -28,6 +28,7 @@ import sys
 import time
 
 import torch
+from cobalt_smart_lender_ai_amd.config import knob
 
 BASELINE_ROWS_PER_S = None  # the reference publishes no throughput (BASELINE.json "published": {})
 
@@ -66,7 +67,7 @@ def main() -> None:
 
     # COBALT_BENCH_SHARED_DEVICE=1: every rank on cuda:0 (the 1-GPU multi-process rehearsal); each rank
     # then launches on its own CU-masked share of the device (parallel/cumask.py)
-    shared = os.environ.get("COBALT_BENCH_SHARED_DEVICE") == "1"
+    shared = knob("COBALT_BENCH_SHARED_DEVICE") == "1"
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if shared and torch.cuda.is_available():
         from cobalt_smart_lender_ai_amd.parallel import cumask
@@ -193,8 +194,8 @@ def main() -> None:
             "dp_transport_fallback": fallback,
             # csrc/gbdt.hip node ownership: deep levels evaluated by the subtree's owner rank only
             "dp_node_ownership": (f"levels {max((world - 1).bit_length(), a.depth - 3)}-{a.depth - 1}"
-                                  if world > 1 and ctx.transport == "ipc" and os.environ.get("COBALT_DP_OWNER", "1") != "0"
-                                  and os.environ.get("COBALT_IPC_FUSED", "1") != "0" else None),
+                                  if world > 1 and ctx.transport == "ipc" and knob("COBALT_DP_OWNER", "1") != "0"
+                                  and knob("COBALT_IPC_FUSED", "1") != "0" else None),
             "replica_check": "in-flight per-tree digest of every rank's split decisions" if world > 1 else None,
             "replicas_agree": replicas_agree,
             "auc": None if auc is None else round(auc, 5),

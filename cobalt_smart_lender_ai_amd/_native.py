@@ -18,6 +18,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the dlopen of the HIP library)
 
 from . import build as _build
+from .config import knob
 
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
@@ -126,7 +127,7 @@ def load(build_if_needed: bool = True) -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        override = os.environ.get("COBALT_NATIVE_LIB")  # e.g. the host-sanitizer build (build --sanitize)
+        override = knob("COBALT_NATIVE_LIB")  # e.g. the host-sanitizer build (build --sanitize)
         path = Path(override) if override else _build.lib_path()
         try:
             if not override and build_if_needed and _build.is_stale() and Path(_build.HIPCC).exists():
@@ -186,4 +187,4 @@ def rccl_path() -> str:
     p = Path(torch.__file__).parent / "lib" / "librccl.so"
     if p.exists():
         return str(p)
-    return os.environ.get("COBALT_RCCL_LIB", "/opt/rocm/lib/librccl.so")
+    return knob("COBALT_RCCL_LIB", "/opt/rocm/lib/librccl.so")

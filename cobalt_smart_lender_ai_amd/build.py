@@ -25,12 +25,13 @@ import shutil
 import subprocess
 import sys
 from pathlib import Path
+from .config import knob
 
 PKG_DIR = Path(__file__).resolve().parent
 CSRC = PKG_DIR / "csrc"
 OUT_DIR = PKG_DIR / "_lib"
 LIB_NAME = "libcobalt_hip.so"
-ARCH = os.environ.get("COBALT_OFFLOAD_ARCH", "gfx950")
+ARCH = knob("COBALT_OFFLOAD_ARCH", "gfx950")
 
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",

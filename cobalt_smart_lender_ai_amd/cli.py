@@ -19,6 +19,7 @@ import argparse
 import json
 import logging
 import sys
+from .config import knob
 
 
 def _store(args):
@@ -109,7 +110,7 @@ def cmd_serve(args) -> int:
     # owns the GPU (serve/scorer.py): one engine, one set of hipGraphs, and micro-batches that pool the
     # requests of every worker.
     scorer = None
-    if args.workers > 1 and not os.environ.get("COBALT_SCORER_SOCKET"):
+    if args.workers > 1 and not knob("COBALT_SCORER_SOCKET"):
         sock = os.path.join(tempfile.mkdtemp(prefix="cobalt_scorer_"), "scorer.sock")
         cmd = [sys.executable, "-m", "cobalt_smart_lender_ai_amd.serve.scorer", "--socket", sock]
         if args.device:

@@ -2564,8 +2564,9 @@ struct GbdtCtx {
   int fault_tree = -1;          // fault injection: tree whose root totals are perturbed on this rank
   uint32_t dec_tag = 0;         // k_eval_part<.., 2>: the launch tag of the decision granules (d.dec)
   // the last grow call's plan (cobalt_gbdt_plan): fused IPC exchange, ownership level, wide gradients,
-  // resident blocks of the fused k_eval, levels run by the fused evaluation + partition pass
-  int32_t plan[6] = {0, -1, 0, 0, 0, 0};
+  // resident blocks of the fused k_eval, levels run by the fused evaluation + partition pass (and of them
+  // the evaluator-block levels, and those whose grid exceeds one block per CU)
+  int32_t plan[7] = {0, -1, 0, 0, 0, 0, 0};
   unsigned* err_pinned = nullptr;  // mapped host word behind d.err_host
   // COBALT_STAMPS=<file>: per-launch in-kernel timing of every grow call, appended to <file>
   const char* stamp_path = nullptr;
@@ -3106,11 +3107,15 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   c->plan[3] = resident;
   c->plan[4] = 0;  // levels run by the fused evaluation + partition pass (bit mask)
   c->plan[5] = 0;  // ... of them in the evaluator-block form
+  c->plan[6] = 0;  // ... of those, levels whose grid (evaluators + items) exceeds one block per CU: the items
+                   // past the resident ones start as earlier blocks retire (in-order dispatch, evaluators first)
   for (int level = 0; level + 1 < D; ++level) {
     int m = 0;
-    if (ep_plan(level, m) > 0) {
+    const int ch = ep_plan(level, m);
+    if (ch > 0) {
       c->plan[4] |= 1 << level;
       if (m >= 2) c->plan[5] |= 1 << level;
+      if (m >= 2 && ceil_div(d.n, ch) + (2 << level) > device_cu_count()) c->plan[6] |= 1 << level;
     }
   }
   d.zero_red = nullptr;
@@ -3599,10 +3604,11 @@ COBALT_API int cobalt_gbdt_set_start(void* h, int t0) {
 
 // The last grow call's launch plan (GbdtCtx::plan): out[0] fused IPC exchange, [1] node-ownership level
 // (-1 off), [2] wide gradients, [3] blocks of the fused k_eval this rank's CUs hold at once, [4] bit mask of
-// the levels run by the fused evaluation + partition pass, [5] of them in the evaluator-block form.
+// the levels run by the fused evaluation + partition pass, [5] of them in the evaluator-block form, [6] of
+// those the levels whose grid exceeds one block per CU.
 COBALT_API int cobalt_gbdt_plan(void* h, int32_t* out) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
-  for (int k = 0; k < 6; ++k) out[k] = c->plan[k];
+  for (int k = 0; k < 7; ++k) out[k] = c->plan[k];
   return 0;
 }
 

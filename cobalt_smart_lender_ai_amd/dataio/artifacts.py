@@ -20,6 +20,7 @@ from pathlib import Path
 import pandas as pd
 
 from ..config import BUCKET_NAME
+from ..config import knob
 
 
 class ArtifactStore:
@@ -115,7 +116,7 @@ class S3Store(ArtifactStore):
 
 
 def get_store(uri: str | None = None) -> ArtifactStore:
-    uri = uri or os.environ.get("COBALT_ARTIFACT_URI", "data-lake")
+    uri = uri or knob("COBALT_ARTIFACT_URI", "data-lake")
     if uri.startswith("s3://"):
         return S3Store(uri[5:].split("/")[0] or BUCKET_NAME)
     return LocalStore(uri)

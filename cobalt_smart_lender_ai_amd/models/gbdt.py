@@ -30,6 +30,7 @@ import torch
 
 from . import gbdt_host, sketch
 from .booster import Booster, dump_pickle_bytes, sigmoid32, trees_from_heap_nodes
+from ..config import knob
 
 log = logging.getLogger(__name__)
 
@@ -247,7 +248,7 @@ def bin_dataset(X, *, max_bin: int = 256, sketch_rows: int | None = SKETCH_AUTO,
     full = not sketch_rows
     if full and dev.type == "cuda" and sketch_mode != "summary":
         # every row, exactly (csrc/sketch.hip: bucket histograms + per-bucket selection, no row sort;
-        # under data parallelism three device all-reduces -- the missing flags ride in the first -- so
+        # under data parallelism four device all-reduces -- the missing flags ride in the first -- so
         # the cuts are the full data's)
         sw = _to_tensor(sketch_weights, dev).reshape(-1) if sketch_weights is not None else None
         cuts, nbins = sketch.device_exact_cuts(Xt, max_bin, sw, has_missing if world == 1 else None,
@@ -413,6 +414,11 @@ def train(X, y, params: GBDTParams | dict | None = None, *, sample_weight=None, 
             total = int(params.n_estimators)
             log.info("resuming from %s at tree %d of %d", checkpoint_path, init_booster.num_trees, total)
     dev = _resolve_device(device, X)
+    # the trainer's shape limits, before the sketch (and its data-parallel collectives) and the binning;
+    # train_binned checks them again for pre-binned inputs
+    check_grad_bits(int(params.grad_bits), int(X.shape[1]), dev.type)
+    if dev.type == "cuda":
+        check_gpu_shape(int(params.max_depth), int(X.shape[0]))
     init_margin = None
     if init_booster is not None:
         from ..ops import predict_ops
@@ -531,10 +537,10 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         trees_so_far.extend(trees_from_heap_nodes(new_nodes, hp.max_depth))
         if checkpoint is not None:
             checkpoint.save(make_booster(trees_so_far))
-        fault_after = int(os.environ.get("COBALT_FAULT_AFTER_TREES", "0") or 0)
-        fault_rank = int(os.environ.get("COBALT_FAULT_RANK", "-1") or -1)
+        fault_after = int(knob("COBALT_FAULT_AFTER_TREES", "0") or 0)
+        fault_rank = int(knob("COBALT_FAULT_RANK", "-1") or -1)
         if fault_after and end >= fault_after and end < T and (fault_rank < 0 or fault_rank == (dist.rank if dist else 0)):
-            stall = float(os.environ.get("COBALT_FAULT_STALL_S", "0") or 0)
+            stall = float(knob("COBALT_FAULT_STALL_S", "0") or 0)
             if stall > 0:  # a slow (not dead) rank: once, then it carries on
                 if not getattr(segment_done, "stalled", False):
                     segment_done.stalled = True
@@ -570,7 +576,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                     yt.contiguous(), wt, margin, fm)
         # 0/1 labels and no sample weights: the labels ride in the row records' padding and the weights
         # follow from them (8 fewer bytes per row in every gradient pass); COBALT_LABEL_IN_RECORD=0 off
-        if (sample_weight is None and os.environ.get("COBALT_LABEL_IN_RECORD", "1") != "0"
+        if (sample_weight is None and knob("COBALT_LABEL_IN_RECORD", "1") != "0"
                 and bd.records.shape[1] == 32 and F <= 23
                 and bool(((yt == 0) | (yt == 1)).all())):
             tr.set_binary_labels(float(np.float32(spw)))
@@ -582,9 +588,9 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
             if world > 1:
                 # COBALT_FAULT_CORRUPT_RANK=r [COBALT_FAULT_CORRUPT_TREE=t]: rank r grows a different tree t
                 # (its root totals perturbed), which the in-flight replica check must catch on every rank
-                cr = int(os.environ.get("COBALT_FAULT_CORRUPT_RANK", "-1") or -1)
+                cr = int(knob("COBALT_FAULT_CORRUPT_RANK", "-1") or -1)
                 if cr == dist.rank:
-                    tr.set_fault(int(os.environ.get("COBALT_FAULT_CORRUPT_TREE", "1") or 1))
+                    tr.set_fault(int(knob("COBALT_FAULT_CORRUPT_TREE", "1") or 1))
             for s0 in range(T0, T, seg):
                 s1 = min(T, s0 + seg)
                 tr.grow(s0, s1 - s0)

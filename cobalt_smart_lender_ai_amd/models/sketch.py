@@ -43,6 +43,7 @@ import math
 
 import numpy as np
 import torch
+from ..config import knob
 
 FLT_MAX = float(np.finfo(np.float32).max)
 MAX_BINS = 256        # bins of a feature without missing values (uint8 codes 0..255)
@@ -404,18 +405,19 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     pass histograms the rows per bucket, the target ranks are located by prefix sums, and only the
     rows of the few buckets that hold a target are gathered and sorted (in LDS, per bucket).
 
-    Under data parallelism (``dist``) every rank passes its shard and the ranks exchange exactly three
+    Under data parallelism (``dist``) every rank passes its shard and the ranks exchange four
     fixed-layout SUM all-reduces on the device (``dist.device_allreduce``; no size exchanges, no
     padding): (1) the global strided sample, placed by global sample index, with the missing-value flags
-    and the weight scale; (2) every rank's bucket counts (+ weight sums) and value range, by rank slot --
-    so each rank also knows where its rows go inside every global candidate segment; (3) the candidates,
-    written straight into the global segment layout. Every rank then computes the full data's cuts.
+    and the weight scale; (2) the bucket counts (+ weight sums), summed, and every rank's value range by
+    rank slot; (2b) every rank's rows of the few selected bucket segments, by rank slot -- where its
+    candidates go inside each global segment; (3) the candidates, written straight into the global
+    segment layout. Every rank then computes the full data's cuts.
     ``w_max`` scales the weights (default: the global max)."""
     import os
 
     N, F = X.shape
     dev = X.device
-    timing = os.environ.get("COBALT_SK_TIMING") == "1"  # per-stage times (device-synchronised) to stderr
+    timing = knob("COBALT_SK_TIMING") == "1"  # per-stage times (device-synchronised) to stderr
     marks = []
 
     def mark(name):
@@ -489,31 +491,48 @@ def _fkey64_inv(k: torch.Tensor) -> torch.Tensor:
 
 
 def _allreduce_buckets(dist, dev, cnt_loc, w_loc, vmin, vmax):
-    """Collective 2 of the data-parallel exact sketch: ONE int64 SUM all-reduce of every rank's bucket
-    counts (and weight sums) in its own rank slot, plus its value range as order keys. Returns the global
-    counts, weight sums, min / max, and this rank's row offset inside every bucket (the rows of the
-    lower ranks) -- the position of its candidates in the global segment layout, with no further
-    exchange."""
+    """Collective 2 of the data-parallel exact sketch: ONE int64 SUM all-reduce of the bucket counts
+    (and weight sums), summed in place -- F x NB cells whatever the rank count -- plus every rank's value
+    range as order keys in its own 2F slots. Returns the global counts, weight sums, min / max. (Each
+    rank's offset inside the few selected buckets comes from collective 2b, _segment_offsets: per-rank
+    slots of the whole F x NB table would grow the message with the rank count -- ~111 MB per rank at 8
+    ranks for the 106-feature RFE fits with weights.)"""
     R, r = dist.world, dist.rank
     F, NB = cnt_loc.shape
     FN = F * NB
     nw = FN if w_loc is not None else 0
-    buf = torch.zeros(R * (FN + nw + 2 * F), dtype=torch.int64, device=dev)
-    base = r * (FN + nw + 2 * F)
-    buf[base:base + FN] = cnt_loc.reshape(-1)
+    buf = torch.zeros(FN + nw + R * 2 * F, dtype=torch.int64, device=dev)
+    buf[:FN] = cnt_loc.reshape(-1)
     if w_loc is not None:
-        buf[base + FN:base + FN + nw] = w_loc.reshape(-1)
-    buf[base + FN + nw:base + FN + nw + F] = _fkey64(vmin)
-    buf[base + FN + nw + F:base + FN + nw + 2 * F] = _fkey64(vmax)
+        buf[FN:FN + nw] = w_loc.reshape(-1)
+    base = FN + nw + r * 2 * F
+    buf[base:base + F] = _fkey64(vmin)
+    buf[base + F:base + 2 * F] = _fkey64(vmax)
     dist.device_allreduce(buf, "sum")
-    per = buf.reshape(R, FN + nw + 2 * F)
-    cnts = per[:, :FN].reshape(R, F, NB)
-    cnt_h = cnts.sum(0)
-    before = (torch.cumsum(cnts, 0) - cnts)[r]
-    w_h = per[:, FN:FN + nw].reshape(R, F, NB).sum(0) if w_loc is not None else None
-    vmin_g = _fkey64_inv(per[:, FN + nw:FN + nw + F].amin(0))
-    vmax_g = _fkey64_inv(per[:, FN + nw + F:].amax(0))
-    return cnt_h, w_h, vmin_g, vmax_g, before
+    cnt_h = buf[:FN].reshape(F, NB)
+    w_h = buf[FN:FN + nw].reshape(F, NB) if w_loc is not None else None
+    keys = buf[FN + nw:].reshape(R, 2 * F)
+    vmin_g = _fkey64_inv(keys[:, :F].amin(0))
+    vmax_g = _fkey64_inv(keys[:, F:].amax(0))
+    return cnt_h, w_h, vmin_g, vmax_g
+
+
+def _segment_offsets(dist, dev, loc_sizes):
+    """Collective 2b: this rank's rows of every selected bucket segment (the same segments on every rank:
+    the selection depends only on the global counts) in its own slot of one R x nseg int64 SUM
+    all-reduce; returns the rows of the lower ranks per segment -- where this rank's candidates start
+    inside the segment's global layout. Issued also when nseg == 0 (one cell), so every data-parallel
+    sketch runs the same number of collectives."""
+    R, r = dist.world, dist.rank
+    nseg = int(loc_sizes.numel())
+    buf = torch.zeros(max(R * nseg, 1), dtype=torch.int64, device=dev)
+    if nseg:
+        buf[r * nseg:(r + 1) * nseg] = loc_sizes
+    dist.device_allreduce(buf, "sum")
+    if not nseg:
+        return torch.zeros(0, dtype=torch.int64, device=dev)
+    per = buf.reshape(R, nseg)
+    return (torch.cumsum(per, 0) - per)[r]
 
 
 def stream_exact_cuts(chunks, n_rows: int, n_features: int, samp: torch.Tensor, has_missing: torch.Tensor,
@@ -525,7 +544,7 @@ def stream_exact_cuts(chunks, n_rows: int, n_features: int, samp: torch.Tensor, 
     import os
 
     dev = torch.device(device)
-    timing = os.environ.get("COBALT_SK_TIMING") == "1"
+    timing = knob("COBALT_SK_TIMING") == "1"
     marks = []
 
     def mark(name):
@@ -613,9 +632,8 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
         if single:
             kept = (XT, Xc.shape[0], wq, nblk, cnt_slab)
     cnt_h = cnt_loc
-    before = None  # (data parallel) this rank's offset inside every bucket's global candidate segment
     if world > 1:  # collective 2
-        cnt_h, w_h, vmin, vmax, before = _allreduce_buckets(dist, dev, cnt_loc, w_h, vmin, vmax)
+        cnt_h, w_h, vmin, vmax = _allreduce_buckets(dist, dev, cnt_loc, w_h, vmin, vmax)
     if w_h is None:
         w_h = cnt_h
     mark("hist")
@@ -667,7 +685,7 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
         cbuf = torch.zeros(max(2 * tot if weighted else tot, 1), dtype=torch.int32, device=dev)
         cval = cbuf[:max(tot, 1)].view(torch.float32)
         cw = cbuf[tot:2 * tot] if weighted else None
-        start = glob_off[:-1] + before.reshape(-1)[sel_f]
+        start = glob_off[:-1] + _segment_offsets(dist, dev, loc_sizes)  # collective 2b
     else:
         tot_loc = int(loc_off[-1])
         cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)

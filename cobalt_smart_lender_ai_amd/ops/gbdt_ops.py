@@ -18,6 +18,7 @@ import torch
 
 from .. import _native
 from ..models.booster import NODE_DTYPE
+from ..config import knob
 
 
 class GbdtConfig(ctypes.Structure):
@@ -83,7 +84,7 @@ def bin_matrix(X: torch.Tensor, cuts: torch.Tensor, nbins: torch.Tensor) -> tupl
     # the vectorised kernel (k_bin_rec32: 32-byte records, F % 4 == 0, 16-byte aligned rows) writes
     # every byte of every record; the generic one only the bins
     whole = (st == 32 and F % 4 == 0 and F <= 24 and X.data_ptr() % 16 == 0
-             and not os.environ.get("COBALT_BIN_SCALAR"))
+             and not knob("COBALT_BIN_SCALAR"))
     bins = (torch.empty if whole else torch.zeros)((N, st), dtype=torch.uint8, device=X.device)
     binsT = torch.empty((F, N), dtype=torch.uint8, device=X.device)
     lib = _native.lib()
@@ -121,7 +122,7 @@ _PARKED_LOCK = threading.Lock()
 
 
 def _cache_on() -> bool:
-    return os.environ.get("COBALT_TRAINER_CACHE", "1") != "0"
+    return knob("COBALT_TRAINER_CACHE", "1") != "0"
 
 
 def release_cached_trainers() -> None:
@@ -215,12 +216,13 @@ class GpuGbdtTrainer:
         fn = getattr(self.lib, "cobalt_gbdt_plan", None)
         if fn is None or not self.h:
             return {}
-        out = (ctypes.c_int32 * 6)()
+        out = (ctypes.c_int32 * 7)()
         fn(self.h, out)
         return {"ipc_fused": bool(out[0]), "own_level": int(out[1]), "wide_gradients": bool(out[2]),
                 "fused_eval_resident_blocks": int(out[3]),
                 "eval_part_levels": [lv for lv in range(16) if (out[4] >> lv) & 1],
-                "eval_block_levels": [lv for lv in range(16) if (out[5] >> lv) & 1]}
+                "eval_block_levels": [lv for lv in range(16) if (out[5] >> lv) & 1],
+                "eval_block_overflow_levels": [lv for lv in range(16) if (out[6] >> lv) & 1]}
 
     def replica_error(self) -> int:
         """Data-parallel replica check (csrc/gbdt.hip GbdtDev::dig): 0 = healthy, 2 = this rank's trees

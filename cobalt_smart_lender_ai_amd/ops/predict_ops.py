@@ -14,12 +14,13 @@ import torch
 
 from .. import _native
 from ..models.booster import Booster, Tree, predict_margin_host, sigmoid32, treeshap_host
+from ..config import knob
 
 # LDS tile capacity in nodes: a model's tile is max(this, its largest tree), at most MAX_TILE_NODES
 # (csrc/predict.hip kMaxTileNodes). 2048 measured best on MI355X (125M-row scoring, 300 depth-7
 # trees: 1024 -> 793M, 2048 -> 810M, 3072 -> 683M, 6144 -> 490M, 8192 -> 261M rows/s) -- smaller
 # tiles mean more resident blocks per CU. COBALT_PRED_TILE overrides it for sweeps.
-TILE_NODES = int(os.environ.get("COBALT_PRED_TILE", "2048"))
+TILE_NODES = int(knob("COBALT_PRED_TILE", "2048"))
 MAX_TILE_NODES = 8192
 MAX_PATH = 15
 

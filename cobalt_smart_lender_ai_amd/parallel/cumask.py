@@ -27,6 +27,7 @@ import os
 from pathlib import Path
 
 import torch
+from ..config import knob
 
 _HIP = None
 
@@ -64,7 +65,7 @@ def shared_device_stream(rank: int, world: int, device: torch.device) -> torch.c
     (default: a contiguous range of mask bits, every XCC covered) or ``interleaved`` (CU rank + k * world;
     leaves XCCs empty when world and 8 share a factor -- scripts/dp_queue_diag.py)."""
     n_cu = torch.cuda.get_device_properties(device).multi_processor_count
-    layout = os.environ.get("COBALT_CU_MASK_LAYOUT", "blocked")
+    layout = knob("COBALT_CU_MASK_LAYOUT", "blocked")
     words = interleaved_mask(rank, world, n_cu) if layout == "interleaved" else blocked_mask(rank, world, n_cu)
     arr = (ctypes.c_uint32 * len(words))(*words)
     h = ctypes.c_void_p()
@@ -98,7 +99,7 @@ MAX_MASKED_RANKS = 8
 def want_shared_mask(world: int) -> bool:
     """Partition the CUs when ranks share a device (``COBALT_SHARED_CU_MASK``: default on for 2 to
     ``MAX_MASKED_RANKS`` ranks, off above -- see the module notes; "1" forces it on, "0" off)."""
-    env = os.environ.get("COBALT_SHARED_CU_MASK")
+    env = knob("COBALT_SHARED_CU_MASK")
     if env is not None:
         return world > 1 and env != "0"
     return 1 < world <= MAX_MASKED_RANKS

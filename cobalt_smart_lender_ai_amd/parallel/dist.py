@@ -26,6 +26,7 @@ from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as tdist
+from ..config import knob
 
 
 @dataclass
@@ -151,9 +152,9 @@ def init_from_env(backend: str | None = None, native: bool | None = None, timeou
     # COBALT_DIST_BACKEND / COBALT_DIST_NATIVE: a gloo bootstrap with the native (IPC) communicator lets
     # several ranks share ONE GPU (RCCL refuses two ranks per device) -- the 1-GPU rehearsal of the
     # multi-rank bench (scripts/gpu_bench_multirank.sh)
-    backend = backend or os.environ.get("COBALT_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
-    if native is None and os.environ.get("COBALT_DIST_NATIVE"):
-        native = os.environ["COBALT_DIST_NATIVE"] not in ("0", "")
+    backend = backend or knob("COBALT_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+    if native is None and knob("COBALT_DIST_NATIVE"):
+        native = knob("COBALT_DIST_NATIVE") not in ("0", "")
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -175,7 +176,7 @@ def init_from_env(backend: str | None = None, native: bool | None = None, timeou
 
 
 def _pick_transport(ctx: DistContext, transport: str | None) -> str:
-    t = (transport or os.environ.get("COBALT_DP_TRANSPORT", "auto")).lower()
+    t = (transport or knob("COBALT_DP_TRANSPORT", "auto")).lower()
     if t not in ("auto", "ipc", "rccl"):
         raise ValueError(f"COBALT_DP_TRANSPORT must be auto, ipc or rccl, not {t!r}")
     if t == "auto":
@@ -194,7 +195,7 @@ def create_native_comm(ctx: DistContext, transport: str | None = None) -> tuple[
         try:
             return create_ipc_comm(ctx), "ipc"
         except IpcGroupFailed as e:
-            if transport == "ipc" or os.environ.get("COBALT_DP_TRANSPORT", "auto").lower() == "ipc" \
+            if transport == "ipc" or knob("COBALT_DP_TRANSPORT", "auto").lower() == "ipc" \
                     or ctx.backend != "nccl":
                 raise
             import warnings
@@ -210,12 +211,12 @@ class IpcGroupFailed(RuntimeError):
 def ipc_slot_bytes() -> int:
     """Send-slot capacity of the IPC group (``COBALT_IPC_SLOT_MB``, default 64 MiB: one level of
     histograms is pairs x (cells + 1) x 16 B, 0.7 MB for the 20-feature depth-7 model)."""
-    return int(float(os.environ.get("COBALT_IPC_SLOT_MB", "64")) * (1 << 20))
+    return int(float(knob("COBALT_IPC_SLOT_MB", "64")) * (1 << 20))
 
 
 def ipc_timeout_s() -> float:
     """How long an exchange waits for a peer before the group is marked failed (``COBALT_IPC_TIMEOUT_S``)."""
-    return float(os.environ.get("COBALT_IPC_TIMEOUT_S", "120"))
+    return float(knob("COBALT_IPC_TIMEOUT_S", "120"))
 
 
 def _agree(ctx: DistContext, ok: bool) -> bool:
@@ -242,7 +243,7 @@ def create_ipc_comm(ctx: DistContext) -> int:
     h = ctypes.c_void_p()
     # the connect self-test runs under a short deadline (the ranks enter it together, right after the
     # handle all-gather): a group whose peer mappings do not work fails in seconds, not minutes
-    connect_s = min(ipc_timeout_s(), float(os.environ.get("COBALT_IPC_CONNECT_TIMEOUT_S", "30")))
+    connect_s = min(ipc_timeout_s(), float(knob("COBALT_IPC_CONNECT_TIMEOUT_S", "30")))
     err = ""
     created = False
     try:
@@ -379,7 +380,7 @@ class CollectiveTimeout(RuntimeError):
 
 def collective_timeout_s() -> float:
     """Watchdog deadline for one enqueued training segment (``COBALT_COLLECTIVE_TIMEOUT_S``)."""
-    return float(os.environ.get("COBALT_COLLECTIVE_TIMEOUT_S", "1800"))
+    return float(knob("COBALT_COLLECTIVE_TIMEOUT_S", "1800"))
 
 
 def wait_with_watchdog(done: "callable", *, timeout_s: float, comm_error: "callable | None" = None,

@@ -27,6 +27,7 @@ import tempfile
 import time
 import traceback
 from pathlib import Path
+from ..config import knob
 
 DEFAULT_PARAMS = dict(n_estimators=6, max_depth=7, learning_rate=0.1, gamma=1.0, subsample=0.9, colsample_bytree=0.8,
                       random_state=5, scale_pos_weight=6.0)
@@ -43,8 +44,8 @@ def rank_main(rank: int, world: int, port: int, out_dir: str, rows: int, params:
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank if one_gpu_per_rank else 0), LOCAL_WORLD_SIZE=str(world))
     os.environ.setdefault("OMP_NUM_THREADS", "2")
-    if "{rank}" in os.environ.get("COBALT_STAMPS", ""):  # per-rank stamp files (diagnostics)
-        os.environ["COBALT_STAMPS"] = os.environ["COBALT_STAMPS"].replace("{rank}", str(rank))
+    if "{rank}" in knob("COBALT_STAMPS", ""):  # per-rank stamp files (diagnostics)
+        os.environ["COBALT_STAMPS"] = knob("COBALT_STAMPS").replace("{rank}", str(rank))
     res: dict = {"rank": rank, "world": world, "ok": False}
     t0 = time.monotonic()
     ctx = None
@@ -63,8 +64,8 @@ def rank_main(rank: int, world: int, port: int, out_dir: str, rows: int, params:
         if not one_gpu_per_rank and cumask.want_shared_mask(world):
             # ranks sharing the device each get their own 1/world of the CUs (see parallel/cumask.py)
             stream = cumask.shared_device_stream(rank, world, dev)
-            res["cu_budget"] = int(os.environ["COBALT_CU_BUDGET"])
-            if os.environ.get("COBALT_TEST_PLACEMENT") == "1":
+            res["cu_budget"] = int(knob("COBALT_CU_BUDGET"))
+            if knob("COBALT_TEST_PLACEMENT") == "1":
                 res["placement"] = cumask.placement(stream, dev)
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             if world > 1:
@@ -156,6 +157,9 @@ def run(procs: int, rows: int = 300_000, params: dict | None = None, *, transpor
         f = Path(out) / f"rank{r}.json"
         results.append(json.loads(f.read_text()) if f.exists() else {"rank": r, "ok": False, "error": "no result",
                                                                       "exitcode": ps[r].exitcode})
+    # one progress line per multi-rank run (long GPU test sessions show they are alive)
+    print(f"[dp_check] {procs} rank(s), {rows} rows: ok={[g.get('ok') for g in results]} "
+          f"fit_s={[round(g.get('fit_s', -1), 2) for g in results]} plan={results[0].get('plan')}", flush=True)
     return results
 
 

@@ -121,9 +121,12 @@ def _nn_dataset(df_log: pd.DataFrame, dev: torch.device) -> pd.DataFrame:
         med = prep_ops.median(X)
         ind = prep_ops.fill_with_indicator_(X, list(range(len(with_nulls))), med.cpu().tolist(), True)
         Xh, Ih = X.cpu().numpy(), ind.cpu().numpy().astype(np.int64)
-        for j, c in enumerate(with_nulls):
-            nn[c + "_NA"] = Ih[j]
-            nn[c] = Xh[j]
+        # one concat for the filled columns and the _NA block (per-column inserts fragment the frame:
+        # pandas PerformanceWarning at the reference's ~30 imputed columns)
+        filled = pd.DataFrame({c: Xh[j] for j, c in enumerate(with_nulls)}, index=nn.index)
+        na = pd.DataFrame({c + "_NA": Ih[j] for j, c in enumerate(with_nulls)}, index=nn.index)
+        order = list(nn.columns) + list(na.columns)
+        nn = pd.concat([nn.drop(columns=with_nulls), filled, na], axis=1)[order]
     nn["no_income"] = (nn["annual_inc"].isna() | (nn["annual_inc"] == 0)).astype(int)
     nn["dti_NA"] = df_log["dti"].isna().astype(int)
     dti_med = prep_ops.median(frame.to_device(nn, ["dti"], dev)).cpu().numpy()[0]

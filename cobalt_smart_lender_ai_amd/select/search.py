@@ -25,6 +25,7 @@ from ..metrics.auc import roc_auc
 from ..models import gbdt
 from ..models.booster import Booster
 from .split import stratified_kfold_indices
+from ..config import knob
 
 log = logging.getLogger(__name__)
 
@@ -76,7 +77,7 @@ def _fold_scores(X, y, folds, base: dict, candidates: list[dict], device, stream
 
     tasks = [(i, k) for k in range(len(folds)) for i in range(len(candidates))]
     dev = bds[0].device if bds else torch.device("cpu")
-    n_streams = streams if streams is not None else int(os.environ.get("COBALT_SEARCH_STREAMS", "4"))
+    n_streams = streams if streams is not None else int(knob("COBALT_SEARCH_STREAMS", "4"))
     if dev.type != "cuda" or n_streams <= 1:
         for i, k in tasks:
             fit(i, k)

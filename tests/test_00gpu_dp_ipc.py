@@ -1,5 +1,5 @@
 """Data parallelism across PROCESSES on one GPU (the multi-rank configuration a 1-GPU box can run):
-2 and 3 ranks share cuda:0, bootstrap over gloo and all-reduce their per-level histograms through the
+2 to 8 ranks share cuda:0, bootstrap over gloo and all-reduce their per-level histograms through the
 IPC one-shot group (csrc/ipccomm.hip; the exchange fused into k_eval or as its own kernel). The model
 must equal the 1-process fit byte for byte, and a
 rank that dies mid-fit must make its peer fail fast through the group's deadline + the watchdog's
@@ -23,6 +23,17 @@ def _check_clean(parent_initialised):
         pytest.skip("HIP already initialised in this process; run this file on its own")
 
 
+def _assert_plan(g, fused, own_level, eval_block_levels, overflow=None):
+    """The launch plan a rank reports (csrc/gbdt.hip cobalt_gbdt_plan) -- so a test states which exchange
+    and evaluation form it exercised instead of assuming it."""
+    plan = g["plan"]
+    assert plan["ipc_fused"] is fused, plan
+    assert plan["own_level"] == own_level, plan
+    assert plan["eval_block_levels"] == eval_block_levels, plan
+    if overflow is not None:
+        assert plan["eval_block_overflow_levels"] == overflow, plan
+
+
 @pytest.mark.timeout(900)
 def test_ipc_data_parallel_processes_equal_single_process():
     from cobalt_smart_lender_ai_amd.parallel import dp_check
@@ -30,38 +41,90 @@ def test_ipc_data_parallel_processes_equal_single_process():
     _check_clean(torch.cuda.is_initialized())
     ref = dp_check.run(1, ROWS)[0]
     assert ref["ok"], ref
-    # the exchange fused into the split evaluation (default: k_eval + k_partition) with 2 to 5 ranks
-    # -- ipc_sum_cells<5> --, and the separate exchange kernel (COBALT_IPC_FUSED=0: the fused evaluation +
-    # partition pass k_eval_part<.., kDP> over the all-reduced histograms). The ranks share the device through disjoint CU masks
-    # (parallel/cumask.py); 8 ranks: test_ipc_eight_ranks_share_one_gpu
-    # node ownership (the default over the fused exchange: levels 4-6 of these depth-7 trees, owners by
-    # subtree) and every rank evaluating every node (COBALT_DP_OWNER=0); a depth-3 fit owns from the
-    # first level with a node per rank
+    # Depth-7 trees. The fused exchange (k_eval_part's evaluator blocks publish, wait and sum the ranks'
+    # cells themselves) needs the deepest level's 64 evaluator blocks resident on the rank's CU share:
+    # 2-4 masked ranks (128 / 85 / 64 CUs) run it, with node ownership from level 4 (D - 3); 5 ranks
+    # (51 CUs) fall back to the separate exchange kernel + k_eval_part<.., 1> over the all-reduced sums
+    # (the fused form at 5-8 ranks: test_ipc_fused_exchange_five_to_eight_ranks, depth 6).
+    # COBALT_DP_OWNER=0: every rank evaluates every node; COBALT_IPC_FUSED=0: the separate exchange.
     for procs, env in ((2, None), (3, None), (4, None), (5, None), (3, {"COBALT_DP_OWNER": "0"}),
                        (2, {"COBALT_IPC_FUSED": "0"}), (4, {"COBALT_IPC_FUSED": "0"})):
         got = dp_check.run(procs, ROWS, timeout_s=400, env=env)
+        fused = procs <= 4 and not (env and env.get("COBALT_IPC_FUSED") == "0")
+        owner = fused and not (env and env.get("COBALT_DP_OWNER") == "0")
         for g in got:
             assert g["ok"], (procs, env, g)
             assert g["transport"] == "ipc"
-            # the connect self-test's four exchanges (each slot twice), the exact sketch's three device
+            _assert_plan(g, fused, 4 if owner else -1, list(range(6)) if fused else [])
+            # the connect self-test's four exchanges (each slot twice), the exact sketch's four device
             # all-reduces, the fit scalars' one, one exchange per level per tree and the final
             # replica-digest exchange of the fit's one grow call
-            assert g["ipc_epochs"] == 4 + 3 + 1 + 7 * ref["trees"] + 1
+            assert g["ipc_epochs"] == 4 + 4 + 1 + 7 * ref["trees"] + 1
             assert g["model_sha256"] == ref["model_sha256"], (procs, env, g["rank"])
     shallow = dict(dp_check.DEFAULT_PARAMS, max_depth=3)
     ref3 = dp_check.run(1, ROWS, shallow)[0]
     for procs in (2, 3):
         for g in dp_check.run(procs, ROWS, shallow, timeout_s=400):
             assert g["ok"] and g["model_sha256"] == ref3["model_sha256"], (procs, g)
+            # a depth-3 fit owns from the first level with a node per rank
+            _assert_plan(g, True, 1 if procs == 2 else 2, [0, 1])
+
+
+@pytest.mark.timeout(600)
+def test_ipc_fused_exchange_five_to_eight_ranks():
+    """The code path of an 8-GPU node at 5-8 ranks: the FUSED exchange summing 5-8 ranks' cells
+    (ipc_sum_cells<5..8>, two cells per round trip), node ownership dealing the deep levels over 5-8
+    owners, and k_eval_part's evaluator blocks at every split level. On a shared device the ranks get
+    32-51 CUs each, so the depth-6 trees (32 evaluator blocks at the deepest level) keep the co-residency
+    guard's fused form -- asserted from each rank's launch plan -- and every rank grows the 1-process
+    model byte for byte."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=4, max_depth=6)
+    rows = 240_000
+    ref = dp_check.run(1, rows, params)[0]
+    assert ref["ok"], ref
+    for procs in (5, 6, 8):
+        got = dp_check.run(procs, rows, params, timeout_s=150, env={"COBALT_IPC_TIMEOUT_S": "30"})
+        for g in got:
+            assert g["ok"], (procs, g)
+            assert g["transport"] == "ipc", g
+            # ownership from level 3: the first level with a node per rank (2^3 >= 5..8) and D - 3
+            _assert_plan(g, True, 3, list(range(5)))
+            assert g["ipc_epochs"] == 4 + 1 + 6 * 4 + 1  # (240k rows: the sample sketch, gathered over gloo)
+            assert g["model_sha256"] == ref["model_sha256"], (procs, g["rank"])
+
+
+@pytest.mark.timeout(600)
+def test_ipc_evaluator_blocks_with_more_items_than_cus():
+    """The evaluator-block pass when a level's grid exceeds one block per CU (an 8-GPU node's 1.25M-row
+    shards at the deep levels): the partition items past the resident ones start only as earlier blocks
+    retire, and the items already running spin on their node's decision granule -- progress relies on
+    in-order dispatch putting the evaluators first. 2 masked ranks of 128 CUs on 1M-row shards run
+    levels 0-1 in the one-block-per-CU form and levels 2-5 past it (the plan says which); the model is
+    the 1-process model byte for byte."""
+    from cobalt_smart_lender_ai_amd.parallel import dp_check
+
+    _check_clean(torch.cuda.is_initialized())
+    params = dict(dp_check.DEFAULT_PARAMS, n_estimators=4)
+    rows = 2_000_000
+    ref = dp_check.run(1, rows, params)[0]
+    assert ref["ok"], ref
+    for g in dp_check.run(2, rows, params, timeout_s=300, env={"COBALT_IPC_TIMEOUT_S": "30"}):
+        assert g["ok"], g
+        _assert_plan(g, True, 4, list(range(6)), overflow=[2, 3, 4, 5])
+        assert g["model_sha256"] == ref["model_sha256"], g["rank"]
 
 
 @pytest.mark.timeout(300)
 def test_ipc_eight_ranks_share_one_gpu():
-    """8 processes on one GPU -- the rank count of an 8-GPU node, so the fused exchange sums 8 ranks'
-    cells (ipc_sum_cells<8>) and node ownership deals the deep levels over 8 owners -- each on its own
-    CU-masked 1/8 of the device (parallel/cumask.py, blocked layout): every rank's blocks land in all 8
-    XCCs on exactly its 32 CUs (the placement probe), and every rank grows the 1-process model byte for
-    byte, in seconds (rounds 4-5 before the layout fix: a deadlock masked, 12.6 s per tree time-sliced)."""
+    """8 processes on one GPU, each on its own CU-masked 1/8 of the device (parallel/cumask.py, blocked
+    layout): every rank's blocks land in all 8 XCCs on exactly its 32 CUs (the placement probe), and every
+    rank grows the 1-process model byte for byte, in seconds (rounds 4-5 before the layout fix: a deadlock
+    masked, 12.6 s per tree time-sliced). These depth-7 trees need 64 resident evaluator blocks for the
+    fused exchange and a rank has 32 CUs, so the co-residency guard picks the SEPARATE exchange kernel
+    (asserted); the fused 8-rank exchange runs in test_ipc_fused_exchange_five_to_eight_ranks."""
     import time
 
     from cobalt_smart_lender_ai_amd.parallel import dp_check
@@ -78,6 +141,7 @@ def test_ipc_eight_ranks_share_one_gpu():
         assert g["ok"], g
         assert g["transport"] == "ipc" and g["cu_budget"] == 32, g
         assert g["placement"]["xccs"] == list(range(8)) and g["placement"]["cus"] == 32, g["placement"]
+        _assert_plan(g, False, -1, [])
         assert g["ipc_epochs"] == 4 + 1 + 7 * 3 + 1  # (240k rows: the 2^18-row sample sketch, gathered over gloo)
         assert g["model_sha256"] == ref["model_sha256"], g["rank"]
     assert wall < 60, wall

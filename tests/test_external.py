@@ -81,6 +81,12 @@ def test_external_exact_streaming_gpu_equals_in_core(colsample):
     ps = external.page_stride(X.shape[1])
     mixed = external.train_external(src, params, device="cuda", sample_rate=1.0, device_page_bytes=40_000 * ps)
     _same_trees(mixed, ref)
+    # every page within the HBM budget: the in-core trainer on the streamed-in records, same trees
+    rep = external.ExternalReport()
+    hbm = external.train_external(src, params, device="cuda", sample_rate=1.0, device_page_bytes=90_000 * ps,
+                                  report=rep)
+    assert rep.mode == "in-core" and rep.host_bytes == 0, rep
+    _same_trees(hbm, ref)
 
 
 @pytest.mark.gpu

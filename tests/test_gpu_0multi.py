@@ -28,9 +28,9 @@ def _params(trees=6):
 
 
 def _expected_ipc_epochs(trees: int) -> int:
-    # connect self-test (4) + the exact sketch's three device all-reduces + the fit scalars' one +
+    # connect self-test (4) + the exact sketch's four device all-reduces + the fit scalars' one +
     # one exchange per level per tree + the final replica-digest exchange of the fit's one grow call
-    return 4 + 3 + 1 + 7 * trees + 1
+    return 4 + 4 + 1 + 7 * trees + 1
 
 
 @pytest.mark.timeout(900)

@@ -32,3 +32,27 @@ def test_bench_prints_one_contract_json_line():
     assert d["value"] == pytest.approx(200_000 / (d["ms_per_step"] / 1e3), rel=1e-3)
     assert d["config"]["global_batch"] == 200_000 and d["config"]["parallelism"] == "dp1"
     assert 0.5 < d["auc"] <= 1.0
+
+
+@pytest.mark.timeout(600)
+def test_torchrun_one_rank_equals_plain_bench():
+    """The driver's scaling harness launches bench.py through torchrun (RANK / WORLD_SIZE / MASTER_* from
+    the environment, the distributed context built from them); with one rank that path must print the
+    same contract line as the plain run -- same n_gpus, config and AUC (the fit is deterministic) -- so the
+    N = 1 point of the scaling curve is the headline bench by construction."""
+    from cobalt_smart_lender_ai_amd.parallel.dp_check import free_port
+
+    args = ["bench.py", "--gpus", "1", "--rows", "1000000", "--trees", "20", "--steps", "1", "--warmup", "1",
+            "--test-rows", "100000"]
+    plain = subprocess.run([sys.executable, *args], cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert plain.returncode == 0, plain.stderr[-2000:]
+    tr = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                         "--master-addr", "127.0.0.1", "--master-port", str(free_port()), *args],
+                        cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert tr.returncode == 0, tr.stderr[-2000:]
+    a, b = ([json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")] for r in (plain, tr))
+    assert len(a) == 1 and len(b) == 1, (plain.stdout[-1000:], tr.stdout[-1000:])
+    a, b = a[0], b[0]
+    for k in ("metric", "n_gpus", "config", "auc", "unit", "scaling", "dtype", "sketch_rows", "rows_global"):
+        assert a[k] == b[k], (k, a[k], b[k])
+    assert b["n_gpus"] == 1 and b["config"]["parallelism"] == "dp1" and b["dp_transport"] is None

@@ -53,3 +53,18 @@ def test_knob_lookup_refuses_unregistered_names():
     assert knob("COBALT_IPC_SLOT_MB", "64") is not None
     with pytest.raises(KeyError):
         knob("COBALT_NOT_A_KNOB")
+
+
+def test_python_reads_knobs_through_the_registry():
+    """The Python side reads COBALT_* variables only through config.knob() (which refuses unregistered
+    names); direct os.environ reads remain only for the registry itself (writes -- e.g. cumask setting
+    COBALT_CU_BUDGET for the native side -- are allowed)."""
+    reads = []
+    pat = re.compile(r'os\.environ\.get\("COBALT_|os\.environ\["COBALT_[A-Z0-9_]+"\](?!\s*=[^=])')
+    for p in [*PKG.rglob("*.py"), ROOT / "bench.py", ROOT / "__graft_entry__.py"]:
+        if p.name == "config.py" and p.parent == PKG:
+            continue
+        for i, line in enumerate(p.read_text().splitlines(), 1):
+            if pat.search(line):
+                reads.append(f"{p.relative_to(ROOT)}:{i}")
+    assert not reads, reads

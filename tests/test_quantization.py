@@ -150,3 +150,21 @@ def test_gpu_shape_limits_are_named():
         gbdt.check_gpu_shape(11, 1000)
     with pytest.raises(ValueError, match="int32 row ids"):
         gbdt.check_gpu_shape(7, 1 << 31)
+
+
+def test_train_names_the_limits_before_sketching(monkeypatch):
+    """gbdt.train checks grad_bits / max_depth against the GPU trainer's limits BEFORE the sketch and
+    binning (which run the data-parallel collectives), not only in train_binned after them (advisor
+    finding, round 5). torch.device("cuda", 0) resolves without a GPU; the sketch is stubbed to fail."""
+    import numpy as np
+    import torch
+
+    def no_sketch(*a, **k):
+        raise AssertionError("bin_dataset ran before the shape checks")
+
+    monkeypatch.setattr(gbdt, "bin_dataset", no_sketch)
+    X, y = np.zeros((64, 30), np.float32), np.zeros(64, np.float32)
+    with pytest.raises(ValueError, match="<= 24 features"):
+        gbdt.train(X, y, gbdt.GBDTParams(grad_bits=25), device=torch.device("cuda", 0))
+    with pytest.raises(ValueError, match="max_depth 1-10"):
+        gbdt.train(X[:, :20], y, gbdt.GBDTParams(max_depth=12), device=torch.device("cuda", 0))

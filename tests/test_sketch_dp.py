@@ -81,7 +81,7 @@ def test_global_sample_equals_single_process_sample(world):
         assert wm == float(w.max())
 
 
-def test_bucket_allreduce_counts_offsets_and_range():
+def test_bucket_allreduce_counts_and_range():
     world, F, NB = 4, 3, 17
     gen = torch.Generator().manual_seed(7)
     cnt = [torch.randint(0, 9, (F, NB), generator=gen) for _ in range(world)]
@@ -93,14 +93,40 @@ def test_bucket_allreduce_counts_offsets_and_range():
     vmin[1][0] = -0.0
 
     def fn(dist, r):
-        return sketch._allreduce_buckets(dist, torch.device("cpu"), cnt[r], wts[r], vmin[r], vmax[r])
+        buf_cells = []
+        orig = dist.device_allreduce
+
+        def spy(t, op="sum"):
+            buf_cells.append(t.numel())
+            return orig(t, op)
+
+        dist.device_allreduce = spy
+        return sketch._allreduce_buckets(dist, torch.device("cpu"), cnt[r], wts[r], vmin[r], vmax[r]), buf_cells
 
     outs, calls = _run(world, fn)
     assert calls == 1
     want_min = torch.stack(vmin).amin(0)
     want_max = torch.stack(vmax).amax(0)
-    for r, (cnt_h, w_h, mn, mx, before) in enumerate(outs):
+    for r, ((cnt_h, w_h, mn, mx), cells) in enumerate(outs):
         assert torch.equal(cnt_h, sum(cnt))
         assert torch.equal(w_h, sum(wts))
-        assert torch.equal(before, sum(cnt[:r]) if r else torch.zeros_like(cnt[0]))
         assert torch.equal(mn, want_min) and torch.equal(mx, want_max)
+        # the table is summed in place: F x NB cells (+ weights), only the ranges take rank slots
+        assert cells == [2 * F * NB + world * 2 * F]
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_segment_offsets_are_the_lower_ranks_rows(world):
+    gen = torch.Generator().manual_seed(world)
+    sizes = [torch.randint(0, 50, (11,), generator=gen) for _ in range(world)]
+
+    def fn(dist, r):
+        return sketch._segment_offsets(dist, torch.device("cpu"), sizes[r])
+
+    outs, calls = _run(world, fn)
+    assert calls == 1
+    for r, before in enumerate(outs):
+        assert torch.equal(before, sum(sizes[:r]) if r else torch.zeros_like(sizes[0]))
+    empty, calls = _run(2, lambda dist, r: sketch._segment_offsets(dist, torch.device("cpu"),
+                                                                  torch.zeros(0, dtype=torch.int64)))
+    assert calls == 1 and all(e.numel() == 0 for e in empty)  # issued even without segments
