@@ -2514,6 +2514,7 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
   }
   if (lane == 0) { s_cnt[0][wv] = nl; s_cnt[1][wv] = nv - nl; }
   __syncthreads();
+  stamp_.probe(5);  // the split bins are in: pass 1 done
   if (threadIdx.x == 0) {
     int tl = 0, tr = 0;
     for (int k = 0; k < kPW; ++k) { tl += s_cnt[0][k]; tr += s_cnt[1][k]; }
@@ -2523,6 +2524,7 @@ __global__ __launch_bounds__(1024) void k_eval_part(GbdtDev d, int parity, int64
     s_base[1] = (int32_t)(c >> 32);
   }
   __syncthreads();
+  stamp_.probe(6);  // the item's ranges are claimed
   int bl = s_base[0], br = s_base[1];
   for (int k = 0; k < wv; ++k) { bl += s_cnt[0][k]; br += s_cnt[1][k]; }
   uint32_t pl_ = (uint32_t)(nstart + bl);

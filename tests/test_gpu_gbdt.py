@@ -437,3 +437,42 @@ def test_labels_in_records_equal_label_arrays(monkeypatch):
     wc = gbdt.train(X, y, p, sample_weight=w, device="cpu")
     assert wg.save_raw("ubj") == wc.save_raw("ubj")
     assert wg.save_raw("ubj") != packed.save_raw("ubj")
+
+
+def _max_unique_path(t) -> int:
+    """Longest root -> leaf path of a tree, counted in distinct split features (the TreeSHAP path length)."""
+    best, stack = 0, [(0, frozenset())]
+    while stack:
+        n, feats = stack.pop()
+        if t.left_children[n] == -1:
+            best = max(best, len(feats))
+            continue
+        f = feats | {int(t.split_indices[n])}
+        stack.append((int(t.left_children[n]), f))
+        stack.append((int(t.right_children[n]), f))
+    return best
+
+
+def test_treeshap_reciprocal_drift_at_long_paths():
+    """The GPU TreeSHAP's UNWIND multiplies by reciprocals (csrc/predict.hip kShapInv, 1 / zero) where the
+    host oracle (models/booster.py treeshap_host, Lundberg's Algorithm 2) divides, so the two agree to
+    rounding, not bit for bit. On trees whose paths reach 14+ distinct features (the kernel's limit is 15
+    + the bias element) the drift is measured and pinned: measured on gfx950 (round 6,
+    profiles/round6/shap_drift.txt) max |GPU - host| = 4.1e-15 at max |phi| = 0.51 (8e-15 of the scale),
+    so the bound is 5e-14 x the largest |phi|: a reordering that grows the error cannot pass silently."""
+    rng = np.random.default_rng(3)  # noise labels + min_child_weight 0: trees split down to depth 15
+    Xn = rng.normal(size=(4000, 24)).astype(np.float32)
+    yb = (rng.random(4000) < 0.5).astype(np.float32)
+    p = gbdt.GBDTParams(n_estimators=3, max_depth=15, learning_rate=0.3, min_child_weight=0.0, gamma=0.0)
+    b = gbdt.train(Xn, yb, p, device="cpu")
+    longest = max(_max_unique_path(t) for t in b.trees)
+    assert longest == 15, longest  # the kernel's longest path (kMaxPath 16 elements incl. the bias)
+    Xq = torch.from_numpy(Xn[:32].copy())
+    phi_g = b.shap_values(Xq.cuda()).cpu().numpy()
+    phi_h = B.treeshap_host(b, Xq.numpy())
+    scale = float(np.abs(phi_h).max())
+    d = np.abs(phi_g - phi_h)
+    rel = float((d / np.maximum(np.abs(phi_h), 1e-300))[np.abs(phi_h) > 1e-6 * scale].max())
+    print(f"[shap-drift] longest path {longest} features, max |phi| {scale:.6g}, max abs diff {float(d.max()):.3g}, "
+          f"max rel diff {rel:.3g} (|phi| > 1e-6 max)")
+    assert float(d.max()) <= 5e-14 * scale, (float(d.max()), scale)
