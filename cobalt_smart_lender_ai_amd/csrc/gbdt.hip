@@ -190,7 +190,8 @@ struct GbdtDev {
   const IpcFusedView* ipcv;  // fused IPC exchange: the group's device views (per slot parity) ...
   unsigned ipc_epoch;        // ... and this level's epoch (k_eval only; 0 = hist_b already holds global sums)
   // write-through (sc1) stores of data the NEXT launch reads from other XCDs (COBALT_WT, bit 0: the
-  // per-item histogram slabs, bit 1: the partition's row ids): the lines leave L2 as they are written
+  // per-item histogram slabs, bit 1: the partition's row ids, bit 2: the root pass's (g, h) record
+  // halves): the lines leave L2 as they are written
   // instead of at the kernel-end write-back that the dependent launch waits for
   int32_t wt;
   // binary labels held in the row records (cobalt_gbdt_set_binary_labels): byte 23 of a 32-byte record
@@ -1080,7 +1081,11 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       th += hq;
       rb[u].z = (uint32_t)hq;
       rb[u].w = (uint32_t)(int32_t)gq;
-      reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
+      if (d.wt & 4) {  // write-through (g, h): no dirty record lines left for the kernel-end write-back
+        store_wt(reinterpret_cast<uint64_t*>(d.bins + i * 32 + 24), ((uint64_t)rb[u].w << 32) | rb[u].z, true);
+      } else {
+        reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
+      }
       if (d.ablate != 21) hist_add_rec32<FT4, kWide>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
     }
   }
@@ -2795,7 +2800,10 @@ COBALT_API int cobalt_gbdt_create(const GbdtConfig* cfg, void** out) {
   // write-through slabs always (10M rows: reduce gaps 14.2 -> 12.0 us per tree, fit 243.7 -> 243.2 ms); write-through
   // row ids below 4M rows only (1M: 240.2 -> 237.4 us per tree with both; at 10M the partition itself
   // slows 210 -> 228 us per tree for 10 us of shorter histogram gaps). COBALT_WT overrides.
-  d.wt = knob_int(Knob::WriteThrough, N < 4000000 ? 3 : 1);
+  // (bit 2, the root pass's (g, h): 1.25M rows 77.1 / 77.3 -> 76.4 / 76.6 ms per fit, 10M 233.9 / 233.5 ->
+  // 233.6 / 233.1, same box, profiles/round6/ab_wt_root.txt -- the kernel-end write-back of the dirty record
+  // lines was the 3-4.5 us gap after the root pass)
+  d.wt = knob_int(Knob::WriteThrough, N < 4000000 ? 7 : 5);
   // Data parallel: every rank histograms the child with the smaller GLOBAL hessian (k_eval's choice,
   // identical on all ranks), so the level's all-reduce sums the same child everywhere. On one GPU the
   // locally smaller row count (+2% histogram time with the hessian rule).

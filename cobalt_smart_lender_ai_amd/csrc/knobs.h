@@ -18,7 +18,7 @@ enum class Knob : int {
   EvalPart,      // COBALT_EVAL_PART: the fused evaluation + partition pass (0 off, 1 auto, 2 forced)
   HistPair,      // COBALT_HIST_PAIR: lane-pair record gathers in k_hist (16 < F <= 24)
   MaxCopyShift,  // COBALT_MAX_COPY_SHIFT: log2 of the per-lane histogram copies of a low-cardinality feature
-  WriteThrough,  // COBALT_WT: write-through stores (bit 0 slabs, bit 1 row ids)
+  WriteThrough,  // COBALT_WT: write-through stores (bit 0 slabs, bit 1 row ids, bit 2 root (g, h))
   IpcFused,      // COBALT_IPC_FUSED: the IPC exchange fused into the split evaluation (0: separate kernel)
   DpOwner,       // COBALT_DP_OWNER: node ownership on the deep levels over the fused IPC exchange
   CuBudget,      // COBALT_CU_BUDGET: CUs of this rank's CU-masked stream (parallel/cumask.py sets it)

@@ -56,3 +56,17 @@ def test_torchrun_one_rank_equals_plain_bench():
     for k in ("metric", "n_gpus", "config", "auc", "unit", "scaling", "dtype", "sketch_rows", "rows_global"):
         assert a[k] == b[k], (k, a[k], b[k])
     assert b["n_gpus"] == 1 and b["config"]["parallelism"] == "dp1" and b["dp_transport"] is None
+
+
+@pytest.mark.timeout(300)
+def test_bench_auc_matches_the_pinned_host_oracle():
+    """bench.py at 100k rows: the GPU fit's test AUC equals the host trainer's pinned one (the same trees;
+    the synthetic rows come from the device generator here, the host one there) and the JSON names the
+    reference's source (bench.py PARITY_AUC)."""
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--rows", "100000", "--test-rows", "100000",
+                          "--steps", "1", "--warmup", "0"], cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert "host trainer" in d["auc_parity_source"], d
+    assert abs(d["auc"] - d["auc_parity_ref"]) <= 2e-5, d
+    assert d["auc_parity_ok"] is True
