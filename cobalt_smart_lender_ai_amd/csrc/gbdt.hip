@@ -199,6 +199,13 @@ struct GbdtDev {
   // so the gradient pass reads neither the label nor the weight array
   int32_t ylab;
   float spw;
+  // label bit (F <= 20 with ylab): the 0/1 label is bit 31 of the record's h word (word 6, bytes 24-27; h_q <
+  // 2^26 never reaches it -- the histogram passes mask it off) instead of byte 23, which frees record word 5
+  // (bytes 20-23) for the row's margin: mrec = the fused root pass keeps every row's fp32 margin THERE
+  // (copied in at the start of a grow call, out at its end), so it reads and writes the record it streams
+  // anyway instead of a separate margin array -- 64 instead of 72 bytes per row per tree
+  int32_t lab31;
+  int32_t mrec;
   // In-flight replica check (data parallel only; dig == nullptr on one GPU). Every node decision a
   // tree finalises adds a 32-bit hash to dig[tree & 1] (eval_finalize). At level 0 of the next tree
   // the reduce writes the previous tree's sum into an extra int64 cell right after the root slot
@@ -491,7 +498,8 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
     }
     const double mm = (double)mf;
     const double p = 1.0 / (1.0 + exp(-mm));
-    const float yf = d.ylab ? (float)(rb.y >> 24) : d.label[i];
+    const uint32_t lbit = rb.z & 0x80000000u;
+    const float yf = d.ylab ? (d.lab31 ? (lbit ? 1.0f : 0.0f) : (float)(rb.y >> 24)) : d.label[i];
     const double y = (double)yf;
     const double w = d.ylab ? (double)(yf != 0.0f ? d.spw : 1.0f) : (double)d.weight[i];
     double g = (p - y) * w;
@@ -503,7 +511,7 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
     int64_t gq, hq;
     quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq, d.wide != 0);
     if (rec32) {
-      rb.z = (uint32_t)hq;
+      rb.z = (uint32_t)hq | (d.lab31 ? lbit : 0u);
       rb.w = (uint32_t)(int32_t)gq;
       rec[1] = rb;
     } else {
@@ -511,6 +519,16 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
           ((uint64_t)(uint32_t)(int32_t)gq << 32) | (uint64_t)(uint32_t)hq;
     }
   }
+}
+
+// GbdtDev::mrec: the margins into record word 5 at the start of a grow call, and back at its end
+__global__ __launch_bounds__(256) void k_margin_in(uint8_t* bins, const float* margin, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<float*>(bins + i * 32)[5] = margin[i];
+}
+__global__ __launch_bounds__(256) void k_margin_out(const uint8_t* bins, float* margin, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    margin[i] = reinterpret_cast<const float*>(bins + i * 32)[5];
 }
 
 // Add tree `t`'s leaf values to the margins (used after the last boosting round).
@@ -871,8 +889,9 @@ template <int FT4, bool kWide = false>
 __device__ __forceinline__ void hist_add_rec32(uint64_t* s_hist, const HistLanes& hl, const uint4& a,
                                                const uint4& b) {
   static_assert(FT4 % 4 == 0 && FT4 > 0 && FT4 <= 24, "32-byte records hold <= 24 bins");
-  const uint64_t gp = ((uint64_t)b.w << 32) | b.z;
-  const uint64_t gw = (uint64_t)(int64_t)(int32_t)b.w, hw = (uint64_t)b.z;
+  const uint32_t hz = b.z & 0x7FFFFFFFu;  // (bit 31: the label, lab31 records)
+  const uint64_t gp = ((uint64_t)b.w << 32) | hz;
+  const uint64_t gw = (uint64_t)(int64_t)(int32_t)b.w, hw = (uint64_t)hz;
   char* base = reinterpret_cast<char*>(s_hist);
 #pragma unroll
   for (int fl = 0; fl < FT4; ++fl) {
@@ -1034,7 +1053,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       const uint4* rec = reinterpret_cast<const uint4*>(d.bins + ii * 32);
       ra[u] = rec[0];
       rb[u] = rec[1];
-      mf[u] = d.margin[ii];
+      mf[u] = d.mrec ? 0.0f : d.margin[ii];
       yl[u] = 0.0f;
       wt[u] = 0.0f;
       if (!d.ylab) {
@@ -1046,6 +1065,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + (int64_t)u * B;
       if (i >= end) continue;
+      if (d.mrec) mf[u] = __int_as_float((int)rb[u].y);  // the margin in record word 5
       if (apply_tree >= 0 && d.ablate != 22) {  // walk the previous tree with the record held in registers
         int nidx = 0;
         uint32_t m = s_meta[0];
@@ -1059,12 +1079,13 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
           m = s_meta[nidx];
         }
         mf[u] += s_leaf[nidx];
-        d.margin[i] = mf[u];
+        if (!d.mrec) d.margin[i] = mf[u];
       }
       const double mm = (double)mf[u];
       const double p = d.ablate == 20 ? 0.5 + 0.01 * mm : 1.0 / (1.0 + exp(-mm));  // (20: timing-only, no exp)
+      const uint32_t lbit = rb[u].z & 0x80000000u;  // (lab31: the label bit rides in the h word)
       if (d.ylab) {
-        yl[u] = (float)(rb[u].y >> 24);
+        yl[u] = d.lab31 ? (lbit ? 1.0f : 0.0f) : (float)(rb[u].y >> 24);
         wt[u] = yl[u] != 0.0f ? d.spw : 1.0f;
       }
       const double y = (double)yl[u];
@@ -1079,13 +1100,16 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       quantize_gh(g, h, d.gscale, d.hscale, dkey, d.row_offset + i, gq, hq, kWide);
       tg += gq;
       th += hq;
-      rb[u].z = (uint32_t)hq;
+      rb[u].y = d.mrec ? (uint32_t)__float_as_int(mf[u]) : rb[u].y;
+      rb[u].z = (uint32_t)hq | (d.lab31 ? lbit : 0u);
       rb[u].w = (uint32_t)(int32_t)gq;
-      if (d.wt & 4) {  // write-through (g, h): no dirty record lines left for the kernel-end write-back
-        store_wt(reinterpret_cast<uint64_t*>(d.bins + i * 32 + 24), ((uint64_t)rb[u].w << 32) | rb[u].z, true);
-      } else {
+      // (g, h) [+ the margin]: one plain 16-byte store when the margin rides along (write-through of the 16
+      // bytes measured slower: 10M 247.5 vs 237.8 ms); else write-through of the 8-byte (g, h) (COBALT_WT bit
+      // 2): no dirty record lines left for the kernel-end write-back
+      if (!d.mrec && (d.wt & 4))
+        store_wt(reinterpret_cast<uint64_t*>(d.bins + i * 32) + 3, ((uint64_t)rb[u].w << 32) | rb[u].z, true);
+      else
         reinterpret_cast<uint4*>(d.bins + i * 32)[1] = rb[u];
-      }
       if (d.ablate != 21) hist_add_rec32<FT4, kWide>(s_hist, hl, ra[u], rb[u]);  // (21: timing-only, no LDS atomics)
     }
   }
@@ -1171,7 +1195,7 @@ __device__ __forceinline__ void hist_rows_pair(const GbdtDev& d, uint64_t* s_his
         v[j] = h ? l1 : own;
       }
       const bool ok = r[u] >= 0;
-      const uint32_t hq = ok ? (h ? x[u].z : pz) : 0u, gq = ok ? (h ? x[u].w : pw) : 0u;
+      const uint32_t hq = ok ? ((h ? x[u].z : pz) & 0x7FFFFFFFu) : 0u, gq = ok ? (h ? x[u].w : pw) : 0u;
       const uint64_t gp = ((uint64_t)gq << 32) | hq;
       if (h == 0) {
         tg += (int64_t)(int32_t)gq;
@@ -1283,7 +1307,7 @@ __global__ __launch_bounds__(kWide ? kHistThreadsWide : kHistThreads) __attribut
       for (int u = 0; u < U; ++u) {
         if (r[u] < 0) { b2[u].z = 0u; b2[u].w = 0u; }
         tg += (int64_t)(int32_t)b2[u].w;
-        th += (int64_t)b2[u].z;
+        th += (int64_t)(b2[u].z & 0x7FFFFFFFu);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) hist_add_rec32<FT4, kWide>(s_hist, hl, a[u], b2[u]);
@@ -1321,7 +1345,7 @@ __global__ __launch_bounds__(kWide ? kHistThreadsWide : kHistThreads) __attribut
         const uint4* t = reinterpret_cast<const uint4*>(rec + f0);
         a[u] = lo_ok ? t[0] : make_uint4(0, 0, 0, 0);
         b[u] = hi_ok ? t[1] : make_uint4(0, 0, 0, 0);
-        gp[u] = *reinterpret_cast<const uint64_t*>(rec + d.goff);
+        gp[u] = *reinterpret_cast<const uint64_t*>(rec + d.goff) & ~0x80000000ull;  // (bit 31 of h: lab31)
       }
 #pragma unroll
       for (int u = 0; u < UW; ++u) {
@@ -2913,6 +2937,7 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   c->d.label = label;
   c->d.weight = weight;
   c->d.ylab = 0;
+  c->d.lab31 = 0;
   c->d.margin = margin;
   c->d.fmask = fmask;
   // Histogram LDS layout from the per-feature bin counts (one small synchronous copy per fit).
@@ -3026,6 +3051,16 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const int ft4 = hist_ft4(d);
   const bool fuse_root = !sampled && ft4 > 0 && ftiles == 1 && (d.ablate == 0 || d.ablate >= 10);
   if (d.wide && sampled) return -15;  // (the sampled pages carry 17-bit pairs)
+  // margins in the row records for this call (GbdtDev::mrec) from 4M rows: 10M 231.9 / 234.2 vs 235.9 / 235.9
+  // ms per fit; at 1.25M the copy-in / copy-out launches and the lost write-through of (g, h) cost more
+  // (78.2 / 78.9 vs 77.2 / 77.0; profiles/round6/ab_margin_in_record.txt). COBALT_MARGIN_IN_RECORD: 0 off,
+  // 2 at any size
+  static const int env_mrec = knob_int(Knob::MarginInRecord, 1);
+  d.mrec = (env_mrec != 0 && d.lab31 && fuse_root && d.n > 0 && (env_mrec == 2 || d.n >= 4000000)) ? 1 : 0;
+  if (d.mrec) {
+    hipLaunchKernelGGL(k_margin_in, dim3(std::min(ceil_div(d.n, 256), 4096)), dim3(256), 0, stream, d.bins, d.margin, d.n);
+    CK_LAUNCH();
+  }
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
   static const int env_fg = knob_int(Knob::EvalFg, -1);
@@ -3272,6 +3307,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
     const int last = c->grown - 1;
     CK(hipMemcpyAsync(d.trees + (size_t)last * c->max_nodes, d.nodes_buf[last & 1], c->max_nodes * sizeof(Node),
                       hipMemcpyDeviceToDevice, stream));
+  }
+  if (d.mrec) {  // the margins back into the array (the last tree's leaves follow, below)
+    hipLaunchKernelGGL(k_margin_out, dim3(std::min(ceil_div(d.n, 256), 4096)), dim3(256), 0, stream, d.bins, d.margin,
+                       d.n);
+    CK_LAUNCH();
+    d.mrec = 0;
   }
   // bring the margins up to date with the last grown tree
   if (c->applied < c->grown) {
@@ -3588,16 +3629,27 @@ __global__ __launch_bounds__(256) void k_put_label(uint8_t* bins, const float* l
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     bins[i * 32 + 23] = label[i] != 0.0f ? 1 : 0;
 }
+// F <= 20 (GbdtDev::lab31): the label as bit 31 of the h word (word 6; the root pass rewrites h under it)
+__global__ __launch_bounds__(256) void k_put_label31(uint8_t* bins, const float* label, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint32_t*>(bins + i * 32)[6] = label[i] != 0.0f ? 0x80000000u : 0u;
+}
 
 COBALT_API int cobalt_gbdt_set_binary_labels(void* h, float spw, hipStream_t stream) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
   GbdtDev& d = c->d;
   if (!d.bins || !d.label || d.stride != 32 || d.F > 23) return -13;
+  // F <= 20: the label bit in the h word, which frees bytes 20-23 for the margin (GbdtDev::lab31 / mrec)
+  const bool l31 = d.F <= 20;
   if (d.n > 0) {
     const int grid = std::min(ceil_div(d.n, 256), 4096);
-    hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
+    if (l31)
+      hipLaunchKernelGGL(k_put_label31, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
+    else
+      hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
     CK(hipGetLastError());
   }
+  d.lab31 = l31 ? 1 : 0;
   d.ylab = 1;
   d.spw = spw;
   return 0;

@@ -25,6 +25,7 @@ enum class Knob : int {
   BinScalar,     // COBALT_BIN_SCALAR: the generic binning kernel for 32-byte records too (tests)
   PredWalk,      // COBALT_PRED_WALK: trees walked at once per predictor thread (2 / 4 / 8)
   EvalBlocks,    // COBALT_EVAL_BLOCKS: the evaluator-block fused pass over the fused IPC exchange
+  MarginInRecord,  // COBALT_MARGIN_IN_RECORD: the root pass keeps the margins in the row records (F <= 20)
   Count
 };
 

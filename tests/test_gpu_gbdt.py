@@ -114,8 +114,10 @@ def test_gpu_histogram_variants_identical_to_host_oracle(env, monkeypatch):
 @pytest.mark.timeout(600)
 def test_gpu_large_n_kernel_shapes_identical_to_host_oracle():
     """Above 4M rows the trainer switches kernel shapes (8192-row partition items in k_partition<16, 8>,
-    8192-row root items, 16384-row work chunks -- the headline 10M-row configuration). Two depth-7 trees on 4.3M rows
-    must equal the NumPy oracle's byte for byte, and the training margins must equal the predictor's."""
+    8192-row root items, 16384-row work chunks -- the headline 10M-row configuration) and keeps the margins
+    in the row records (GbdtDev::mrec: label bit in the h word, margin copied in / out per grow call). Two
+    depth-7 trees on 4.3M rows must equal the NumPy oracle's byte for byte, and the training margins must
+    equal the predictor's."""
     n = 4_300_000
     X, y = synth.make_lendingclub(n, seed=31)
     spw = float((y == 0).sum() / (y == 1).sum())
