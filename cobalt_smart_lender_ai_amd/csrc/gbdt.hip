@@ -521,10 +521,25 @@ __global__ __launch_bounds__(256) void k_grad(GbdtDev d, int tree, int apply_tre
   }
 }
 
+// F <= 20 (GbdtDev::lab31): the label as bit 31 of the h word (word 6; the root pass rewrites h under it)
+__global__ __launch_bounds__(256) void k_put_label31(uint8_t* bins, const float* label, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint32_t*>(bins + i * 32)[6] = label[i] != 0.0f ? 0x80000000u : 0u;
+}
 // GbdtDev::mrec: the margins into record word 5 at the start of a grow call, and back at its end
 __global__ __launch_bounds__(256) void k_margin_in(uint8_t* bins, const float* margin, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     reinterpret_cast<float*>(bins + i * 32)[5] = margin[i];
+}
+// ... together with the label bit at a fit's first grow call (words 5 and 6 of a record, one pass instead of
+// two over the records; the root pass rewrites h under the bit)
+__global__ __launch_bounds__(256) void k_margin_label_in(uint8_t* bins, const float* margin, const float* label,
+                                                         int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(bins + i * 32);
+    w[5] = (uint32_t)__float_as_int(margin[i]);
+    w[6] = label[i] != 0.0f ? 0x80000000u : 0u;
+  }
 }
 __global__ __launch_bounds__(256) void k_margin_out(const uint8_t* bins, float* margin, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -2594,6 +2609,7 @@ struct GbdtCtx {
   int fit_first = 0;            // first tree this context grows in the current fit (no replica check)
   int fault_tree = -1;          // fault injection: tree whose root totals are perturbed on this rank
   uint32_t dec_tag = 0;         // k_eval_part<.., 2>: the launch tag of the decision granules (d.dec)
+  bool label_pending = false;   // lab31 labels set, to be written into the records by the next grow call
   // the last grow call's plan (cobalt_gbdt_plan): fused IPC exchange, ownership level, wide gradients,
   // resident blocks of the fused k_eval, levels run by the fused evaluation + partition pass (and of them
   // the evaluator-block levels, and those whose grid exceeds one block per CU)
@@ -2938,6 +2954,7 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
   c->d.weight = weight;
   c->d.ylab = 0;
   c->d.lab31 = 0;
+  c->label_pending = false;
   c->d.margin = margin;
   c->d.fmask = fmask;
   // Histogram LDS layout from the per-feature bin counts (one small synchronous copy per fit).
@@ -3057,9 +3074,16 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   // 2 at any size
   static const int env_mrec = knob_int(Knob::MarginInRecord, 1);
   d.mrec = (env_mrec != 0 && d.lab31 && fuse_root && d.n > 0 && (env_mrec == 2 || d.n >= 4000000)) ? 1 : 0;
-  if (d.mrec) {
-    hipLaunchKernelGGL(k_margin_in, dim3(std::min(ceil_div(d.n, 256), 4096)), dim3(256), 0, stream, d.bins, d.margin, d.n);
-    CK_LAUNCH();
+  {
+    const dim3 g1(std::max(1, std::min(ceil_div(d.n, 256), 4096)));
+    if (c->label_pending && d.mrec)
+      hipLaunchKernelGGL(k_margin_label_in, g1, dim3(256), 0, stream, d.bins, d.margin, d.label, d.n);
+    else if (c->label_pending)
+      hipLaunchKernelGGL(k_put_label31, g1, dim3(256), 0, stream, d.bins, d.label, d.n);
+    else if (d.mrec)
+      hipLaunchKernelGGL(k_margin_in, g1, dim3(256), 0, stream, d.bins, d.margin, d.n);
+    if (c->label_pending || d.mrec) CK_LAUNCH();
+    c->label_pending = false;
   }
   // grouped split evaluation: features per block (0 = one 1024-thread block per node); at most 64
   // groups per node, at most 32 features per group (16 waves x 2). COBALT_EVAL_FG overrides.
@@ -3629,11 +3653,6 @@ __global__ __launch_bounds__(256) void k_put_label(uint8_t* bins, const float* l
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     bins[i * 32 + 23] = label[i] != 0.0f ? 1 : 0;
 }
-// F <= 20 (GbdtDev::lab31): the label as bit 31 of the h word (word 6; the root pass rewrites h under it)
-__global__ __launch_bounds__(256) void k_put_label31(uint8_t* bins, const float* label, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    reinterpret_cast<uint32_t*>(bins + i * 32)[6] = label[i] != 0.0f ? 0x80000000u : 0u;
-}
 
 COBALT_API int cobalt_gbdt_set_binary_labels(void* h, float spw, hipStream_t stream) {
   GbdtCtx* c = static_cast<GbdtCtx*>(h);
@@ -3641,12 +3660,11 @@ COBALT_API int cobalt_gbdt_set_binary_labels(void* h, float spw, hipStream_t str
   if (!d.bins || !d.label || d.stride != 32 || d.F > 23) return -13;
   // F <= 20: the label bit in the h word, which frees bytes 20-23 for the margin (GbdtDev::lab31 / mrec)
   const bool l31 = d.F <= 20;
-  if (d.n > 0) {
+  // (F <= 20: written by the next grow call, together with the margins when they go to the records)
+  c->label_pending = l31 && d.n > 0;
+  if (d.n > 0 && !l31) {
     const int grid = std::min(ceil_div(d.n, 256), 4096);
-    if (l31)
-      hipLaunchKernelGGL(k_put_label31, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
-    else
-      hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
+    hipLaunchKernelGGL(k_put_label, dim3(grid), dim3(256), 0, stream, d.bins, d.label, d.n);
     CK(hipGetLastError());
   }
   d.lab31 = l31 ? 1 : 0;

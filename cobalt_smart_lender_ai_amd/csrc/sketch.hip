@@ -50,11 +50,14 @@ __device__ __forceinline__ void sk_load_bounds(float* s_u, const float* __restri
 // Pass 1. grid = (blocks per feature, F); X feature-major [F][ldx]; w: int32 quantised weights or
 // nullptr (unit). cnt_slab [gridDim.x][F][kSkBuckets] u32 row counts; w_slab (kW) the same shape in
 // u64 weight sums; bmm [gridDim.x][F][2] the block's min / max valid value.
-template <bool kW>
+// kIds: every value's bucket also goes to bid [F][ldx] (u16, 0xFFFF = missing), so pass 2 (k_sk_gather<..,
+// true>) reads 2 bytes per value instead of repeating the 12-step search (the in-core sketch, one chunk).
+template <bool kW, bool kIds>
 __global__ __launch_bounds__(kSkThreads) void k_sk_hist(const float* __restrict__ X, int64_t n, int64_t ldx,
                                                        const int32_t* __restrict__ w, const float* __restrict__ bounds,
                                                        const int32_t* __restrict__ nbound, uint32_t* __restrict__ cnt_slab,
-                                                       unsigned long long* __restrict__ w_slab, float* __restrict__ bmm) {
+                                                       unsigned long long* __restrict__ w_slab, float* __restrict__ bmm,
+                                                       uint16_t* __restrict__ bid) {
   __shared__ float s_u[kSkMaxBounds];
   __shared__ uint32_t s_c[kSkBuckets];
   __shared__ unsigned long long s_w[kW ? kSkBuckets : 1];
@@ -84,6 +87,7 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_hist(const float* __restrict_
       b = sk_bucket(s_u, m, v);
       wi = kW ? (int64_t)w[r] : 1;
     }
+    if (kIds && r < r1) bid[(int64_t)f * ldx + r] = b >= 0 ? (uint16_t)b : (uint16_t)0xFFFFu;
     // Low-cardinality features put most lanes of a wave on one or two buckets: 64 same-address LDS
     // atomics serialise. Two leader rounds add the wave's most common buckets once (popcount /
     // wave sum), the remaining lanes add their own.
@@ -140,12 +144,15 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_hist(const float* __restrict_
 // per-block bucket counts, plus the segment's offset -- the same row partition as k_sk_hist, so one
 // walk over the rows suffices). Writes candidate values (and int32 weights) into their segments
 // through LDS cursors.
-template <bool kW>
+// kIds: the buckets come from pass 1's bid table (no boundary search; a value is loaded only when its
+// bucket is selected).
+template <bool kW, bool kIds>
 __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restrict__ X, int64_t n, int64_t ldx,
                                                          const int32_t* __restrict__ w, const float* __restrict__ bounds,
                                                          const int32_t* __restrict__ nbound,
                                                          const int32_t* __restrict__ slot, const int64_t* __restrict__ blk_off,
-                                                         int nseg, float* __restrict__ cval, int32_t* __restrict__ cw) {
+                                                         int nseg, float* __restrict__ cval, int32_t* __restrict__ cw,
+                                                         const uint16_t* __restrict__ bid) {
   __shared__ float s_u[kSkMaxBounds];
   __shared__ int32_t s_slot[kSkBuckets];
   // per selected bucket: this block's rows written so far (relative to the block's int64 segment offset
@@ -153,7 +160,7 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
   // rows, while one block's count always fits 32 bits)
   __shared__ uint32_t s_cur[kSkBuckets];
   const int f = blockIdx.y;
-  sk_load_bounds(s_u, bounds, f);
+  if (!kIds) sk_load_bounds(s_u, bounds, f);
   const int64_t* bo = blk_off + (int64_t)blockIdx.x * nseg;
   for (int i = threadIdx.x; i < kSkBuckets; i += blockDim.x) {
     s_slot[i] = slot[(int64_t)f * kSkBuckets + i];
@@ -165,9 +172,18 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
   const int64_t r0 = (int64_t)blockIdx.x * per, r1 = min(n, r0 + per);
   const float* col = X + (int64_t)f * ldx;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-    const float v = canon(col[r]);
-    if (v != v) continue;
-    const int b = sk_bucket(s_u, m, v);
+    int b;
+    float v;
+    if (kIds) {
+      const uint32_t bb = bid[(int64_t)f * ldx + r];
+      if (bb == 0xFFFFu || s_slot[bb] < 0) continue;
+      b = (int)bb;
+      v = canon(col[r]);
+    } else {
+      v = canon(col[r]);
+      if (v != v) continue;
+      b = sk_bucket(s_u, m, v);
+    }
     const int sg = s_slot[b];
     if (sg < 0) continue;
     const int64_t pos = bo[sg] + (int64_t)atomicAdd(&s_cur[b], 1u);
@@ -376,32 +392,39 @@ __global__ __launch_bounds__(1024) void k_sk_exact(const int64_t* __restrict__ c
 
 }  // namespace
 
+// bid: nullptr, or [F][ldx] u16 -- every value's bucket for a later cobalt_sk_gather(.., bid) of the same rows
 COBALT_API int cobalt_sk_hist(const float* X, int64_t n, int64_t ldx, int F, const int32_t* w, const float* bounds,
                               const int32_t* nbound, int nblk, uint32_t* cnt_slab, void* w_slab, float* bmm,
-                              hipStream_t stream) {
+                              uint16_t* bid, hipStream_t stream) {
   if (F <= 0 || nblk <= 0) return -3;
   const dim3 grid(nblk, F);
-  if (w)
-    hipLaunchKernelGGL(k_sk_hist<true>, grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, cnt_slab,
-                       static_cast<unsigned long long*>(w_slab), bmm);
-  else
-    hipLaunchKernelGGL(k_sk_hist<false>, grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, cnt_slab,
-                       static_cast<unsigned long long*>(w_slab), bmm);
+  auto* ws = static_cast<unsigned long long*>(w_slab);
+#define SK_HIST(KW, KI) \
+  hipLaunchKernelGGL((k_sk_hist<KW, KI>), grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, cnt_slab, ws, bmm, bid)
+  if (w) {
+    if (bid) SK_HIST(true, true); else SK_HIST(true, false);
+  } else {
+    if (bid) SK_HIST(false, true); else SK_HIST(false, false);
+  }
+#undef SK_HIST
   CK_LAUNCH();
   return 0;
 }
 
 COBALT_API int cobalt_sk_gather(const float* X, int64_t n, int64_t ldx, int F, const int32_t* w, const float* bounds,
                                 const int32_t* nbound, const int32_t* slot, const int64_t* blk_off, int nseg,
-                                float* cval, int32_t* cw, int nblk, hipStream_t stream) {
+                                float* cval, int32_t* cw, int nblk, const uint16_t* bid, hipStream_t stream) {
   if (F <= 0 || nblk <= 0 || nseg <= 0) return -3;
   const dim3 grid(nblk, F);
-  if (w)
-    hipLaunchKernelGGL(k_sk_gather<true>, grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, slot,
-                       blk_off, nseg, cval, cw);
-  else
-    hipLaunchKernelGGL(k_sk_gather<false>, grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, slot,
-                       blk_off, nseg, cval, cw);
+#define SK_GATHER(KW, KI) \
+  hipLaunchKernelGGL((k_sk_gather<KW, KI>), grid, dim3(kSkThreads), 0, stream, X, n, ldx, w, bounds, nbound, slot, blk_off, \
+                     nseg, cval, cw, bid)
+  if (w) {
+    if (bid) SK_GATHER(true, true); else SK_GATHER(true, false);
+  } else {
+    if (bid) SK_GATHER(false, true); else SK_GATHER(false, false);
+  }
+#undef SK_GATHER
   CK_LAUNCH();
   return 0;
 }

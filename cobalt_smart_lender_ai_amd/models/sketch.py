@@ -376,9 +376,9 @@ def _sk_lib():
 
         V, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
         lib.cobalt_sk_hist.restype = I
-        lib.cobalt_sk_hist.argtypes = [V, I64, I64, I, V, V, V, I, V, V, V, V]
+        lib.cobalt_sk_hist.argtypes = [V, I64, I64, I, V, V, V, I, V, V, V, V, V]
         lib.cobalt_sk_gather.restype = I
-        lib.cobalt_sk_gather.argtypes = [V, I64, I64, I, V, V, V, V, V, I, V, V, I, V]
+        lib.cobalt_sk_gather.argtypes = [V, I64, I64, I, V, V, V, V, V, I, V, V, I, V, V]
         lib.cobalt_sk_select.restype = I
         lib.cobalt_sk_select.argtypes = [V, V, V, I, V, V, V, V, V, V, V, V, V]
         lib.cobalt_sk_transpose.restype = I
@@ -601,7 +601,7 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
     mark("bounds")
 
     # 2. bucket histograms (row counts; weight sums when weighted) + min / max valid value, per chunk
-    def chunk_hist(XT, n, wq):
+    def chunk_hist(XT, n, wq, bid=None):
         nblk = max(1, min(64, -(-n // 65536)))
         cnt_slab = torch.zeros((nblk, F, NB), dtype=torch.int32, device=dev)
         w_slab = torch.zeros((nblk, F, NB), dtype=torch.int64, device=dev) if wq is not None else None
@@ -610,7 +610,7 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
         bmm[:, :, 1] = float("-inf")
         if n:
             rc = lib.cobalt_sk_hist(XT.data_ptr(), n, n, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), nblk,
-                                    cnt_slab.data_ptr(), _ptr(w_slab), bmm.data_ptr(), stream)
+                                    cnt_slab.data_ptr(), _ptr(w_slab), bmm.data_ptr(), _ptr(bid), stream)
             _native.check(rc, "cobalt_sk_hist")
         return nblk, cnt_slab, w_slab, bmm
 
@@ -623,14 +623,17 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
         Xc = Xc.to(torch.float32)
         XT = _sk_transpose(lib, Xc, stream)
         mark("transpose")
-        nblk, cnt_slab, w_slab, bmm = chunk_hist(XT, Xc.shape[0], wq)
+        # one chunk (the in-core sketch): pass 1 also keeps every value's bucket, so the candidate pass
+        # reads 2 bytes per value instead of searching the boundaries again
+        bid = torch.empty((F, Xc.shape[0]), dtype=torch.int16, device=dev) if single and Xc.shape[0] else None
+        nblk, cnt_slab, w_slab, bmm = chunk_hist(XT, Xc.shape[0], wq, bid)
         cnt_loc += cnt_slab.sum(0, dtype=torch.int64)
         if w_h is not None:
             w_h += w_slab.sum(0)
         vmin = torch.minimum(vmin, bmm[:, :, 0].amin(0))
         vmax = torch.maximum(vmax, bmm[:, :, 1].amax(0))
         if single:
-            kept = (XT, Xc.shape[0], wq, nblk, cnt_slab)
+            kept = (XT, Xc.shape[0], wq, nblk, cnt_slab, bid)
     cnt_h = cnt_loc
     if world > 1:  # collective 2
         cnt_h, w_h, vmin, vmax = _allreduce_buckets(dist, dev, cnt_loc, w_h, vmin, vmax)
@@ -694,8 +697,9 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
     if nseg and N:
         cursor = start.clone()
         for Xc, wq in (iter([(None, None)]) if single else chunks()):
+            bid = None
             if single:
-                XT, n, wq, nblk, cnt_slab = kept
+                XT, n, wq, nblk, cnt_slab, bid = kept
             else:
                 Xc = Xc.to(torch.float32)
                 n = Xc.shape[0]
@@ -707,7 +711,7 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
             blk_off = (torch.cumsum(per_blk, 0) - per_blk + cursor[None, :]).contiguous()
             rc = lib.cobalt_sk_gather(XT.data_ptr(), n, n, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(),
                                       slot.data_ptr(), blk_off.data_ptr(), nseg, cval.data_ptr(), _ptr(cw), nblk,
-                                      stream)
+                                      _ptr(bid), stream)
             _native.check(rc, "cobalt_sk_gather")
             cursor += per_blk.sum(0)
     if world > 1 and nseg:  # collective 3: every rank's candidates, already in the global layout
