@@ -34,6 +34,7 @@ import torch
 
 from . import gbdt_host, sketch
 from .booster import NODE_DTYPE, Booster, trees_from_heap_nodes
+from . import gbdt
 from .gbdt import GBDTParams, _resolve_device, feature_masks
 from .stream import ChunkSource, _as_np, _PinnedUploader, stream_cuts
 
@@ -155,6 +156,12 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
                              f"features (got max_depth={params.max_depth}, features={n_feat}); use sample_rate < 1")
     rep = report if report is not None else ExternalReport()
     t0 = time.perf_counter()
+    if (exact and dev.type == "cuda" and n_rows is not None and n_feat is not None
+            and device_page_bytes >= page_stride(n_feat) * int(n_rows) and _in_core_fits(int(n_rows), n_feat, dev, raw=True)):
+        # every page would sit in HBM and so does the raw matrix: ONE pass over the stream into a device
+        # matrix and the in-core fit (device sketch + binning + trees: the cuts of the streamed sketch and
+        # the trees of the exact page passes, byte for byte) -- no further passes over the source
+        return _train_in_core_raw(source, params, int(n_rows), n_feat, dev, feature_names, feature_types, rep)
     # the sketch: exact streaming (every row) sketches every row by default, like the in-core fit on a
     # GPU; the sampled mode keeps the 2^18-row strided sample (one pass over the stream instead of
     # three -- with a regenerated or re-read source the extra passes cost seconds at 100M rows)
@@ -278,17 +285,55 @@ def train_external(source: ChunkSource, params: GBDTParams | dict | None = None,
                                      external_sample_rate=float(sample_rate)))
 
 
-def _in_core_fits(N: int, F: int, dev: torch.device) -> bool:
+def _in_core_fits(N: int, F: int, dev: torch.device, raw: bool = False) -> bool:
     """The in-core trainer's ~72 B per row (32-byte records, feature-major bins, margins, labels,
-    weights, two row-index buffers; models/gbdt.py) fit the device's free memory with headroom, and
-    the rows fit its int32 row ids."""
+    weights, two row-index buffers; models/gbdt.py) -- plus, with ``raw``, the float32 matrix and the
+    sketch's transposed copy and bucket ids -- fit the device's free memory with headroom, and the rows
+    fit its int32 row ids."""
     from ..ops import gbdt_ops
 
     if N >= (1 << 31) - 1:
         return False
     free, _ = torch.cuda.mem_get_info(dev)
-    need = N * (gbdt_ops.row_stride(F) + F + 4 * 6) + (256 << 20)
+    need = N * (gbdt_ops.row_stride(F) + F + 4 * 6 + (F * 10 if raw else 0)) + (256 << 20)
     return need <= 0.9 * free
+
+
+def _train_in_core_raw(source, params: GBDTParams, N: int, F: int, dev: torch.device, feature_names, feature_types,
+                       rep: ExternalReport) -> Booster:
+    """Exact external-memory fit whose raw matrix fits the device: the stream is read once into a device
+    [N, F] float32 matrix and the in-core trainer fits it (``gbdt.train``)."""
+    from .gbdt import train
+
+    t0 = time.perf_counter()
+    up = _PinnedUploader(dev)
+    X = torch.empty((N, F), dtype=torch.float32, device=dev)
+    y = torch.empty(N, dtype=torch.float32, device=dev)
+    r0 = 0
+    for Xc, yc in source():
+        Xc = _as_np(Xc, np.float32)
+        if r0 + len(Xc) > N or Xc.shape[1] != F:
+            raise ValueError(f"the stream yields more than n_rows={N} rows or not {F} features")
+        X[r0:r0 + len(Xc)] = up.put(Xc)
+        y[r0:r0 + len(Xc)] = torch.from_numpy(_as_np(yc, np.float32)).to(dev)
+        r0 += len(Xc)
+    if r0 != N:
+        raise ValueError(f"the stream yielded {r0} rows, n_rows={N}")
+    torch.cuda.synchronize(dev)
+    rep.n_rows = N
+    rep.n_pages = 0
+    rep.host_bytes = 0
+    rep.device_page_bytes = int(X.numel() * 4)
+    rep.t_pages = time.perf_counter() - t0
+    rep.mode = "in-core"
+    t0 = time.perf_counter()
+    fr = gbdt.FitReport()
+    bst = train(X, y, params, device=dev, feature_names=feature_names, feature_types=feature_types, report=fr)
+    torch.cuda.synchronize(dev)
+    rep.t_sketch = fr.t_sketch
+    rep.t_boost = time.perf_counter() - t0 - fr.t_sketch
+    rep.sample_rows = [N] * int(params.n_estimators)
+    return bst
 
 
 def _train_in_core(source, params: GBDTParams, N: int, F: int, dev: torch.device, cuts, nbins, feature_names,

@@ -87,6 +87,12 @@ def test_external_exact_streaming_gpu_equals_in_core(colsample):
                                   report=rep)
     assert rep.mode == "in-core" and rep.host_bytes == 0, rep
     _same_trees(hbm, ref)
+    # ... and with n_rows given and the raw matrix fitting too: one pass over the stream + the in-core fit
+    rep = external.ExternalReport()
+    raw = external.train_external(src, params, n_rows=90_000, device="cuda", sample_rate=1.0,
+                                  device_page_bytes=90_000 * ps, report=rep)
+    assert rep.mode == "in-core" and rep.device_page_bytes == 90_000 * X.shape[1] * 4, rep
+    _same_trees(raw, ref)
 
 
 @pytest.mark.gpu
