@@ -1937,6 +1937,22 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
   // waits for the peers, and the ranks' sums are subtracted from it there -- no global load after the
   // exchange, and no parent registers held across it; grouped blocks load it after the exchange)
   constexpr bool kParLds = kFused && !kGroups;
+  // Without the exchange, the node's histogram bins and its parent's are issued HERE, with the node record's
+  // (scalar) loads: their addresses come from the kernel arguments and the block index, and the vector
+  // loads do not wait on the scalar ones -- one round trip for both instead of record -> bins
+  longlong2 v[2][4];
+  auto load_bins = [&]() {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb) + cofs[s][c])
+                           : make_longlong2(0, 0);
+  };
+  if (!kFused) {
+    load_bins();
+    load_parent();
+  }
   // round trip 1 (uniform scalar loads); unconditional (in-bounds) loads selected after
   const int status = nodes[n].status;
   const bool built = nodes[n].build != 0;
@@ -2007,20 +2023,16 @@ __device__ __forceinline__ bool eval_core(const GbdtDev& d, int level, int parit
   const longlong2* hb2 = reinterpret_cast<const longlong2*>(hb);
   // one pass: a block covers at most 2 features per wave (the host keeps F <= 32 per block)
   {
-  // round trip 2: the histogram bins (and the parent's, for the subtraction) of both features, all
-  // issued before the first use (clamped cells: the loads need no per-load guard)
-  longlong2 v[2][4];
+  // the histogram bins (and the parent's, for the subtraction) of both features: loaded above without the
+  // exchange; with it, the ranks' sums from LDS (clamped cells: the loads need no per-load guard)
+  if (kFused) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (kFused)  // the ranks' sums, from LDS
+      for (int c = 0; c < 4; ++c)
         v[s][c] = ld[s][c] ? s_cells[cofs[s][c] / (uint32_t)sizeof(longlong2) - (uint32_t)cb] : make_longlong2(0, 0);
-      else
-        v[s][c] = ld[s][c] ? *reinterpret_cast<const longlong2*>(reinterpret_cast<const char*>(hb2) + cofs[s][c])
-                           : make_longlong2(0, 0);
-    }
-  if (!kParLds) load_parent();
+    if (!kParLds) load_parent();
+  }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     EvalFeat& e = ef[s];
