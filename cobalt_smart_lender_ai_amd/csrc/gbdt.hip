@@ -421,6 +421,61 @@ __device__ __forceinline__ void stage_tree(const GbdtDev& d, const Node* tr, uin
   }
 }
 
+// Branch-free walk of a staged tree over a 32-byte record held in registers (the fused root pass's
+// prediction-cache update). A node is two 16-byte LDS words:
+//   {s0, s1, s2, leaf}: v_perm_b32 selectors that pull the split feature's byte out of record words
+//     (0, 1), (2, 3) or (4, 5) -- the two pairs that do not hold it select zero bytes (0x0c) -- so
+//     b = perm(w1, w0, s0) | perm(w3, w2, s1) | perm(w5, w4, s2) is the bin with no per-lane word select;
+//   {K, V, cb, cbr}: the row goes to cb (left) iff K - b >= V (unsigned), else to cbr. With K = 255 - dl
+//     and V = 255 - j - dl this is "bin <= j, the missing code 255 -> default_left" in one compare
+//     (dl = 1: b = 255 wraps K - b past every V). A leaf has zero selectors, K = V = 0 and cb = cbr = itself,
+//     so the walk runs a uniform max_depth steps and a row that reached its leaf stays there.
+// 8 VALU ops + two ds_read_b128 per level, no exec-mask branches: the `while (split)` walk over a
+// `q == 0 ? .x : q == 1 ? ...` word chain compiled to ~60 instructions of nested s_and_saveexec branches
+// per level, the root pass's largest VALU cost after the fp64 gradients.
+constexpr uint32_t kPermZero = 0x0c0c0c0cu;
+constexpr int kWalkNodeBytes = 32;
+
+__device__ __forceinline__ void stage_walk(const GbdtDev& d, const Node* tr, uint4* s_walk) {
+  for (int i = threadIdx.x; i < d.max_nodes; i += blockDim.x) {
+    const Node nd = tr[i];
+    uint4 a = make_uint4(kPermZero, kPermZero, kPermZero, __float_as_uint(nd.leaf_value));
+    uint4 c = make_uint4(0u, 0u, (uint32_t)i, (uint32_t)i);
+    if (nd.status == kSplit) {
+      const uint32_t f = (uint32_t)nd.feat, dl = (uint32_t)(nd.default_left & 1);
+      const uint32_t sel = 0x0c0c0c00u | (f & 7u);
+      a.x = (f >> 3) == 0 ? sel : kPermZero;
+      a.y = (f >> 3) == 1 ? sel : kPermZero;
+      a.z = (f >> 3) == 2 ? sel : kPermZero;
+      c = make_uint4(255u - dl, (uint32_t)(255 - nd.bin) - dl, (uint32_t)(2 * i + 1), (uint32_t)(2 * i + 2));
+    }
+    s_walk[2 * i] = a;
+    s_walk[2 * i + 1] = c;
+  }
+}
+
+// Leaf values of U rows' records (ra = record words 0-3, rb = words 4-7), walked together so the rows'
+// dependent LDS reads overlap.
+template <int U>
+__device__ __forceinline__ void walk_leaves(const uint4* s_walk, int depth, const uint4 (&ra)[U], const uint4 (&rb)[U],
+                                            float (&leaf)[U]) {
+  uint32_t n[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) n[u] = 0;
+  for (int s = 0; s < depth; ++s) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 w = s_walk[2 * n[u]];
+      const uint4 c = s_walk[2 * n[u] + 1];
+      const uint32_t b = __builtin_amdgcn_perm(ra[u].y, ra[u].x, w.x) | __builtin_amdgcn_perm(ra[u].w, ra[u].z, w.y) |
+                         __builtin_amdgcn_perm(rb[u].y, rb[u].x, w.z);
+      n[u] = (c.x - b >= c.y) ? c.z : c.w;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) leaf[u] = __uint_as_float(s_walk[2 * n[u]].w);
+}
+
 // Leaf of row i in a staged tree (the partition step's routing), walked over the FEATURE-MAJOR bins:
 // row i's bin of feature f is binsT[f][i], so the lanes of a wave (consecutive rows) read consecutive
 // bytes of each column they visit -- a coalesced load per level
@@ -1022,8 +1077,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
   const HistLaneRaw lraw = hist_lanes_load(d, tree, 0, ft);
   const FlushMeta fmeta = flush_meta_load(d, tree, 0, ft);
   uint64_t* s_hist = s_dyn;
-  uint32_t* s_meta = reinterpret_cast<uint32_t*>(s_dyn + entries * kW);
-  float* s_leaf = reinterpret_cast<float*>(s_meta + d.max_nodes);
+  uint4* s_walk = reinterpret_cast<uint4*>(s_dyn + entries * kW);  // the previous tree (stage_walk)
   {  // zero the root histogram slot (k_hist_reduce accumulates into it)
     int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[0]);
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < d.slot_elems / 2;
@@ -1031,7 +1085,7 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
       zp[e] = make_int4(0, 0, 0, 0);
   }
   if (apply_tree >= 0) {
-    stage_tree(d, d.prev_nodes, s_meta, s_leaf);
+    stage_walk(d, d.prev_nodes, s_walk);
     const int4* src = reinterpret_cast<const int4*>(d.prev_nodes);
     int4* dst = reinterpret_cast<int4*>(d.trees + (int64_t)apply_tree * d.max_nodes);
     const int nv = d.max_nodes * (int)(sizeof(Node) / sizeof(int4));
@@ -1076,24 +1130,18 @@ __device__ __forceinline__ void grad_hist_body(const GbdtDev& d, int tree, int a
         wt[u] = d.weight[ii];
       }
     }
+    // walk the previous tree with the U records held in registers (branch-free, all rows together; rows
+    // past the item walk their clamped copy and are dropped below)
+    float lf[U];
+    const bool walk = apply_tree >= 0 && d.ablate != 22;
+    if (walk) walk_leaves<U>(s_walk, d.max_depth, ra, rb, lf);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + (int64_t)u * B;
       if (i >= end) continue;
       if (d.mrec) mf[u] = __int_as_float((int)rb[u].y);  // the margin in record word 5
-      if (apply_tree >= 0 && d.ablate != 22) {  // walk the previous tree with the record held in registers
-        int nidx = 0;
-        uint32_t m = s_meta[0];
-        while (m & kMetaSplit) {
-          const int f = m & 0xFFFF, q = f >> 2;
-          const uint32_t word = q == 0 ? ra[u].x : q == 1 ? ra[u].y : q == 2 ? ra[u].z : q == 3 ? ra[u].w
-                              : q == 4 ? rb[u].x : rb[u].y;
-          const uint32_t b = (word >> (8 * (f & 3))) & 0xffu;
-          const bool left = meta_left(m, b);
-          nidx = 2 * nidx + (left ? 1 : 2);
-          m = s_meta[nidx];
-        }
-        mf[u] += s_leaf[nidx];
+      if (walk) {
+        mf[u] += lf[u];
         if (!d.mrec) d.margin[i] = mf[u];
       }
       const double mm = (double)mf[u];
@@ -3019,7 +3067,7 @@ COBALT_API int cobalt_gbdt_set_data(void* h, uint8_t* bins, const uint8_t* binsT
       if (HistKernel k = hist_kernel(hist_ft4(c->d), v == 1, v == 2))
         CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_hist));
   }
-  const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * 8;
+  const size_t grad_hist_lds = c->lds_hist + (size_t)c->max_nodes * kWalkNodeBytes;
   if (grad_hist_lds > 64 * 1024 && grad_hist_kernel(hist_ft4(c->d), wide))
     CK(hipFuncSetAttribute((const void*)grad_hist_kernel(hist_ft4(c->d), wide),
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_hist_lds));
@@ -3059,6 +3107,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   const int grad_grid = std::min(ceil_div(d.n, 256), 256 * 16);
   const int ftiles = ceil_div(d.F, d.feat_tile);
   const size_t tree_lds = (size_t)c->max_nodes * 8;
+  const size_t walk_lds = (size_t)c->max_nodes * kWalkNodeBytes;  // k_grad_hist's staged tree (stage_walk)
   if (t0 != c->grown) return -11;  // trees must be grown in order
   if (int rc = stamp_begin(c, stream)) return rc;
   // any native communicator turns on the data-parallel protocol (a 1-rank one exercises it on 1 GPU)
@@ -3235,7 +3284,7 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
       GLAUNCH("k_tree_begin", k_tree_begin, dim3(std::max(1, std::min(64, ceil_div(d.slot_elems / 2, 256)))), dim3(256), 0,
               stream, d);
     else if (fuse_root)
-      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.wide != 0), dim3(ceil_div(d.n, root_chunk)), dim3(d.wide ? 1024 : 512), c->lds_hist + tree_lds,
+      GLAUNCH("k_grad_hist", grad_hist_kernel(ft4, d.wide != 0), dim3(ceil_div(d.n, root_chunk)), dim3(d.wide ? 1024 : 512), c->lds_hist + walk_lds,
               stream, d, t, apply, root_chunk);
     else
       GLAUNCH("k_grad", k_grad, dim3(std::max(grad_grid, 1)), dim3(256), tree_lds, stream, d, t, apply);
