@@ -12,4 +12,5 @@ f=$(find /tmp/prof_$name -name '*kernel_trace.csv' | head -1)
 s=$(find /tmp/prof_$name -name '*kernel_stats.csv' | head -1)
 python3 $R/scripts/prof_summary.py "$f" "$trees" > $R/gpurun_out/prof_$name.summary.txt 2>&1
 cp "$s" $R/gpurun_out/prof_$name.kernel_stats.csv
+python3 $R/scripts/prof_prelude.py "$f" > $R/gpurun_out/prof_$name.prelude.txt 2>&1
 tail -n 60 $R/gpurun_out/prof_$name.summary.txt
