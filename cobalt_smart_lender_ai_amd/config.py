@@ -153,6 +153,7 @@ KNOBS: dict[str, Knob] = {
     "COBALT_MAX_COPY_SHIFT": Knob("4", "native", "log2 of the per-lane LDS histogram copies of a low-cardinality feature (0..6)"),
     "COBALT_WT": Knob("auto", "native", "write-through stores: bit 0 histogram slabs, bit 1 partition row ids, bit 2 the root pass's (g, h) (7 below 4M rows, else 5)"),
     "COBALT_MARGIN_IN_RECORD": Knob("1", "native", "binary labels, <= 20 features, >= 4M rows: the root pass keeps every row's margin in its 32-byte record (0 off, 2 at any row count)"),
+    "COBALT_PART_POS": Knob("1", "native", "row partition in position-ordered blocks whose row-id loads need no plan (0: node-ordered items)"),
     "COBALT_BIN_SCALAR": Knob("", "native", "force the generic binning kernel for 32-byte records (tests)"),
     "COBALT_PRED_WALK": Knob("4", "native", "trees walked at once per predictor thread (2 / 4 / 8)"),
     # -- data parallelism --

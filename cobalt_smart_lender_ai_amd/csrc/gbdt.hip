@@ -2409,6 +2409,272 @@ __global__ __launch_bounds__(kPartWaves * 64) void k_partition(GbdtDev d, int pa
   }
 }
 
+// Row partition by POSITION (levels with <= 64 nodes): block b takes the row-id positions [b C, (b + 1) C)
+// of the level's ridx buffer (C = 16 waves x kSteps x 64), whatever nodes they belong to. A level's nodes
+// own disjoint, position-ordered ranges of that buffer (every child range lies inside its parent's), so the
+// block's row-id loads depend on nothing but the block index: they are issued at kernel entry, in the same
+// round trip as the level's node records -- where the node-ordered k_partition first plans its item from
+// the node table and only then loads its row ids (~1.1-1.4 us per block at 10M rows, one of ~4 dependent
+// round trips). A wave's 512 positions cover a few ranges: a uniform walk over the split ranges that start
+// before each 64-row step gives every lane its node; positions of leaves (and gaps) route nowhere. Counts
+// are kept per (wave, range) in LDS, one cursor claim per range per block (all in one round trip), and the
+// scatter advances per-(wave, range) pointers as k_partition's per-wave ones (left rows ascending from the
+// node start, right rows descending from its end).
+constexpr int kPartPosNodes = 64;
+
+template <int kSteps>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_part_pos(GbdtDev d, int parity, int64_t zero_next, int level) {
+  constexpr int kPW = 16;
+  constexpr int kN = kPartPosNodes;
+  BlockStamp stamp_(d);
+  __shared__ int s_rs[kN], s_re[kN];  // split ranges (position order): start, end
+  __shared__ uint32_t s_rm[kN];        // feature | (j + 1) << 16 | dl << 25
+  __shared__ int s_rn[kN];             // node index
+  __shared__ int s_nr;
+  __shared__ int32_t s_cnt[kPW][kN][2];  // per (wave, range): left / right rows, then the wave's scatter bases
+  __shared__ int s_one, s_one_node, s_one_start, s_one_end;  // the block's one range (s_one < 0: several)
+  __shared__ uint32_t s_one_meta;
+  __shared__ int32_t s_wc[2][kPW];
+  __shared__ int32_t s_wbase[2];
+  {  // zero the next level's histogram slots (hist_b of the other parity is free at this point)
+    int4* zp = reinterpret_cast<int4*>(d.zero_red ? d.zero_red : d.hist_b[parity ^ 1]);
+    const int64_t nz = zero_next / 2;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nz; e += (int64_t)gridDim.x * blockDim.x)
+      zp[e] = make_int4(0, 0, 0, 0);
+  }
+  const int n = (int)d.n;
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id()), lane = lane_id();
+  const int wb = blockIdx.x * (kPW * kSteps * kWave) + wv * (kSteps * kWave);
+  const bool identity = parity == 0 && level == 0;  // the root's rows in identity order (never written)
+  const int32_t* cur = d.ridx[parity];
+  int32_t* nxt = d.ridx[parity ^ 1];
+  // row ids first: unconditional loads at clamped positions (no dependence on the node table)
+  int r[kSteps];
+#pragma unroll
+  for (int k = 0; k < kSteps; ++k) {
+    const int p = min(wb + k * kWave + lane, n - 1);
+    r[k] = identity ? p : cur[p];
+  }
+  // the level's split nodes with rows -> LDS, in position order (wave 0, one lane per node)
+  const int first = (1 << level) - 1, nlev = 1 << level;
+  if (wv == 0) {
+    const int e = lane;
+    const Node& nd = d.nodes[first + min(e, nlev - 1)];
+    const int st = nd.status, start = nd.start, cnt = nd.count, f = nd.feat, j = nd.bin, dl = nd.default_left;
+    const bool on = e < nlev && st == kSplit && cnt > 0;
+    const uint64_t m = __ballot(on);
+    if (on) {
+      const int k = mask_rank(m);
+      s_rs[k] = start;
+      s_re[k] = start + cnt;
+      s_rm[k] = (uint32_t)f | ((uint32_t)(j + 1) & 0x1FFu) << 16 | (uint32_t)(dl & 1) << 25;
+      s_rn[k] = first + e;
+    }
+    if (e == 0) s_nr = __popcll(m);
+    // the block's positions inside ONE split range (nearly every block: a node's range spans ~10^5 rows)?
+    const int b0 = blockIdx.x * (kPW * kSteps * kWave), b1 = min(n, b0 + kPW * kSteps * kWave);
+    const uint64_t hit = __ballot(on && start <= b0 && start + cnt >= b1);
+    if (e == 0) s_one = hit ? __ffsll((unsigned long long)hit) - 1 : -1;
+    if (hit && e == __ffsll((unsigned long long)hit) - 1) {
+      s_one_node = first + e;
+      s_one_start = start;
+      s_one_end = start + cnt;
+      s_one_meta = (uint32_t)f | ((uint32_t)(j + 1) & 0x1FFu) << 16 | (uint32_t)(dl & 1) << 25;
+    }
+  }
+  for (int i = threadIdx.x; i < kPW * kN * 2; i += blockDim.x) (&s_cnt[0][0][0])[i] = 0;
+  __syncthreads();
+  stamp_.probe(1);
+  const int nr = s_nr;
+  if (nr == 0) return;
+  if (s_one >= 0) {
+    // One range: k_partition's per-wave passes (counts by ballot, one claim, running per-wave pointers)
+    const int node = s_one_node, nstart = s_one_start, nend = s_one_end;
+    const uint32_t m = s_one_meta;
+    const uint8_t* col = d.binsT + (int64_t)(m & 0xFFFFu) * d.ldt;
+    uint8_t bv1[kSteps];
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) bv1[k] = col[r[k]];
+    const int jm1 = (int)((m >> 16) & 0x1FFu);
+    const uint32_t dlv = (m >> 25) & 1u;
+    const int nv = max(0, min(n, wb + kSteps * kWave) - wb);  // valid positions of this wave (a prefix)
+    uint32_t lb = 0;
+    int nl = 0;
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) {
+      const uint32_t b = bv1[k];
+      const uint32_t lt = (uint32_t)((int)b - jm1) >> 31;
+      const uint32_t ms = (b + 1u) >> 8;
+      const uint32_t ok = (uint32_t)(k * kWave + lane < nv);
+      const uint32_t left = (lt | (ms & dlv)) & ok;
+      lb |= left << k;
+      nl += __popcll(__ballot(left != 0u));
+    }
+    asm volatile("" : "+v"(lb));
+    if (lane == 0) { s_wc[0][wv] = nl; s_wc[1][wv] = nv - nl; }
+    __syncthreads();
+    stamp_.probe(2);
+    if (threadIdx.x == 0) {
+      int tl = 0, tr = 0;
+      for (int k = 0; k < kPW; ++k) { tl += s_wc[0][k]; tr += s_wc[1][k]; }
+      const unsigned long long c =
+          d.ablate == 12 ? 0ull
+                         : atomicAdd(reinterpret_cast<unsigned long long*>(d.cursors + 2 * node),
+                                     ((unsigned long long)(uint32_t)tr << 32) | (uint32_t)tl);
+      s_wbase[0] = (int32_t)(uint32_t)c;
+      s_wbase[1] = (int32_t)(c >> 32);
+    }
+    __syncthreads();
+    stamp_.probe(3);
+    int bl = s_wbase[0], br = s_wbase[1];
+    for (int k = 0; k < wv; ++k) { bl += s_wc[0][k]; br += s_wc[1][k]; }
+    uint32_t pl_ = (uint32_t)(nstart + bl);
+    uint32_t pr_ = (uint32_t)(nend - 1 - br);
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) {
+      const bool valid = k * kWave + lane < nv;
+      const uint32_t left = (lb >> k) & 1u;
+      const uint64_t lm = __ballot(left != 0u), vm = __ballot(valid);
+      const uint32_t rk_l = mask_rank(lm);
+      const uint32_t dst = rk_l + (left ? pl_ : pr_ - (uint32_t)lane);
+      if (valid) store_wt(nxt + dst, r[k], (d.wt & 2) != 0);
+      const uint32_t cl = (uint32_t)__popcll(lm);
+      pl_ += cl;
+      pr_ -= (uint32_t)__popcll(vm) - cl;
+    }
+    return;
+  }
+  // first range that ends past the wave's first position (uniform binary search over the LDS ends)
+  int k0 = 0;
+  {
+    int lo = 0, hi = nr;  // first k with re[k] > wb
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (__builtin_amdgcn_readfirstlane(s_re[mid]) > wb) hi = mid; else lo = mid + 1;
+    }
+    k0 = lo;
+  }
+  // pass 1: each lane's range (uniform walk over the ranges that start inside or before the step), the
+  // split feature's bin, the direction; per (wave, range) counts
+  // each row's range, packed 8 bits per step (0xFF: routes nowhere) -- 2 VGPRs instead of kSteps (the kernel
+  // must stay within 64 VGPRs for two 1024-thread blocks per CU)
+  uint32_t klp[(kSteps + 3) / 4];
+#pragma unroll
+  for (int i = 0; i < (kSteps + 3) / 4; ++i) klp[i] = 0xFFFFFFFFu;
+  auto kl_of = [&](int k) -> int {
+    const uint32_t v = (klp[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+    return v == 0xFFu ? -1 : (int)v;
+  };
+  uint32_t lbits = 0, inbits = 0;
+  uint8_t bv[kSteps];
+  // Fast path (nearly every wave: a node's range spans ~10^5 positions): the wave's positions lie inside one
+  // range -- every lane's node is k0, no per-lane search. Otherwise each lane binary-searches the ranges
+  // from k0 on (the last one starting at or before its position) and checks the range's end.
+  const bool one = k0 < nr && __builtin_amdgcn_readfirstlane(s_rs[k0]) <= wb &&
+                   __builtin_amdgcn_readfirstlane(s_re[k0]) >= wb + kSteps * kWave;
+  if (one) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane(s_rm[k0]);
+    const uint8_t* col = d.binsT + (int64_t)(m & 0xFFFFu) * d.ldt;
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) {
+      klp[k >> 2] &= ~((uint32_t)(0xFFu ^ (uint32_t)k0) << (8 * (k & 3)));
+      bv[k] = col[max(r[k], 0)];
+    }
+    inbits = (1u << kSteps) - 1u;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kSteps; ++k) {
+      const int p = wb + k * kWave + lane;
+      int lo = k0, hi = nr - 1, kk = -1;  // last t in [k0, nr) with rs[t] <= p
+      while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_rs[mid] <= p) { kk = mid; lo = mid + 1; } else hi = mid - 1;
+      }
+      const bool in = kk >= 0 && p < n && p < s_re[max(kk, 0)];
+      if (in) klp[k >> 2] &= ~((uint32_t)(0xFFu ^ (uint32_t)kk) << (8 * (k & 3)));
+      inbits |= (in ? 1u : 0u) << k;
+      // the split feature's bin: an unconditional load (lanes outside a range read their nearest one's column)
+      const uint32_t m = s_rm[max(kk, 0)];
+      bv[k] = d.binsT[(int64_t)(m & 0xFFFFu) * d.ldt + max(r[k], 0)];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kSteps; ++k) {
+    const int klk = kl_of(k);
+    const uint32_t m = s_rm[max(klk, 0)];
+    const uint32_t b = bv[k];
+    const int jm1 = (int)((m >> 16) & 0x1FFu);  // j + 1
+    const uint32_t lt = (uint32_t)((int)b - jm1) >> 31;
+    const uint32_t ms = (b + 1u) >> 8;
+    const uint32_t left = (lt | (ms & ((m >> 25) & 1u))) & ((inbits >> k) & 1u);
+    lbits |= left << k;
+    // per-range counts of this step (uniform loop over the ranges present in it; usually one)
+    uint64_t rem = __ballot((inbits >> k) & 1u);
+    const uint64_t lm = __ballot(left != 0u);
+    while (rem) {
+      const int src = __ffsll((unsigned long long)rem) - 1;
+      const int kk = __builtin_amdgcn_readlane(klk, src);
+      const uint64_t mk = __ballot(klk == kk) & rem;
+      if (lane == 0) {
+        s_cnt[wv][kk][0] += __popcll(mk & lm);
+        s_cnt[wv][kk][1] += __popcll(mk & ~lm);
+      }
+      rem &= ~mk;
+    }
+  }
+  __syncthreads();
+  stamp_.probe(2);
+  // one claim per range for the whole block (thread t: range t), then each wave's bases
+  if ((int)threadIdx.x < nr) {
+    const int t = threadIdx.x;
+    int tl = 0, tr = 0;
+    for (int w = 0; w < kPW; ++w) { tl += s_cnt[w][t][0]; tr += s_cnt[w][t][1]; }
+    if (tl + tr > 0) {
+      const unsigned long long c =
+          d.ablate == 12 ? 0ull
+                         : atomicAdd(reinterpret_cast<unsigned long long*>(d.cursors + 2 * s_rn[t]),
+                                     ((unsigned long long)(uint32_t)tr << 32) | (uint32_t)tl);
+      int bl = s_rs[t] + (int)(uint32_t)c;                // next left slot
+      int br = s_re[t] - 1 - (int)(uint32_t)(c >> 32);    // next right slot (descending)
+      for (int w = 0; w < kPW; ++w) {
+        const int cl = s_cnt[w][t][0], cr = s_cnt[w][t][1];
+        s_cnt[w][t][0] = bl;
+        s_cnt[w][t][1] = br;
+        bl += cl;
+        br -= cr;
+      }
+    }
+  }
+  __syncthreads();
+  stamp_.probe(3);
+  // pass 2: scatter with ballot ranks inside each (step, range)
+#pragma unroll
+  for (int k = 0; k < kSteps; ++k) {
+    const bool in = (inbits >> k) & 1u;
+    const uint32_t left = (lbits >> k) & 1u;
+    const int klk = kl_of(k);
+    uint64_t rem = __ballot(in);
+    const uint64_t lm = __ballot(left != 0u);
+    while (rem) {
+      const int src = __ffsll((unsigned long long)rem) - 1;
+      const int kk = __builtin_amdgcn_readlane(klk, src);
+      const uint64_t mk = __ballot(klk == kk) & rem;
+      const int pl = __builtin_amdgcn_readfirstlane(s_cnt[wv][kk][0]);
+      const int pr = __builtin_amdgcn_readfirstlane(s_cnt[wv][kk][1]);
+      const uint64_t ml = mk & lm, mr = mk & ~lm;
+      if (klk == kk) {
+        const int dst = left ? pl + mask_rank(ml) : pr - mask_rank(mr);
+        store_wt(nxt + dst, r[k], (d.wt & 2) != 0);
+      }
+      if (lane == 0) {
+        s_cnt[wv][kk][0] = pl + __popcll(ml);
+        s_cnt[wv][kk][1] = pr - __popcll(mr);
+      }
+      rem &= ~mk;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Split evaluation fused with the row partition (one GPU, a level's items <= CUs, levels 0 .. max_depth - 2).
 // At small row counts a level is a chain of short launches whose fixed costs dominate (1M rows:
@@ -3265,6 +3531,8 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
   }
   const int root_chunk = std::max(root_min, env_root > 0 ? std::min(16384, std::max(1024, env_root / 64 * 64))
                                                          : root_rule);
+  // COBALT_PART_POS=0: node-ordered partition items (k_partition) instead of position-ordered blocks
+  const bool part_pos = knob_int(Knob::PartPos, 1) != 0;
   // Per tree: grad (+ root histogram, node-table init, archive/apply of the previous tree), then per
   // level: hist -> reduce -> [data parallel: the histogram collective] -> eval [-> partition], or
   // hist -> reduce [-> collective] -> the fused evaluation + partition pass; the last split level's
@@ -3373,6 +3641,12 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           const int evals = ep_mode >= 2 ? (1 << level) : 0;  // the evaluator blocks come first
           launch_eval_part(steps, ep_mode, dim3(ubp + evals), ep_mode == 2 ? fused_lds : 0, stream, d, parity, zero_next,
                            level, chp, t, c->eval_slots, ++c->dec_tag);
+        } else if (part_pos && (1 << level) <= kPartPosNodes) {  // position-ordered blocks (k_part_pos)
+          const dim3 pg(std::max(1, (int)ceil_div(d.n, (int64_t)16 * kWave * steps)));
+          if (steps <= 4)
+            GLAUNCH("k_partition", (k_part_pos<4>), pg, dim3(16 * kWave), 0, stream, d, parity, zero_next, level);
+          else
+            GLAUNCH("k_partition", (k_part_pos<8>), pg, dim3(16 * kWave), 0, stream, d, parity, zero_next, level);
         } else if (steps <= 4)
           GLAUNCH("k_partition", (k_partition<16, 4>), dim3(ubp), dim3(16 * kWave), 0, stream, d, parity, zero_next,
                   level, chp);

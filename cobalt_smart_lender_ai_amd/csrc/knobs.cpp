@@ -12,7 +12,7 @@ static const char* const kKnobNames[(int)Knob::Count] = {
     "COBALT_ROOT_CHUNK",   "COBALT_PART_CHUNK",  "COBALT_EVAL_FG",        "COBALT_EVAL_PART",
     "COBALT_HIST_PAIR",    "COBALT_MAX_COPY_SHIFT", "COBALT_WT",          "COBALT_IPC_FUSED",
     "COBALT_DP_OWNER",     "COBALT_CU_BUDGET",   "COBALT_BIN_SCALAR",     "COBALT_PRED_WALK",
-    "COBALT_EVAL_BLOCKS",  "COBALT_MARGIN_IN_RECORD",
+    "COBALT_EVAL_BLOCKS",  "COBALT_MARGIN_IN_RECORD", "COBALT_PART_POS",
 };
 
 const char* knob_name(Knob k) { return kKnobNames[(int)k]; }

@@ -26,6 +26,7 @@ enum class Knob : int {
   PredWalk,      // COBALT_PRED_WALK: trees walked at once per predictor thread (2 / 4 / 8)
   EvalBlocks,    // COBALT_EVAL_BLOCKS: the evaluator-block fused pass over the fused IPC exchange
   MarginInRecord,  // COBALT_MARGIN_IN_RECORD: the root pass keeps the margins in the row records (F <= 20)
+  PartPos,       // COBALT_PART_POS: position-ordered partition blocks (k_part_pos; 0: node-ordered items)
   Count
 };
 

@@ -95,12 +95,14 @@ def test_gpu_trees_identical_to_host_oracle(kw):
 
 @pytest.mark.parametrize("env", [{"COBALT_HIST_PAIR": "0"}, {"COBALT_MAX_COPY_SHIFT": "6"}, {"COBALT_MAX_COPY_SHIFT": "5"},
                                  {"COBALT_MAX_COPY_SHIFT": "0", "COBALT_HIST_PAIR": "0"},
-                                 {"COBALT_EVAL_PART": "0"}, {"COBALT_EVAL_FG": "4"}])
+                                 {"COBALT_EVAL_PART": "0"}, {"COBALT_EVAL_PART": "0", "COBALT_PART_POS": "0"},
+                                 {"COBALT_EVAL_FG": "4"}])
 def test_gpu_histogram_variants_identical_to_host_oracle(env, monkeypatch):
     """The variants behind switches (one lane per row instead of the default lane-pair record gathers;
     64, 32 or 1 per-lane copies of a low-cardinality feature instead of 16; the separate evaluation and
-    partition passes instead of the fused one; grouped split evaluation) grow the oracle's trees (the
-    switches are read when a trainer context is created)."""
+    partition passes instead of the fused one -- position-ordered partition blocks (k_part_pos), and the
+    node-ordered items (k_partition); grouped split evaluation) grow the oracle's trees (the switches are
+    read when a trainer context is created, COBALT_PART_POS per grow call)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     X, y = _data(60_000, seed=4)
