@@ -3642,8 +3642,10 @@ static int grow_impl(GbdtCtx* c, int t0, int n_trees, hipStream_t stream, bool s
           launch_eval_part(steps, ep_mode, dim3(ubp + evals), ep_mode == 2 ? fused_lds : 0, stream, d, parity, zero_next,
                            level, chp, t, c->eval_slots, ++c->dec_tag);
         } else if (part_pos && (1 << level) <= kPartPosNodes) {  // position-ordered blocks (k_part_pos)
-          const dim3 pg(std::max(1, (int)ceil_div(d.n, (int64_t)16 * kWave * steps)));
-          if (steps <= 4)
+          // (the grid from the instantiation's rows per block: COBALT_PART_CHUNK may give 1-3 or 5-7 steps)
+          const int ps = steps <= 4 ? 4 : 8;
+          const dim3 pg(std::max(1, (int)ceil_div(d.n, (int64_t)16 * kWave * ps)));
+          if (ps == 4)
             GLAUNCH("k_partition", (k_part_pos<4>), pg, dim3(16 * kWave), 0, stream, d, parity, zero_next, level);
           else
             GLAUNCH("k_partition", (k_part_pos<8>), pg, dim3(16 * kWave), 0, stream, d, parity, zero_next, level);
