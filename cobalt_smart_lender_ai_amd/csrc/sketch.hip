@@ -6,14 +6,15 @@
 // segmented sort of F x N (value, weight) pairs costs ~85 ms at 10M x 20 on one MI355X; 255 order
 // statistics per feature do not need the order of all N values:
 //
-//  1. boundaries: <= 4095 distinct values of a strided sample, sorted (host side, torch.sort of a
-//     few 10k values per feature). They split the value axis into buckets 2k+1 = {u_k} (a value of
+//  1. boundaries: <= 4095 distinct values of a strided sample (torch.sort of a few 10k values per
+//     feature, then k_sk_bounds). They split the value axis into buckets 2k+1 = {u_k} (a value of
 //     the sample) and 2k = (u_{k-1}, u_k) (strictly between two of them) -- 2m + 1 buckets.
 //  2. k_sk_hist: one pass over the (feature-major) values: the bucket of every value by a branchless
 //     binary search over the boundaries in LDS, integer weight sums per bucket in an LDS histogram,
 //     written as the block's slab row (no global atomics), plus the block's minimum value.
-//  3. (torch) prefix sums over the buckets locate every target rank: a target in an equal bucket IS
-//     its value; one in an open bucket needs that bucket's values ("candidates", ~N / 4096 rows each).
+//  3. k_sk_plan1-3: prefix sums over the buckets locate every target rank: a target in an equal
+//     bucket IS its value; one in an open bucket needs that bucket's values ("candidates", ~N / 4096
+//     rows each). The selected buckets become segments with their offsets (one host read: the sizes).
 //  4. k_sk_gather: a second pass writes the values of the selected open buckets into per-bucket
 //     segments (LDS-aggregated range reservations: one global atomic per block and bucket).
 //  5. k_sk_select: one block per selected bucket sorts its segment in LDS (bitonic, values with their
@@ -390,6 +391,532 @@ __global__ __launch_bounds__(1024) void k_sk_exact(const int64_t* __restrict__ c
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// The planning between the passes, on the device. The bucket arithmetic between pass 1 and the
+// candidate select (boundaries from the sorted sample, slab sums, the target buckets, the selected
+// segments and their offsets, the per-target arguments of k_sk_select, the cut tables) was ~150 small
+// torch launches and five host synchronisations: ~2 ms per sketch, most of the sketch's wall time
+// (1.25M rows: 2.5 ms of which ~0.4 ms kernel time). Here it is six kernels and ONE host read of the
+// plan's sizes. Every quantity is the same integer / float arithmetic as the torch form it replaces
+// (models/sketch.py keeps the rare host fallbacks), so the cuts stay bit-identical to compute_cuts.
+// ------------------------------------------------------------------------------------------
+constexpr int kSkT = 255;                                 // targets j = 1..255 per feature
+constexpr int kSkPer = (kSkBuckets + 1023) / 1024;        // buckets per thread of a 1024-thread block (9)
+
+// Block-wide exclusive scan of one int64 per thread (1024 threads); `total` = the block's sum in every
+// thread. s_w: 16 int64 of LDS. Contains the barriers that publish LDS writes made before the call.
+__device__ __forceinline__ int64_t sk_block_excl(int64_t v, int64_t* s_w, int64_t& total) {
+  const int lane = lane_id(), wv = wave_id();
+  const int64_t incl = wave_incl_scan(v);
+  if (lane == kWave - 1) s_w[wv] = incl;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+  for (int i = 0; i < (int)(blockDim.x / kWave); ++i) {
+    const int64_t x = s_w[i];
+    if (i < wv) base += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return base + incl - v;
+}
+
+// Boundaries from the sorted strided sample sv [F][S] (NaN last): the values at positions k * cnt / K
+// (K = kSkMaxBounds - 1, k = 0..K-1) that differ from their predecessor, compacted; +inf padding.
+__global__ __launch_bounds__(1024) void k_sk_bounds(const float* __restrict__ sv, int S, float* __restrict__ bounds,
+                                                    int32_t* __restrict__ nbound) {
+  constexpr int K = kSkMaxBounds - 1;
+  __shared__ int64_t s_w[16];
+  __shared__ int s_cnt;
+  const int f = blockIdx.x, t = threadIdx.x;
+  const float* x = sv + (int64_t)f * S;
+  float* bo = bounds + (int64_t)f * kSkMaxBounds;
+  if (t == 0) {  // valid values = the index of the first NaN
+    int lo = 0, hi = S;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (x[mid] == x[mid]) lo = mid + 1; else hi = mid;
+    }
+    s_cnt = lo;
+  }
+  for (int i = t; i < kSkMaxBounds; i += blockDim.x) bo[i] = INFINITY;
+  __syncthreads();
+  const int64_t cnt = s_cnt;
+  float u[4];
+  bool nv[4];
+  int64_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 4 * t + q;
+    nv[q] = false;
+    u[q] = 0.0f;
+    if (k < K) {
+      const int64_t pos = (int64_t)k * cnt / K;
+      u[q] = x[min(pos, (int64_t)S - 1)];
+      const bool ok = pos < cnt;
+      bool diff = true;
+      if (k > 0) diff = u[q] != x[min((int64_t)(k - 1) * cnt / K, (int64_t)S - 1)];
+      nv[q] = ok && diff;
+    }
+    c += nv[q] ? 1 : 0;
+  }
+  int64_t total;
+  int64_t r = sk_block_excl(c, s_w, total);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (nv[q]) bo[r++] = u[q];
+  if (t == 0) nbound[f] = (int32_t)total;
+}
+
+// The boundaries straight from the strided sample (S <= kSkSampleCap values per feature): the sample's
+// column is loaded (-0 -> +0; NaN and padding as the largest key, torch.sort's NaN-last order) and
+// bitonic-sorted as ordered-float keys, 32 per thread in registers: the stages with partners in the
+// same thread (j < 32) are register compare-exchanges, the others go through LDS (element t * 32 + e at
+// word e * 1024 + t: conflict-free), then reduced to boundaries as k_sk_bounds does -- one launch
+// instead of a segmented torch.sort and k_sk_bounds. value (i, f) = X[i * srow + f * scol].
+constexpr int kSkSampleCap = 32768;  // 128 KB of keys in LDS
+constexpr int kSkSortE = kSkSampleCap / 1024;  // keys per thread
+
+__global__ __launch_bounds__(1024) void k_sk_sample_bounds(const float* __restrict__ X, int64_t srow, int64_t scol, int S,
+                                                           float* __restrict__ bounds, int32_t* __restrict__ nbound) {
+  constexpr int K = kSkMaxBounds - 1;
+  constexpr int E = kSkSortE;
+  extern __shared__ uint32_t s_key[];
+  __shared__ int64_t s_w[16];
+  const int f = blockIdx.x, t = threadIdx.x;
+  uint32_t r[E];
+  int64_t valid = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = t * E + e;
+    uint32_t k = 0xFFFFFFFFu;
+    if (i < S) {
+      const float v = X[(int64_t)i * srow + (int64_t)f * scol] + 0.0f;
+      if (v == v) {
+        k = fkey(v);
+        ++valid;
+      }
+    }
+    r[e] = k;
+  }
+  float* bo = bounds + (int64_t)f * kSkMaxBounds;
+  for (int i = t; i < kSkMaxBounds; i += blockDim.x) bo[i] = INFINITY;
+  for (int k = 2; k <= kSkSampleCap; k <<= 1) {
+    for (int j = k >> 1; j >= E; j >>= 1) {  // partner in thread t ^ (j / E), same register
+#pragma unroll
+      for (int e = 0; e < E; ++e) s_key[e * 1024 + t] = r[e];
+      __syncthreads();
+      const int tp = t ^ (j / E);
+      const bool lower = t < tp;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const uint32_t a = r[e], b = s_key[e * 1024 + tp];
+        const bool up = ((t * E + e) & k) == 0;
+        r[e] = (lower == up) ? min(a, b) : max(a, b);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int jj = E / 2; jj >= 1; jj >>= 1) {  // partner in the same thread
+      if (jj < k) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int pe = e ^ jj;
+          if (pe > e) {
+            const uint32_t a = r[e], b = r[pe];
+            const bool up = ((t * E + e) & k) == 0;
+            const bool sw = (a > b) == up;
+            r[e] = sw ? b : a;
+            r[pe] = sw ? a : b;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) s_key[e * 1024 + t] = r[e];
+  int64_t cnt;
+  sk_block_excl(valid, s_w, cnt);  // (its barriers publish the sorted keys)
+  auto key_at = [&](int64_t p) { return s_key[(p % E) * 1024 + p / E]; };
+  float u[4];
+  bool nv[4];
+  int64_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 4 * t + q;
+    nv[q] = false;
+    u[q] = 0.0f;
+    if (k < K) {
+      const int64_t pos = (int64_t)k * cnt / K;
+      u[q] = fval(key_at(min(pos, (int64_t)S - 1)));
+      const bool ok = pos < cnt;
+      bool diff = true;
+      if (k > 0) diff = u[q] != fval(key_at(min((int64_t)(k - 1) * cnt / K, (int64_t)S - 1)));
+      nv[q] = ok && diff;
+    }
+    c += nv[q] ? 1 : 0;
+  }
+  int64_t total;
+  int64_t rr = sk_block_excl(c, s_w, total);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (nv[q]) bo[rr++] = u[q];
+  if (t == 0) nbound[f] = (int32_t)total;
+}
+
+// Pass-1 slabs summed into the bucket tables (accumulated: a streamed sketch adds chunk by chunk) and
+// the blocks' value ranges into vmin / vmax. grid = (buckets / 256, F).
+template <bool kW>
+__global__ __launch_bounds__(256) void k_sk_reduce(const uint32_t* __restrict__ cnt_slab,
+                                                   const unsigned long long* __restrict__ w_slab,
+                                                   const float* __restrict__ bmm, int nblk, int F, int64_t* __restrict__ cnt,
+                                                   int64_t* __restrict__ wsum, float* __restrict__ vmin,
+                                                   float* __restrict__ vmax) {
+  const int f = blockIdx.y;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < kSkBuckets) {
+    int64_t s = 0, sw = 0;
+    for (int k = 0; k < nblk; ++k) {
+      const int64_t row = (int64_t)k * F + f;
+      s += cnt_slab[row * kSkBuckets + b];
+      if (kW) sw += (int64_t)w_slab[row * kSkBuckets + b];
+    }
+    cnt[(int64_t)f * kSkBuckets + b] += s;
+    if (kW) wsum[(int64_t)f * kSkBuckets + b] += sw;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float a = vmin[f], z = vmax[f];
+    for (int k = 0; k < nblk; ++k) {
+      a = fminf(a, bmm[((int64_t)k * F + f) * 2]);
+      z = fmaxf(z, bmm[((int64_t)k * F + f) * 2 + 1]);
+    }
+    vmin[f] = a;
+    vmax[f] = z;
+  }
+}
+
+// The plan's device arrays, carved from one int64 workspace (offsets in int64 words: sk_plan_layout).
+enum SkArr {
+  kSel, kFstat, kFbase, kSummary, kQ0, kThr, kPre, kTb, kNeed, kSlot, kSegFeat, kSegBucket, kLocSizes, kGlobSizes,
+  kLocOff, kGlobOff, kTgtOff, kWant, kNdist, kTpos, kTprefix, kTthr, kTmaxb, kSkArrCount
+};
+// per-feature statistics (kFstat, 5 words): selected buckets, open targets, local / global rows of the
+// selected buckets, uncertain flag; bases (kFbase, 4 words): the exclusive prefixes of the first four.
+// summary (8 words): nseg, T, local rows, global rows, any uncertain, big segments with targets, big
+// segments of uncertain features, 0.
+struct SkPlan {
+  uint8_t* sel;
+  int64_t *fstat, *fbase, *summary;
+  float* q0;
+  int64_t *thr, *pre;
+  int32_t* tb;
+  uint8_t* need;
+  int32_t *slot, *seg_feat, *seg_bucket;
+  int64_t *loc_sizes, *glob_sizes, *loc_off, *glob_off;
+  int32_t* tgt_off;
+  uint8_t* want;
+  int32_t *ndist, *tpos;
+  int64_t *tprefix, *tthr, *tmaxb;
+};
+
+__host__ inline void sk_plan_layout(int F, int64_t* off) {
+  const int64_t SC = (int64_t)F * kSkBuckets, TC = (int64_t)F * kSkT;
+  const int64_t words[kSkArrCount] = {
+      (SC + 7) / 8, 5LL * F, 4LL * F, 8, (TC + 1) / 2, TC, TC, (TC + 1) / 2, (TC + 7) / 8, (SC + 1) / 2, (SC + 1) / 2,
+      (SC + 1) / 2, SC, SC, SC + 1, SC + 1, (SC + 2) / 2, (SC + 7) / 8, (SC + 1) / 2, (TC + 1) / 2, TC, TC, TC};
+  int64_t o = 0;
+  for (int i = 0; i < kSkArrCount; ++i) {
+    off[i] = o;
+    o += words[i];
+  }
+  off[kSkArrCount] = o;
+}
+
+__host__ inline SkPlan sk_plan_views(int F, int64_t* ws) {
+  int64_t off[kSkArrCount + 1];
+  sk_plan_layout(F, off);
+  SkPlan p;
+  p.sel = reinterpret_cast<uint8_t*>(ws + off[kSel]);
+  p.fstat = ws + off[kFstat];
+  p.fbase = ws + off[kFbase];
+  p.summary = ws + off[kSummary];
+  p.q0 = reinterpret_cast<float*>(ws + off[kQ0]);
+  p.thr = ws + off[kThr];
+  p.pre = ws + off[kPre];
+  p.tb = reinterpret_cast<int32_t*>(ws + off[kTb]);
+  p.need = reinterpret_cast<uint8_t*>(ws + off[kNeed]);
+  p.slot = reinterpret_cast<int32_t*>(ws + off[kSlot]);
+  p.seg_feat = reinterpret_cast<int32_t*>(ws + off[kSegFeat]);
+  p.seg_bucket = reinterpret_cast<int32_t*>(ws + off[kSegBucket]);
+  p.loc_sizes = ws + off[kLocSizes];
+  p.glob_sizes = ws + off[kGlobSizes];
+  p.loc_off = ws + off[kLocOff];
+  p.glob_off = ws + off[kGlobOff];
+  p.tgt_off = reinterpret_cast<int32_t*>(ws + off[kTgtOff]);
+  p.want = reinterpret_cast<uint8_t*>(ws + off[kWant]);
+  p.ndist = reinterpret_cast<int32_t*>(ws + off[kNdist]);
+  p.tpos = reinterpret_cast<int32_t*>(ws + off[kTpos]);
+  p.tprefix = ws + off[kTprefix];
+  p.tthr = ws + off[kTthr];
+  p.tmaxb = ws + off[kTmaxb];
+  return p;
+}
+
+// Plan 1, one block per feature: prefix sums C of the bucket weights, the target bucket b_j of every
+// rank j W / maxb (first bucket with C * maxb > j W), its value when b_j is an equal bucket, the
+// feature's class (many / exactly known / uncertain distinct values), the open targets and the
+// selected buckets (the open targets' buckets; for an uncertain feature also every open bucket with
+// rows), and the per-feature totals.
+__global__ __launch_bounds__(1024) void k_sk_plan1(const int64_t* __restrict__ cnt_h, const int64_t* __restrict__ w_h,
+                                                   const int64_t* __restrict__ cnt_loc, const float* __restrict__ bounds,
+                                                   const int64_t* __restrict__ maxb, const float* __restrict__ vmax,
+                                                   SkPlan p) {
+  __shared__ int64_t s_C[kSkBuckets];
+  __shared__ uint8_t s_sel[kSkBuckets];
+  __shared__ int64_t s_w[16];
+  const int f = blockIdx.x, t = threadIdx.x;
+  const int64_t* ch = cnt_h + (int64_t)f * kSkBuckets;
+  const int64_t* wh = w_h ? w_h + (int64_t)f * kSkBuckets : ch;
+  const int64_t* cl = cnt_loc + (int64_t)f * kSkBuckets;
+  const int b0 = t * kSkPer;
+  int64_t v[kSkPer];
+  int64_t mine = 0, e = 0, o = 0;
+#pragma unroll
+  for (int q = 0; q < kSkPer; ++q) {
+    const int b = b0 + q;
+    v[q] = b < kSkBuckets ? wh[b] : 0;
+    mine += v[q];
+    if (b < kSkBuckets) {
+      s_sel[b] = 0;
+      if (ch[b] > 0) {
+        if (b & 1) ++e; else ++o;
+      }
+    }
+  }
+  int64_t W, E, O;
+  int64_t run = sk_block_excl(mine, s_w, W);
+#pragma unroll
+  for (int q = 0; q < kSkPer; ++q) {
+    run += v[q];
+    if (b0 + q < kSkBuckets) s_C[b0 + q] = run;
+  }
+  sk_block_excl(e, s_w, E);
+  sk_block_excl(o, s_w, O);  // (its barriers publish s_C and the zeroed s_sel)
+  const int64_t mb = maxb[f];
+  const bool many = E + O > mb, exact_known = O == 0 && E <= mb, uncertain = !many && O > 0;
+  int64_t need = 0;
+  if (t < kSkT) {
+    const int j = t + 1;
+    const int64_t th = (int64_t)j * W;
+    int lo = 0, hi = kSkBuckets;  // first bucket with C * maxb > j W (searchsorted right), clamped
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_C[mid] * mb > th) hi = mid; else lo = mid + 1;
+    }
+    const int bt = min(lo, kSkBuckets - 1);
+    const bool inb = j < mb, eq = (bt & 1) != 0;
+    const int qi = min(max((bt - 1) / 2, 0), kSkMaxBounds - 1);
+    const float q = W > 0 ? bounds[(int64_t)f * kSkMaxBounds + qi] : vmax[f];
+    need = (inb && !eq && W > 0 && !exact_known) ? 1 : 0;
+    const int64_t i = (int64_t)f * kSkT + t;
+    p.q0[i] = q;
+    p.thr[i] = th;
+    p.pre[i] = bt > 0 ? s_C[bt - 1] : 0;
+    p.tb[i] = bt;
+    p.need[i] = (uint8_t)need;
+    if (need) s_sel[bt] = 1;
+  }
+  __syncthreads();
+  if (t == 0) s_sel[kSkBuckets - 1] = 0;  // never a used bucket (m <= kSkMaxBounds - 1)
+  __syncthreads();
+  if (uncertain)
+    for (int b = t; b < kSkBuckets; b += blockDim.x)
+      if (!(b & 1) && ch[b] > 0) s_sel[b] = 1;
+  __syncthreads();
+  int64_t ns = 0, sl = 0, sg = 0;
+#pragma unroll
+  for (int q = 0; q < kSkPer; ++q) {
+    const int b = b0 + q;
+    if (b < kSkBuckets) {
+      const uint8_t s = s_sel[b];
+      p.sel[(int64_t)f * kSkBuckets + b] = s;
+      if (s) { ++ns; sl += cl[b]; sg += ch[b]; }
+    }
+  }
+  int64_t NS, NT, SL, SG;
+  sk_block_excl(ns, s_w, NS);
+  sk_block_excl(need, s_w, NT);
+  sk_block_excl(sl, s_w, SL);
+  sk_block_excl(sg, s_w, SG);
+  if (t == 0) {
+    int64_t* fs = p.fstat + 5LL * f;
+    fs[0] = NS;
+    fs[1] = NT;
+    fs[2] = SL;
+    fs[3] = SG;
+    fs[4] = uncertain ? 1 : 0;
+  }
+}
+
+// Plan 2 (one thread): the features' bases and the plan summary.
+__global__ void k_sk_plan2(int F, SkPlan p) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t a = 0, b = 0, c = 0, d = 0, u = 0;
+  for (int f = 0; f < F; ++f) {
+    const int64_t* fs = p.fstat + 5LL * f;
+    int64_t* fb = p.fbase + 4LL * f;
+    fb[0] = a; fb[1] = b; fb[2] = c; fb[3] = d;
+    a += fs[0]; b += fs[1]; c += fs[2]; d += fs[3];
+    u |= fs[4];
+  }
+  int64_t* s = p.summary;
+  s[0] = a; s[1] = b; s[2] = c; s[3] = d; s[4] = u; s[5] = 0; s[6] = 0; s[7] = 0;
+  p.loc_off[a] = c;
+  p.glob_off[a] = d;
+  p.tgt_off[a] = (int32_t)b;
+}
+
+// Plan 3, one block per feature: the global layout -- every bucket's segment (slot), the segments'
+// feature / bucket / local and global rows / offsets / first target / distinct-value request, the
+// open targets' global index (tpos) and k_sk_select arguments; big segments (beyond the LDS sort) are
+// counted in the summary for the host fallbacks.
+__global__ __launch_bounds__(1024) void k_sk_plan3(const int64_t* __restrict__ cnt_h, const int64_t* __restrict__ cnt_loc,
+                                                   const int64_t* __restrict__ maxb, SkPlan p) {
+  __shared__ int64_t s_w[16];
+  __shared__ int32_t s_tb[kSkT];
+  const int f = blockIdx.x, t = threadIdx.x;
+  const int64_t* ch = cnt_h + (int64_t)f * kSkBuckets;
+  const int64_t* cl = cnt_loc + (int64_t)f * kSkBuckets;
+  const int64_t* fb = p.fbase + 4LL * f;
+  const int64_t segbase = fb[0], tgtbase = fb[1], locbase = fb[2], globbase = fb[3];
+  const bool unc = p.fstat[5LL * f + 4] != 0;
+  const int64_t mb = maxb[f];
+  // open targets (ascending j, so ascending bucket)
+  const int64_t nd = t < kSkT ? p.need[(int64_t)f * kSkT + t] : 0;
+  int64_t nt;
+  const int64_t lt = sk_block_excl(nd, s_w, nt);
+  if (t < kSkT) {
+    const int64_t i = (int64_t)f * kSkT + t;
+    const int64_t g = tgtbase + lt;
+    p.tpos[i] = nd ? (int32_t)g : -1;
+    if (nd) {
+      p.tprefix[g] = p.pre[i];
+      p.tthr[g] = p.thr[i];
+      p.tmaxb[g] = mb;
+      s_tb[lt] = p.tb[i];
+    }
+  }
+  // selected buckets: segment index and row offsets
+  const int b0 = t * kSkPer;
+  int64_t ns = 0, sl = 0, sg = 0;
+  uint32_t selm = 0;
+#pragma unroll
+  for (int q = 0; q < kSkPer; ++q) {
+    const int b = b0 + q;
+    if (b < kSkBuckets && p.sel[(int64_t)f * kSkBuckets + b]) {
+      selm |= 1u << q;
+      ++ns;
+      sl += cl[b];
+      sg += ch[b];
+    }
+  }
+  int64_t tot;
+  int64_t es = sk_block_excl(ns, s_w, tot);
+  int64_t el = sk_block_excl(sl, s_w, tot);
+  int64_t eg = sk_block_excl(sg, s_w, tot);  // (its barriers publish s_tb)
+  const int T_f = (int)nt;
+#pragma unroll
+  for (int q = 0; q < kSkPer; ++q) {
+    const int b = b0 + q;
+    if (b >= kSkBuckets) break;
+    if (!((selm >> q) & 1u)) {
+      p.slot[(int64_t)f * kSkBuckets + b] = -1;
+      continue;
+    }
+    const int64_t s = segbase + es;
+    p.slot[(int64_t)f * kSkBuckets + b] = (int32_t)s;
+    p.seg_feat[s] = f;
+    p.seg_bucket[s] = b;
+    p.loc_sizes[s] = cl[b];
+    p.glob_sizes[s] = ch[b];
+    p.loc_off[s] = locbase + el;
+    p.glob_off[s] = globbase + eg;
+    p.want[s] = unc ? 1 : 0;
+    p.ndist[s] = -1;
+    int lo = 0, hi = T_f;  // first open target with bucket >= b
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_tb[mid] < b) lo = mid + 1; else hi = mid;
+    }
+    p.tgt_off[s] = (int32_t)(tgtbase + lo);
+    if (ch[b] > kSkSortCap) {  // beyond the LDS sort: the host takes its targets / distinct values
+      const bool has_t = lo < T_f && s_tb[lo] == b;
+      if (has_t) atomicAdd(reinterpret_cast<unsigned long long*>(p.summary + 5), 1ull);
+      if (unc) atomicAdd(reinterpret_cast<unsigned long long*>(p.summary + 6), 1ull);
+    }
+    ++es;
+    el += cl[b];
+    eg += ch[b];
+  }
+}
+
+// Pass-2 block offsets of one chunk: blk_off [nblk][nseg] = cursor + the exclusive prefix over the
+// blocks of the chunk's per-block rows of each segment (pass 1's slabs); cursor advances by them.
+__global__ __launch_bounds__(256) void k_sk_blkoff(SkPlan p, int nseg, int F, const uint32_t* __restrict__ cnt_slab,
+                                                   int nblk, int64_t* __restrict__ cursor, int64_t* __restrict__ blk_off) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  const int f = p.seg_feat[s], b = p.seg_bucket[s];
+  int64_t run = cursor[s];
+  for (int k = 0; k < nblk; ++k) {
+    blk_off[(int64_t)k * nseg + s] = run;
+    run += cnt_slab[((int64_t)k * F + f) * kSkBuckets + b];
+  }
+  cursor[s] = run;
+}
+
+// The cut tables, one 256-thread block per feature: q_j (the equal bucket's value, or the selected
+// candidate of an open target), the quantile path's de-duplicated cuts above the minimum, the exact
+// path's distinct values when the feature has <= maxb of them, the sentinel, -0 -> +0.
+__global__ __launch_bounds__(256) void k_sk_assemble(SkPlan p, const float* __restrict__ sel_out,
+                                                     const float* __restrict__ vmin, const int64_t* __restrict__ maxb,
+                                                     const int64_t* __restrict__ nd, const float* __restrict__ cuts_ex,
+                                                     float* __restrict__ cuts, int32_t* __restrict__ nbins) {
+  __shared__ float s_q[kSkT];
+  __shared__ float s_cut[256];
+  __shared__ int s_cnt[4];
+  const int f = blockIdx.x, t = threadIdx.x;
+  const int64_t mb = maxb[f];
+  float q = 0.0f;
+  if (t < kSkT) {
+    const int64_t i = (int64_t)f * kSkT + t;
+    const int tp = p.tpos[i];
+    q = tp >= 0 ? sel_out[tp] : p.q0[i];
+    s_q[t] = q;
+  }
+  s_cut[t] = FLT_MAX;
+  __syncthreads();
+  const bool keep = t < kSkT && (t + 1) < mb && q > vmin[f] && (t == 0 || q != s_q[t - 1]);
+  const uint64_t bal = __ballot(keep);
+  const int wv = wave_id();
+  if (lane_id() == 0) s_cnt[wv] = __popcll(bal);
+  __syncthreads();
+  int base = 0, K = 0;
+  for (int w = 0; w < 4; ++w) {
+    if (w < wv) base += s_cnt[w];
+    K += s_cnt[w];
+  }
+  if (keep) s_cut[base + mask_rank(bal)] = q;
+  __syncthreads();
+  const int64_t ndf = nd[f];
+  const bool exact = ndf >= 0 && ndf <= mb;
+  const int nbv = exact ? (int)(ndf > 0 ? ndf : 1) : K + 1;
+  float c = exact ? cuts_ex[(int64_t)f * 257 + t] : s_cut[t];
+  if (t == max(nbv - 1, 0)) c = FLT_MAX;
+  cuts[(int64_t)f * 256 + t] = c + 0.0f;
+  if (t == 0) nbins[f] = nbv;
+}
+
 }  // namespace
 
 // bid: nullptr, or [F][ldx] u16 -- every value's bucket for a later cobalt_sk_gather(.., bid) of the same rows
@@ -470,3 +997,94 @@ COBALT_API int cobalt_sk_select(const float* cval, const int32_t* cw, const int6
 COBALT_API int cobalt_sk_bounds() { return kSkMaxBounds; }
 COBALT_API int cobalt_sk_buckets() { return kSkBuckets; }
 COBALT_API int cobalt_sk_sort_cap() { return kSkSortCap; }
+
+// ---- the device planning (see k_sk_plan1) ----
+COBALT_API int cobalt_sk_bounds_build(const float* sv, int F, int S, float* bounds, int32_t* nbound, hipStream_t stream) {
+  if (F <= 0 || S <= 0) return -3;
+  hipLaunchKernelGGL(k_sk_bounds, dim3(F), dim3(1024), 0, stream, sv, S, bounds, nbound);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_sk_reduce(const uint32_t* cnt_slab, const void* w_slab, const float* bmm, int nblk, int F,
+                                int64_t* cnt, int64_t* wsum, float* vmin, float* vmax, hipStream_t stream) {
+  if (F <= 0 || nblk <= 0) return -3;
+  const dim3 grid((kSkBuckets + 255) / 256, F);
+  if (w_slab)
+    hipLaunchKernelGGL(k_sk_reduce<true>, grid, dim3(256), 0, stream, cnt_slab,
+                       static_cast<const unsigned long long*>(w_slab), bmm, nblk, F, cnt, wsum, vmin, vmax);
+  else
+    hipLaunchKernelGGL(k_sk_reduce<false>, grid, dim3(256), 0, stream, cnt_slab, nullptr, bmm, nblk, F, cnt, wsum, vmin,
+                       vmax);
+  CK_LAUNCH();
+  return 0;
+}
+
+// int64 word offsets of the plan's arrays inside its workspace (kSkArrCount + 1 entries, the last = the
+// workspace size), in SkArr order.
+COBALT_API int cobalt_sk_plan_layout(int F, int64_t* off) {
+  if (F <= 0) return -3;
+  sk_plan_layout(F, off);
+  return kSkArrCount;
+}
+
+// Plan 1-3 over the (global) bucket tables, then ONE host read of the summary (8 int64 to `summary_host`).
+// w_h: nullptr = unit weights (cnt_h); cnt_loc: this rank's counts (== cnt_h on one rank).
+COBALT_API int cobalt_sk_plan(int F, const int64_t* cnt_h, const int64_t* w_h, const int64_t* cnt_loc, const float* bounds,
+                              const int64_t* maxb, const float* vmax, int64_t* ws, int64_t* summary_host,
+                              hipStream_t stream) {
+  if (F <= 0) return -3;
+  const SkPlan p = sk_plan_views(F, ws);
+  hipLaunchKernelGGL(k_sk_plan1, dim3(F), dim3(1024), 0, stream, cnt_h, w_h, cnt_loc, bounds, maxb, vmax, p);
+  CK_LAUNCH();
+  hipLaunchKernelGGL(k_sk_plan2, dim3(1), dim3(64), 0, stream, F, p);
+  CK_LAUNCH();
+  hipLaunchKernelGGL(k_sk_plan3, dim3(F), dim3(1024), 0, stream, cnt_h, cnt_loc, maxb, p);
+  CK_LAUNCH();
+  static int64_t* pinned = nullptr;
+  if (!pinned) CK(hipHostMalloc((void**)&pinned, 8 * sizeof(int64_t), hipHostMallocDefault));
+  CK(hipMemcpyAsync(pinned, p.summary, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  for (int i = 0; i < 8; ++i) summary_host[i] = pinned[i];
+  return 0;
+}
+
+COBALT_API int cobalt_sk_blkoff(int F, int64_t* ws, int nseg, const uint32_t* cnt_slab, int nblk, int64_t* cursor,
+                                int64_t* blk_off, hipStream_t stream) {
+  if (F <= 0 || nblk <= 0) return -3;
+  if (nseg <= 0) return 0;
+  hipLaunchKernelGGL(k_sk_blkoff, dim3((nseg + 255) / 256), dim3(256), 0, stream, sk_plan_views(F, ws), nseg, F, cnt_slab,
+                     nblk, cursor, blk_off);
+  CK_LAUNCH();
+  return 0;
+}
+
+// sel_out: k_sk_select's answers by global target index (nullptr when there are no open targets);
+// nd / cuts_ex: k_sk_exact's (after any host fallback). cuts [F][256], nbins [F] int32.
+COBALT_API int cobalt_sk_assemble(int F, int64_t* ws, const float* sel_out, const float* vmin, const int64_t* maxb,
+                                  const int64_t* nd, const float* cuts_ex, float* cuts, int32_t* nbins, hipStream_t stream) {
+  if (F <= 0) return -3;
+  hipLaunchKernelGGL(k_sk_assemble, dim3(F), dim3(256), 0, stream, sk_plan_views(F, ws), sel_out, vmin, maxb, nd, cuts_ex,
+                     cuts, nbins);
+  CK_LAUNCH();
+  return 0;
+}
+
+// Boundaries from the strided sample without a torch sort (k_sk_sample_bounds); -4: S beyond the LDS sort.
+COBALT_API int cobalt_sk_sample_bounds(const float* X, int64_t srow, int64_t scol, int S, int F, float* bounds,
+                                       int32_t* nbound, hipStream_t stream) {
+  if (F <= 0 || S <= 0) return -3;
+  if (S > kSkSampleCap) return -4;
+  static bool attr = false;
+  if (!attr) {
+    CK(hipFuncSetAttribute((const void*)k_sk_sample_bounds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)(kSkSampleCap * sizeof(uint32_t))));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_sk_sample_bounds, dim3(F), dim3(1024), (size_t)kSkSampleCap * sizeof(uint32_t), stream, X, srow,
+                     scol, S, bounds, nbound);
+  CK_LAUNCH();
+  return 0;
+}
+
+COBALT_API int cobalt_sk_sample_cap() { return kSkSampleCap; }

@@ -49,6 +49,9 @@ FLT_MAX = float(np.finfo(np.float32).max)
 MAX_BINS = 256        # bins of a feature without missing values (uint8 codes 0..255)
 MAX_BINS_U8 = 255     # bins of a feature with missing values (code 255 = missing)
 WEIGHT_SCALE = 1 << 20
+# rows of the strided sample whose order statistics bound the exact device sketch's buckets (any sample
+# gives the same cuts; <= 32768 rows per feature sort in LDS in one kernel, csrc/sketch.hip)
+BOUNDARY_SAMPLE_ROWS = 1 << 15
 
 
 def sample_stride(n_global: int, sketch_rows: int) -> int:
@@ -385,7 +388,21 @@ def _sk_lib():
         lib.cobalt_sk_transpose.argtypes = [V, I64, I, V, V]
         lib.cobalt_sk_exact.restype = I
         lib.cobalt_sk_exact.argtypes = [I, V, V, V, V, V, V, V, V, V, V]
-        for name in ("cobalt_sk_bounds", "cobalt_sk_buckets", "cobalt_sk_sort_cap"):
+        lib.cobalt_sk_bounds_build.restype = I
+        lib.cobalt_sk_bounds_build.argtypes = [V, I, I, V, V, V]
+        lib.cobalt_sk_reduce.restype = I
+        lib.cobalt_sk_reduce.argtypes = [V, V, V, I, I, V, V, V, V, V]
+        lib.cobalt_sk_plan_layout.restype = I
+        lib.cobalt_sk_plan_layout.argtypes = [I, V]
+        lib.cobalt_sk_plan.restype = I
+        lib.cobalt_sk_plan.argtypes = [I, V, V, V, V, V, V, V, V, V]
+        lib.cobalt_sk_blkoff.restype = I
+        lib.cobalt_sk_blkoff.argtypes = [I, V, I, V, I, V, V, V]
+        lib.cobalt_sk_assemble.restype = I
+        lib.cobalt_sk_assemble.argtypes = [I, V, V, V, V, V, V, V, V, V]
+        lib.cobalt_sk_sample_bounds.restype = I
+        lib.cobalt_sk_sample_bounds.argtypes = [V, I64, I64, I, I, V, V, V]
+        for name in ("cobalt_sk_bounds", "cobalt_sk_buckets", "cobalt_sk_sort_cap", "cobalt_sk_sample_cap"):
             getattr(lib, name).restype = I
             getattr(lib, name).argtypes = []
         lib._sk_declared = True
@@ -399,7 +416,7 @@ def _ptr(t):
 def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor | None = None,
                       has_missing: torch.Tensor | None = None, *, dist=None, row_offset: int = 0,
                       n_rows_global: int | None = None, w_max: float | None = None,
-                      sample_rows: int = 1 << 16) -> tuple[torch.Tensor, torch.Tensor]:
+                      sample_rows: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """:func:`compute_cuts` over EVERY row of ``X`` [N, F] (a CUDA tensor), bit for bit, without sorting
     the rows (csrc/sketch.hip): sample boundaries split each feature's value axis into buckets, one
     pass histograms the rows per bucket, the target ranks are located by prefix sums, and only the
@@ -428,7 +445,7 @@ def device_exact_cuts(X: torch.Tensor, max_bin: int = 256, weights: torch.Tensor
     world = dist.world if dist is not None else 1
     n_glob = n_rows_global if n_rows_global is not None else N
     X = X.to(torch.float32)
-    stride = sample_stride(n_glob, sample_rows)
+    stride = sample_stride(n_glob, BOUNDARY_SAMPLE_ROWS if sample_rows is None else sample_rows)
     samp = local_sample(X, row_offset, stride)
     wd = weights.to(device=dev, dtype=torch.float64).reshape(-1) if weights is not None else None
     if wd is not None:
@@ -568,132 +585,138 @@ def _sk_transpose(lib, X, stream):
     return X.t().contiguous()
 
 
+# the device plan's arrays, in the order of csrc/sketch.hip SkArr (their int64 word offsets inside the
+# plan workspace come from cobalt_sk_plan_layout)
+_PLAN_ARRS = ("sel", "fstat", "fbase", "summary", "q0", "thr", "pre", "tb", "need", "slot", "seg_feat", "seg_bucket",
+              "loc_sizes", "glob_sizes", "loc_off", "glob_off", "tgt_off", "want", "ndist", "tpos", "tprefix", "tthr",
+              "tmaxb")
+_plan_offsets: dict = {}
+
+
+def _plan_layout(lib, F: int) -> list:
+    off = _plan_offsets.get(F)
+    if off is None:
+        import ctypes
+
+        buf = (ctypes.c_int64 * (len(_PLAN_ARRS) + 1))()
+        n = lib.cobalt_sk_plan_layout(F, ctypes.addressof(buf))
+        if n != len(_PLAN_ARRS):
+            raise RuntimeError(f"cobalt_sk_plan_layout: {n} arrays, expected {len(_PLAN_ARRS)}")
+        off = _plan_offsets[F] = list(buf)
+    return off
+
+
 def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, weighted, mark, marks, timing):
     """The bucketed exact sketch over the rows of ``chunks()`` ((X_chunk, int32 weights or None)
-    pairs; ``single``: one chunk, its transpose and pass-1 slabs are reused by the gather)."""
+    pairs; ``single``: one chunk, its transpose and pass-1 slabs are reused by the gather).
+
+    Everything between the passes runs on the device (csrc/sketch.hip: k_sk_bounds, k_sk_reduce,
+    k_sk_plan1-3, k_sk_blkoff, k_sk_assemble) with ONE host read -- the plan's sizes, which the candidate
+    buffers and the collectives need; only the rare fallbacks (a segment beyond the LDS sort) run torch
+    code here."""
+    import ctypes
+
     from .. import _native
 
     lib = _sk_lib()
+    if F == 0:
+        return (torch.empty((0, 256), dtype=torch.float32, device=dev), torch.empty(0, dtype=torch.int32, device=dev))
     world = dist.world if dist is not None else 1
     NBND, NB, CAP = lib.cobalt_sk_bounds(), lib.cobalt_sk_buckets(), lib.cobalt_sk_sort_cap()
     stream = _native.stream_handle()
-    maxb = feature_max_bins(max_bin, has_missing.to(dev))                            # [F] int64
+    chk = _native.check
+    maxb = feature_max_bins(max_bin, has_missing.to(dev)).contiguous()              # [F] int64
 
-    # 1. boundaries: <= NBND - 1 distinct values of the global strided sample
-    sv = torch.sort((samp.t() + 0.0).contiguous(), dim=1).values                     # [F, S], NaN last
-    mark("sort")
-    S = sv.shape[1]
-    K = NBND - 1
-    cnt = (~torch.isnan(sv)).sum(1)
-    bounds = torch.full((F, NBND + 1), float("inf"), dtype=torch.float32, device=dev)
-    if S:
-        pos = (torch.arange(K, device=dev)[None, :] * cnt[:, None]) // K
-        u = sv.gather(1, pos.clamp(max=S - 1))
-        ok = pos < cnt[:, None]
-        newv = ok.clone()
-        newv[:, 1:] &= u[:, 1:] != u[:, :-1]
-        slotp = torch.where(newv, torch.cumsum(newv.to(torch.int64), 1) - 1, NBND)
-        bounds.scatter_(1, slotp, u)
-        m = newv.sum(1).to(torch.int32)
+    # 1. boundaries: <= NBND - 1 distinct values of the global strided sample -- sorted in LDS straight
+    # from the (strided) sample view (k_sk_sample_bounds), or torch.sort + k_sk_bounds beyond its cap
+    S = samp.shape[0]
+    bounds = torch.empty((F, NBND), dtype=torch.float32, device=dev)
+    m = torch.empty(F, dtype=torch.int32, device=dev)
+    if 0 < S <= lib.cobalt_sk_sample_cap():
+        sp = samp if samp.dtype == torch.float32 else samp.to(torch.float32)
+        chk(lib.cobalt_sk_sample_bounds(sp.data_ptr(), sp.stride(0), sp.stride(1), S, F, bounds.data_ptr(),
+                                        m.data_ptr(), stream), "cobalt_sk_sample_bounds")
+        mark("sort")
+    elif S:
+        sv = torch.sort((samp.t() + 0.0).contiguous(), dim=1).values                 # [F, S], NaN last
+        mark("sort")
+        chk(lib.cobalt_sk_bounds_build(sv.data_ptr(), F, S, bounds.data_ptr(), m.data_ptr(), stream),
+            "cobalt_sk_bounds_build")
     else:
-        m = torch.zeros(F, dtype=torch.int32, device=dev)
-    bounds = bounds[:, :NBND].contiguous()
+        bounds.fill_(float("inf"))
+        m.zero_()
     mark("bounds")
 
-    # 2. bucket histograms (row counts; weight sums when weighted) + min / max valid value, per chunk
+    # 2. bucket histograms (row counts; weight sums when weighted) + min / max valid value, per chunk;
+    # the slabs are summed on the device (k_sk_reduce)
     def chunk_hist(XT, n, wq, bid=None):
         nblk = max(1, min(64, -(-n // 65536)))
-        cnt_slab = torch.zeros((nblk, F, NB), dtype=torch.int32, device=dev)
-        w_slab = torch.zeros((nblk, F, NB), dtype=torch.int64, device=dev) if wq is not None else None
+        cnt_slab = torch.empty((nblk, F, NB), dtype=torch.int32, device=dev)
+        w_slab = torch.empty((nblk, F, NB), dtype=torch.int64, device=dev) if wq is not None else None
         bmm = torch.empty((nblk, F, 2), dtype=torch.float32, device=dev)
-        bmm[:, :, 0] = float("inf")
-        bmm[:, :, 1] = float("-inf")
         if n:
             rc = lib.cobalt_sk_hist(XT.data_ptr(), n, n, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(), nblk,
                                     cnt_slab.data_ptr(), _ptr(w_slab), bmm.data_ptr(), _ptr(bid), stream)
-            _native.check(rc, "cobalt_sk_hist")
+            chk(rc, "cobalt_sk_hist")
         return nblk, cnt_slab, w_slab, bmm
 
     cnt_loc = torch.zeros((F, NB), dtype=torch.int64, device=dev)
-    w_h = torch.zeros((F, NB), dtype=torch.int64, device=dev) if weighted else None
+    w_loc = torch.zeros((F, NB), dtype=torch.int64, device=dev) if weighted else None
     vmin = torch.full((F,), float("inf"), dtype=torch.float32, device=dev)
     vmax = torch.full((F,), float("-inf"), dtype=torch.float32, device=dev)
     kept = None
     for Xc, wq in chunks():
         Xc = Xc.to(torch.float32)
+        n = Xc.shape[0]
         XT = _sk_transpose(lib, Xc, stream)
         mark("transpose")
         # one chunk (the in-core sketch): pass 1 also keeps every value's bucket, so the candidate pass
         # reads 2 bytes per value instead of searching the boundaries again
-        bid = torch.empty((F, Xc.shape[0]), dtype=torch.int16, device=dev) if single and Xc.shape[0] else None
-        nblk, cnt_slab, w_slab, bmm = chunk_hist(XT, Xc.shape[0], wq, bid)
-        cnt_loc += cnt_slab.sum(0, dtype=torch.int64)
-        if w_h is not None:
-            w_h += w_slab.sum(0)
-        vmin = torch.minimum(vmin, bmm[:, :, 0].amin(0))
-        vmax = torch.maximum(vmax, bmm[:, :, 1].amax(0))
+        bid = torch.empty((F, n), dtype=torch.int16, device=dev) if single and n else None
+        nblk, cnt_slab, w_slab, bmm = chunk_hist(XT, n, wq, bid)
+        if n:
+            chk(lib.cobalt_sk_reduce(cnt_slab.data_ptr(), _ptr(w_slab), bmm.data_ptr(), nblk, F, cnt_loc.data_ptr(),
+                                     _ptr(w_loc), vmin.data_ptr(), vmax.data_ptr(), stream), "cobalt_sk_reduce")
         if single:
-            kept = (XT, Xc.shape[0], wq, nblk, cnt_slab, bid)
-    cnt_h = cnt_loc
+            kept = (XT, n, wq, nblk, cnt_slab, bid)
+    cnt_h, w_h = cnt_loc, w_loc
     if world > 1:  # collective 2
-        cnt_h, w_h, vmin, vmax = _allreduce_buckets(dist, dev, cnt_loc, w_h, vmin, vmax)
-    if w_h is None:
-        w_h = cnt_h
+        cnt_h, w_h, vmin, vmax = _allreduce_buckets(dist, dev, cnt_loc, w_loc, vmin, vmax)
+    cnt_h, vmin, vmax = cnt_h.contiguous(), vmin.contiguous(), vmax.contiguous()
     mark("hist")
 
-    # 3. targets: bucket of every rank j * W / maxb; equal buckets ARE their value
-    C = torch.cumsum(w_h, 1)
-    W = C[:, -1]
-    jj = torch.arange(1, MAX_BINS, device=dev, dtype=torch.int64)                      # j = 1..255
-    thr = jj[None, :] * W[:, None]
-    b = torch.searchsorted((C * maxb[:, None]).contiguous(), thr.contiguous(), right=True).clamp(max=NB - 1)
-    inb = jj[None, :] < maxb[:, None]
-    eq_t = (b % 2) == 1
-    q = bounds.gather(1, ((b - 1) // 2).clamp(0, NBND - 1))
-    q = torch.where(W[:, None] > 0, q, vmax[:, None])                                  # W == 0: compute_cuts' clamp
-    nz = cnt_h > 0
-    E = nz[:, 1::2].sum(1)
-    O = nz[:, 0::2].sum(1)
-    many = (E + O) > maxb
-    exact_known = (O == 0) & (E <= maxb)
-    uncertain = (~many) & (O > 0)
-    need_t = inb & ~eq_t & (W[:, None] > 0) & ~exact_known[:, None]
-    sel = torch.zeros((F, NB), dtype=torch.bool, device=dev)
-    sel.scatter_(1, torch.where(need_t, b, NB - 1), True)
-    sel[:, NB - 1] = False  # (never a used bucket: m <= NBND - 1, so buckets end at 2m <= NB - 3)
-    even = (torch.arange(NB, device=dev) % 2) == 0
-    sel |= uncertain[:, None] & nz & even[None, :]
-    sel_f = sel.reshape(-1)
-    seg_of = torch.cumsum(sel_f.to(torch.int64), 0) - 1
-    slot = torch.where(sel_f, seg_of, -1).to(torch.int32).contiguous()
-    seg_feat = torch.nonzero(sel_f).reshape(-1) // NB                                  # feature of every segment
-    loc_sizes = cnt_loc.reshape(-1)[sel_f]                                             # this rank's rows per segment
-    glob_sizes = cnt_h.reshape(-1)[sel_f]
-    nseg = int(loc_sizes.numel())
-    loc_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
-    if nseg:
-        loc_off[1:] = torch.cumsum(loc_sizes, 0)
-    glob_off = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
-    if nseg:
-        glob_off[1:] = torch.cumsum(glob_sizes, 0)
+    # 3. the plan (k_sk_plan1-3): targets j * W / maxb, their buckets (an equal bucket IS the value), the
+    # selected open buckets as segments with their local / global offsets; one host read of the sizes
+    off = _plan_layout(lib, F)
+    ws = torch.empty(off[-1], dtype=torch.int64, device=dev)
+
+    def arr(name, dtype, count):
+        k = _PLAN_ARRS.index(name)
+        return ws[off[k]:off[k + 1]].view(dtype)[:count]
+
+    summ = (ctypes.c_int64 * 8)()
+    chk(lib.cobalt_sk_plan(F, cnt_h.data_ptr(), _ptr(w_h), cnt_loc.data_ptr(), bounds.data_ptr(), maxb.data_ptr(),
+                           vmax.data_ptr(), ws.data_ptr(), ctypes.addressof(summ), stream), "cobalt_sk_plan")
+    nseg, T, tot_loc, tot_glob, any_unc, nbig_t, nbig_w = (int(x) for x in summ[:7])
+    slot = arr("slot", torch.int32, F * NB)
+    glob_off = arr("glob_off", torch.int64, nseg + 1)
     mark("targets")
 
     # 4. candidates: the rows of the selected buckets, per segment (a second walk over the chunks;
-    # each block writes at its offset from the chunk's per-block bucket counts). Data parallel: straight
-    # into the GLOBAL segment layout (this rank's rows of segment s start at glob_off[s] + the lower
-    # ranks' rows of s), zeros elsewhere, and collective 3 sums the ranks' buffers: values and weights
-    # in one int32 buffer [tot | tot].
+    # each block writes at its offset from the chunk's per-block bucket counts, k_sk_blkoff). Data
+    # parallel: straight into the GLOBAL segment layout (this rank's rows of segment s start at
+    # glob_off[s] + the lower ranks' rows of s), zeros elsewhere, and collective 3 sums the ranks'
+    # buffers: values and weights in one int32 buffer [tot | tot].
     if world > 1:
-        tot_loc = tot = int(glob_off[-1])
+        tot_loc = tot = tot_glob
         cbuf = torch.zeros(max(2 * tot if weighted else tot, 1), dtype=torch.int32, device=dev)
         cval = cbuf[:max(tot, 1)].view(torch.float32)
         cw = cbuf[tot:2 * tot] if weighted else None
-        start = glob_off[:-1] + _segment_offsets(dist, dev, loc_sizes)  # collective 2b
+        start = glob_off[:-1] + _segment_offsets(dist, dev, arr("loc_sizes", torch.int64, nseg))  # collective 2b
     else:
-        tot_loc = int(loc_off[-1])
         cval = torch.empty(max(tot_loc, 1), dtype=torch.float32, device=dev)
         cw = torch.empty(max(tot_loc, 1), dtype=torch.int32, device=dev) if weighted else None
-        start = loc_off[:-1]
+        start = arr("loc_off", torch.int64, nseg + 1)[:-1]
     if nseg and N:
         cursor = start.clone()
         for Xc, wq in (iter([(None, None)]) if single else chunks()):
@@ -707,89 +730,74 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
                 nblk, cnt_slab, _, _ = chunk_hist(XT, n, wq)
             if not n:
                 continue
-            per_blk = cnt_slab.reshape(nblk, -1)[:, sel_f].to(torch.int64)                # [nblk, nseg]
-            blk_off = (torch.cumsum(per_blk, 0) - per_blk + cursor[None, :]).contiguous()
+            blk_off = torch.empty((nblk, nseg), dtype=torch.int64, device=dev)
+            chk(lib.cobalt_sk_blkoff(F, ws.data_ptr(), nseg, cnt_slab.data_ptr(), nblk, cursor.data_ptr(),
+                                     blk_off.data_ptr(), stream), "cobalt_sk_blkoff")
             rc = lib.cobalt_sk_gather(XT.data_ptr(), n, n, F, _ptr(wq), bounds.data_ptr(), m.data_ptr(),
                                       slot.data_ptr(), blk_off.data_ptr(), nseg, cval.data_ptr(), _ptr(cw), nblk,
                                       _ptr(bid), stream)
-            _native.check(rc, "cobalt_sk_gather")
-            cursor += per_blk.sum(0)
+            chk(rc, "cobalt_sk_gather")
     if world > 1 and nseg:  # collective 3: every rank's candidates, already in the global layout
         dist.device_allreduce(cbuf, "sum")
 
     mark("gather")
-    # 5. select the open targets from their bucket's sorted candidates
-    tf, tj = torch.nonzero(need_t, as_tuple=True)
-    T = int(tf.numel())
-    # segments of the features that may be exact (one bin per distinct value): their distinct values
-    want = uncertain[seg_feat].to(torch.uint8).contiguous() if nseg else None
-    ndist = torch.full((max(nseg, 1),), -1, dtype=torch.int32, device=dev)
+    # 5. select the open targets from their bucket's sorted candidates (k_sk_select); for the features
+    # that may be exact (one bin per distinct value), also their segments' distinct values
+    out = torch.empty(max(T, 1), dtype=torch.float32, device=dev)
+    ndist = arr("ndist", torch.int32, max(nseg, 1))
     dval = torch.empty_like(cval)
-    if T or (nseg and bool(uncertain.any())):
-        tb = b[tf, tj]
-        tseg = slot.reshape(F, NB)[tf, tb].to(torch.int64)
-        tgt_off = torch.zeros(nseg + 1, dtype=torch.int32, device=dev)
-        if T:
-            tgt_off[1:] = torch.cumsum(torch.bincount(tseg, minlength=nseg), 0).to(torch.int32)
-        prefix = torch.where(tb > 0, C[tf, (tb - 1).clamp(min=0)], torch.zeros_like(tb)).contiguous()
-        tthr = thr[tf, tj].contiguous()
-        tmaxb = maxb[tf].contiguous()
-        out = torch.empty(T, dtype=torch.float32, device=dev)
+    if nseg and (T or any_unc):
+        tgt_off = arr("tgt_off", torch.int32, nseg + 1)
+        prefix = arr("tprefix", torch.int64, T)
+        tthr = arr("tthr", torch.int64, T)
+        tmaxb = arr("tmaxb", torch.int64, T)
         rc = lib.cobalt_sk_select(cval.data_ptr(), _ptr(cw), glob_off.data_ptr(), nseg, tgt_off.data_ptr(),
-                                  prefix.data_ptr(), tthr.data_ptr(), tmaxb.data_ptr(), out.data_ptr(), _ptr(want),
-                                  dval.data_ptr(), ndist.data_ptr(), stream)
-        _native.check(rc, "cobalt_sk_select")
-        big = torch.nonzero(glob_sizes > CAP).reshape(-1).tolist()  # rare: segments beyond the LDS sort
-        for s in big:
-            t0, t1 = int(tgt_off[s]), int(tgt_off[s + 1])
-            if t0 == t1:
-                continue
-            o0, o1 = int(glob_off[s]), int(glob_off[s + 1])
-            vs, order = torch.sort(cval[o0:o1])
-            ws = (cw[o0:o1][order].to(torch.int64) if cw is not None else torch.ones_like(order))
-            cum = torch.cumsum(ws, 0)
-            key = ((prefix[t0:t1, None] + cum[None, :]) * tmaxb[t0:t1, None]).contiguous()
-            i = torch.searchsorted(key, tthr[t0:t1, None].contiguous(), right=True)[:, 0].clamp(max=o1 - o0 - 1)
-            out[t0:t1] = vs[i]
-        if T:
-            q[tf, tj] = out
+                                  prefix.data_ptr(), tthr.data_ptr(), tmaxb.data_ptr(), out.data_ptr(),
+                                  arr("want", torch.uint8, nseg).data_ptr(), dval.data_ptr(), ndist.data_ptr(), stream)
+        chk(rc, "cobalt_sk_select")
+        if nbig_t:  # rare: segments beyond the LDS sort with targets -- sorted here
+            glob_sizes = arr("glob_sizes", torch.int64, nseg)
+            for s in torch.nonzero(glob_sizes > CAP).reshape(-1).tolist():
+                t0, t1 = int(tgt_off[s]), int(tgt_off[s + 1])
+                if t0 == t1:
+                    continue
+                o0, o1 = int(glob_off[s]), int(glob_off[s + 1])
+                vs, order = torch.sort(cval[o0:o1])
+                ws_ = (cw[o0:o1][order].to(torch.int64) if cw is not None else torch.ones_like(order))
+                cum = torch.cumsum(ws_, 0)
+                key = ((prefix[t0:t1, None] + cum[None, :]) * tmaxb[t0:t1, None]).contiguous()
+                i = torch.searchsorted(key, tthr[t0:t1, None].contiguous(), right=True)[:, 0].clamp(max=o1 - o0 - 1)
+                out[t0:t1] = vs[i]
 
     mark("select")
-    # 6. the cut tables, as compute_cuts assembles them
-    trash = torch.full((F, 257), FLT_MAX, dtype=torch.float32, device=dev)
-    keep = inb & (q > vmin[:, None])
-    keep[:, 1:] &= q[:, 1:] != q[:, :-1]
-    qpos = torch.cumsum(keep.to(torch.int64), 1) - 1
-    cuts_q = trash.clone().scatter_(1, torch.where(keep, qpos, 256), q)
-    nbq = keep.sum(1) + 1
-    # exact path: one bin per distinct value (the sample's values that occur, + for the uncertain
-    # features the distinct values of their open buckets)
-    cuts_ex = trash.clone()
+    # 6. the cut tables (k_sk_exact: one bin per distinct value where a feature has <= maxb of them;
+    # k_sk_assemble: the quantile path, the choice between them, the sentinel)
+    cuts_ex = torch.full((F, 257), FLT_MAX, dtype=torch.float32, device=dev)
     nd = torch.empty(F, dtype=torch.int64, device=dev)
-    _native.check(lib.cobalt_sk_exact(F, cnt_h.contiguous().data_ptr(), bounds.data_ptr(), slot.data_ptr(),
-                                      glob_off.data_ptr(), ndist.data_ptr(), dval.data_ptr(), maxb.contiguous().data_ptr(),
-                                      cuts_ex.data_ptr(), nd.data_ptr(), stream), "cobalt_sk_exact")
-    exact = (nd >= 0) & (nd <= maxb)
-    # rare: an exact-candidate feature with a segment beyond the LDS sort -- its distinct values on the host
-    for f in torch.nonzero(uncertain & (nd < 0)).reshape(-1).tolist():
-        eqnz = nz[f, 1::2][:NBND]
-        segs = torch.nonzero(slot.reshape(F, NB)[f] >= 0).reshape(-1)
-        parts = [bounds[f][eqnz]]
-        for bb in segs.tolist():
-            s = int(slot.reshape(F, NB)[f, bb])
-            parts.append(cval[int(glob_off[s]):int(glob_off[s + 1])])
-        dv = torch.unique(torch.cat(parts))                                            # sorted
-        nd[f] = dv.numel()
-        if dv.numel() <= int(maxb[f]):
-            exact[f] = True
-            row = torch.full((257,), FLT_MAX, dtype=torch.float32, device=dev)
-            row[: dv.numel() - 1] = dv[1:]
-            cuts_ex[f] = row
-    nb_ex = torch.where(nd > 0, nd, torch.ones_like(nd))
-    cuts = torch.where(exact[:, None], cuts_ex[:, :256], cuts_q[:, :256]).contiguous()
-    nbv = torch.where(exact, nb_ex, nbq)
-    cuts.scatter_(1, (nbv - 1).clamp(min=0)[:, None], FLT_MAX)
-    out = cuts + 0.0, nbv.to(torch.int32)
+    chk(lib.cobalt_sk_exact(F, cnt_h.data_ptr(), bounds.data_ptr(), slot.data_ptr(), glob_off.data_ptr(),
+                            ndist.data_ptr(), dval.data_ptr(), maxb.data_ptr(), cuts_ex.data_ptr(), nd.data_ptr(),
+                            stream), "cobalt_sk_exact")
+    if nbig_w:  # rare: an exact-candidate feature with a segment beyond the LDS sort -- distinct values here
+        uncertain = arr("fstat", torch.int64, 5 * F).view(F, 5)[:, 4] > 0
+        nz = cnt_h > 0
+        slot2 = slot.view(F, NB)
+        for f in torch.nonzero(uncertain & (nd < 0)).reshape(-1).tolist():
+            eqnz = nz[f, 1::2][:NBND]
+            segs = torch.nonzero(slot2[f] >= 0).reshape(-1)
+            parts = [bounds[f][eqnz]]
+            for bb in segs.tolist():
+                s = int(slot2[f, bb])
+                parts.append(cval[int(glob_off[s]):int(glob_off[s + 1])])
+            dv = torch.unique(torch.cat(parts))                                            # sorted
+            nd[f] = dv.numel()
+            if dv.numel() <= int(maxb[f]):
+                row = torch.full((257,), FLT_MAX, dtype=torch.float32, device=dev)
+                row[: dv.numel() - 1] = dv[1:]
+                cuts_ex[f] = row
+    cuts = torch.empty((F, 256), dtype=torch.float32, device=dev)
+    nbv = torch.empty(F, dtype=torch.int32, device=dev)
+    chk(lib.cobalt_sk_assemble(F, ws.data_ptr(), out.data_ptr(), vmin.data_ptr(), maxb.data_ptr(), nd.data_ptr(),
+                               cuts_ex.data_ptr(), cuts.data_ptr(), nbv.data_ptr(), stream), "cobalt_sk_assemble")
     mark("assemble")
     if timing:
         import sys
@@ -797,6 +805,6 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
         print("[sketch] " + " ".join(f"{marks[i][0]}={1e3 * (marks[i][1] - marks[i - 1][1]):.3f}ms"
                                      for i in range(1, len(marks))) + f" candidates={tot_loc} segments={nseg}",
               file=sys.stderr)
-    return out
+    return cuts, nbv
 
 

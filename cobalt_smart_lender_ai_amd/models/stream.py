@@ -107,7 +107,7 @@ def stream_cuts(source: ChunkSource, *, n_rows: int | None = None, max_bin: int 
     exact_dev = dev.type == "cuda" and (sketch_rows is None or sketch_rows == 0 or
                                         (sketch_rows < 0 and n_glob > SKETCH_SAMPLE_ROWS))
     if exact_dev:  # the boundary sample of sketch.device_exact_cuts (same global rows)
-        stride = sketch.sample_stride(n_glob, 1 << 16)
+        stride = sketch.sample_stride(n_glob, sketch.BOUNDARY_SAMPLE_ROWS)
     else:
         if sketch_rows is not None and sketch_rows < 0:
             sketch_rows = SKETCH_SAMPLE_ROWS
