@@ -591,10 +591,28 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                 cr = int(knob("COBALT_FAULT_CORRUPT_RANK", "-1") or -1)
                 if cr == dist.rank:
                     tr.set_fault(int(knob("COBALT_FAULT_CORRUPT_TREE", "1") or 1))
-            for s0 in range(T0, T, seg):
-                s1 = min(T, s0 + seg)
-                tr.grow(s0, s1 - s0)
+            head = None
+            if checkpoint is None and T - T0 >= 64:
+                # Two grow calls: the first part's trees are fetched (on a side stream) and converted on
+                # the host while the GPU grows the last ones -- the host's ~1 ms per 300 trees of
+                # fetch + conversion leaves the fit's critical path.
+                tail = min(32, (T - T0) // 4)
+                head = T - tail
+                tr.grow(T0, head - T0)
+                ev = torch.cuda.Event()
+                ev.record()
+                tr.grow(head, T - head)
                 rep.extra["plan"] = tr.plan()
+                if world > 1:
+                    _watch_segment(dist, dev, T0, head, tr, ev)
+                else:
+                    ev.synchronize()
+                trees_so_far.extend(trees_from_heap_nodes(tr.fetch(T0, head - T0, _side_stream(dev)), hp.max_depth))
+            for s0 in ([head] if head is not None else range(T0, T, seg)):
+                s1 = min(T, s0 + seg)
+                if head is None:
+                    tr.grow(s0, s1 - s0)
+                    rep.extra["plan"] = tr.plan()
                 if world > 1:  # fail fast (abort the communicator) if a peer rank dies mid-segment
                     _watch_segment(dist, dev, s0, s1, tr)
                 tp = rep.mark("grow", tp, dev)
@@ -644,12 +662,26 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     return bst
 
 
-def _watch_segment(dist, dev, s0: int, s1: int, tr=None) -> None:
+_side_streams: dict = {}
+
+
+def _side_stream(dev) -> torch.cuda.Stream:
+    """A second stream of ``dev`` (created once) for copies that must not wait on the trainer's stream."""
+    key = torch.device(dev).index or 0
+    if key not in _side_streams:
+        _side_streams[key] = torch.cuda.Stream(torch.device("cuda", key))
+    return _side_streams[key]
+
+
+def _watch_segment(dist, dev, s0: int, s1: int, tr=None, ev=None) -> None:
+    """Wait for trees [s0, s1) -- the work before ``ev`` (default: everything enqueued so far) -- with
+    the data-parallel watchdog (a dead or failed peer aborts the communicator instead of hanging)."""
     from .. import _native
     from ..parallel import dist as pdist
 
-    ev = torch.cuda.Event()
-    ev.record()
+    if ev is None:
+        ev = torch.cuda.Event()
+        ev.record()
     comm = dist.native_comm
     lib = _native.lib()
 

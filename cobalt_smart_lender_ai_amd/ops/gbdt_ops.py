@@ -256,9 +256,11 @@ class GpuGbdtTrainer:
     def tree_ptr(self, t: int) -> int:
         return int(self.lib.cobalt_gbdt_tree_ptr(self.h, t))
 
-    def fetch(self, t0: int, n: int) -> np.ndarray:
+    def fetch(self, t0: int, n: int, stream: torch.cuda.Stream | None = None) -> np.ndarray:
+        """Node records of trees [t0, t0 + n) (copied on ``stream``, default the current one, and
+        synchronised with it only)."""
         out = np.zeros((n, self.max_nodes), dtype=NODE_DTYPE)
-        rc = self.lib.cobalt_gbdt_fetch_trees(self.h, t0, n, out.ctypes.data, _native.stream_handle())
+        rc = self.lib.cobalt_gbdt_fetch_trees(self.h, t0, n, out.ctypes.data, _native.stream_handle(stream))
         _native.check(rc, "cobalt_gbdt_fetch_trees")
         return out
 
