@@ -35,17 +35,30 @@ constexpr int kSkThreads = 1024;
 
 __device__ __forceinline__ float canon(float v) { return v + 0.0f; }  // -0 -> +0 (compute_cuts' rule)
 
-// number of boundaries < v (branchless over the padded power-of-two table) and whether u[k] == v
-__device__ __forceinline__ int sk_bucket(const float* __restrict__ u, int m, float v) {
+// Number of boundaries < v and whether u[k] == v. The search runs over the boundaries in Eytzinger
+// (breadth-first) order, e[i] = the BST node i of u[0..4094]: at step l a wave's lanes can only touch
+// the 2^l consecutive words [2^l - 1, 2^(l+1) - 1), distinct LDS banks -- over the sorted table the
+// candidates of steps 2-7 were 2^l words 4096 / 2^l apart, ALL in one bank (up to 32-way conflicts
+// per step: ~10x the search's conflict-free LDS time, most of k_sk_hist).
+constexpr int kSkTreeNodes = kSkMaxBounds - 1;  // 4095 = a complete BST of 12 levels
+__device__ __forceinline__ int sk_bucket(const float* __restrict__ u, const float* __restrict__ e, int m, float v) {
   int k = 0;
 #pragma unroll
-  for (int s = kSkMaxBounds / 2; s > 0; s >>= 1) k += (u[k + s - 1] < v) ? s : 0;
+  for (int l = 0; l < 12; ++l) k = 2 * k + 1 + (e[k] < v ? 1 : 0);
+  k -= kSkTreeNodes;  // the in-order rank: boundaries < v
   const bool eq = k < m && u[k] == v;
   return 2 * k + (eq ? 1 : 0);
 }
 
-__device__ __forceinline__ void sk_load_bounds(float* s_u, const float* __restrict__ bounds, int f) {
-  for (int i = threadIdx.x; i < kSkMaxBounds; i += blockDim.x) s_u[i] = bounds[(int64_t)f * kSkMaxBounds + i];
+// The feature's sorted boundaries into s_u and their Eytzinger order into s_e (BFS node i at depth d,
+// position p in its level = in-order index (2 p + 1) 2^(11 - d) - 1). Publish with a barrier.
+__device__ __forceinline__ void sk_load_bounds(float* s_u, float* s_e, const float* __restrict__ bounds, int f) {
+  const float* b = bounds + (int64_t)f * kSkMaxBounds;
+  for (int i = threadIdx.x; i < kSkMaxBounds; i += blockDim.x) s_u[i] = b[i];
+  for (int i = threadIdx.x; i < kSkTreeNodes; i += blockDim.x) {
+    const int d = 31 - __clz(i + 1), p = i + 1 - (1 << d);
+    s_e[i] = b[((2 * p + 1) << (11 - d)) - 1];
+  }
 }
 
 // Pass 1. grid = (blocks per feature, F); X feature-major [F][ldx]; w: int32 quantised weights or
@@ -59,12 +72,12 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_hist(const float* __restrict_
                                                        const int32_t* __restrict__ nbound, uint32_t* __restrict__ cnt_slab,
                                                        unsigned long long* __restrict__ w_slab, float* __restrict__ bmm,
                                                        uint16_t* __restrict__ bid) {
-  __shared__ float s_u[kSkMaxBounds];
+  __shared__ float s_u[kSkMaxBounds], s_e[kSkTreeNodes];
   __shared__ uint32_t s_c[kSkBuckets];
   __shared__ unsigned long long s_w[kW ? kSkBuckets : 1];
   __shared__ float s_mm[2][kSkThreads / kWave];
   const int f = blockIdx.y, F = gridDim.y;
-  sk_load_bounds(s_u, bounds, f);
+  sk_load_bounds(s_u, s_e, bounds, f);
   for (int i = threadIdx.x; i < kSkBuckets; i += blockDim.x) {
     s_c[i] = 0u;
     if (kW) s_w[i] = 0ull;
@@ -85,7 +98,7 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_hist(const float* __restrict_
     if (v == v) {  // NaN: the missing bin, no weight
       mn = fminf(mn, v);
       mx = fmaxf(mx, v);
-      b = sk_bucket(s_u, m, v);
+      b = sk_bucket(s_u, s_e, m, v);
       wi = kW ? (int64_t)w[r] : 1;
     }
     if (kIds && r < r1) bid[(int64_t)f * ldx + r] = b >= 0 ? (uint16_t)b : (uint16_t)0xFFFFu;
@@ -154,14 +167,14 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
                                                          const int32_t* __restrict__ slot, const int64_t* __restrict__ blk_off,
                                                          int nseg, float* __restrict__ cval, int32_t* __restrict__ cw,
                                                          const uint16_t* __restrict__ bid) {
-  __shared__ float s_u[kSkMaxBounds];
+  __shared__ float s_u[kIds ? 1 : kSkMaxBounds], s_e[kIds ? 1 : kSkTreeNodes];
   __shared__ int32_t s_slot[kSkBuckets];
   // per selected bucket: this block's rows written so far (relative to the block's int64 segment offset
   // bo[segment]: a streamed sketch accumulates offsets across chunks, past 2^32 candidates at billions of
   // rows, while one block's count always fits 32 bits)
   __shared__ uint32_t s_cur[kSkBuckets];
   const int f = blockIdx.y;
-  if (!kIds) sk_load_bounds(s_u, bounds, f);
+  if (!kIds) sk_load_bounds(s_u, s_e, bounds, f);
   const int64_t* bo = blk_off + (int64_t)blockIdx.x * nseg;
   for (int i = threadIdx.x; i < kSkBuckets; i += blockDim.x) {
     s_slot[i] = slot[(int64_t)f * kSkBuckets + i];
@@ -183,7 +196,7 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
     } else {
       v = canon(col[r]);
       if (v != v) continue;
-      b = sk_bucket(s_u, m, v);
+      b = sk_bucket(s_u, s_e, m, v);
     }
     const int sg = s_slot[b];
     if (sg < 0) continue;
