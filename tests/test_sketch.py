@@ -311,3 +311,28 @@ def test_stream_exact_cuts_equal_in_core():
     ref = gbdt.train(torch.from_numpy(Xh).cuda(), torch.from_numpy(yh).cuda(), params, device="cuda")
     got = stream.train_stream(stream.array_chunks(Xh, yh, 70_000), params, n_rows=len(Xh), device="cuda")
     assert got.save_raw("ubj") == ref.save_raw("ubj")
+
+
+def test_device_plan_layout_holds_every_array():
+    """The device sketch's plan workspace (csrc/sketch.hip sk_plan_layout, carved by models/sketch.py
+    _exact_core): one region per array in SkArr order, each large enough for its worst case -- every
+    bucket of every feature a segment, every rank of every feature an open target (host-only check)."""
+    from cobalt_smart_lender_ai_amd import _native
+
+    if not _native.available():
+        pytest.skip("native library not built")
+    lib = sketch._sk_lib()
+    NB, T = lib.cobalt_sk_buckets(), 255
+    size = {"sel": 1, "fstat": 8, "fbase": 8, "summary": 8, "q0": 4, "thr": 8, "pre": 8, "tb": 4, "need": 1,
+            "slot": 4, "seg_feat": 4, "seg_bucket": 4, "loc_sizes": 8, "glob_sizes": 8, "loc_off": 8, "glob_off": 8,
+            "tgt_off": 4, "want": 1, "ndist": 4, "tpos": 4, "tprefix": 8, "tthr": 8, "tmaxb": 8}
+    assert tuple(size) == sketch._PLAN_ARRS
+    for F in (1, 20, 106):
+        off = sketch._plan_layout(lib, F)
+        count = {"sel": F * NB, "fstat": 5 * F, "fbase": 4 * F, "summary": 8, "q0": F * T, "thr": F * T, "pre": F * T,
+                 "tb": F * T, "need": F * T, "slot": F * NB, "seg_feat": F * NB, "seg_bucket": F * NB,
+                 "loc_sizes": F * NB, "glob_sizes": F * NB, "loc_off": F * NB + 1, "glob_off": F * NB + 1,
+                 "tgt_off": F * NB + 1, "want": F * NB, "ndist": F * NB, "tpos": F * T, "tprefix": F * T,
+                 "tthr": F * T, "tmaxb": F * T}
+        for i, name in enumerate(sketch._PLAN_ARRS):
+            assert (off[i + 1] - off[i]) * 8 >= count[name] * size[name], (F, name)
