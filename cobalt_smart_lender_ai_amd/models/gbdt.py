@@ -466,9 +466,10 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     yt = _to_tensor(y, dev).reshape(-1)
     if yt.shape[0] != N:
         raise ValueError("X and y row counts differ")
-    wt = _to_tensor(sample_weight, dev).reshape(-1) if sample_weight is not None else torch.ones(N, device=dev)
     spw = float(params.scale_pos_weight if params.scale_pos_weight is not None else 1.0)
-    wt = wt * torch.where(yt == 1.0, torch.tensor(spw, device=dev), torch.tensor(1.0, device=dev))
+    # (python scalars, not device tensors: no host-to-device copies; the same float32 values)
+    pw = torch.where(yt == 1.0, spw, 1.0).to(torch.float32)
+    wt = (_to_tensor(sample_weight, dev).reshape(-1) * pw) if sample_weight is not None else pw
     wt = wt.to(torch.float32).contiguous()
 
     T0 = init_booster.num_trees if init_booster is not None else 0
@@ -478,6 +479,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
     # weight (the fixed-point scales); under data parallelism both in ONE collective: [sum w, sum w y,
     # every rank's max weight in its own slot] summed on the device
     need_bs = init_booster is None and params.base_score is None
+    labels_binary = None  # known after the one-rank read below
     if world > 1:
         buf = torch.zeros(2 + world, dtype=torch.float64, device=dev)
         if need_bs:
@@ -492,10 +494,13 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
             dist.allreduce(t, "sum")
             buf = t.to(dev)
         sw, swy, wmax = (float(v) for v in (buf[0], buf[1], buf[2:].max()))
-    else:
-        sw = float(wt.double().sum()) if need_bs else 0.0
-        swy = float((wt.double() * yt.double()).sum()) if need_bs else 0.0
-        wmax = float(wt.max()) if N else 1.0
+    else:  # one device -> host read for the three (and whether the labels are 0 / 1, for the trainer)
+        wd = wt.double()
+        z = torch.zeros((), dtype=torch.float64, device=dev)
+        sw, swy, wmax, y01 = torch.stack([wd.sum() if need_bs else z, (wd * yt.double()).sum() if need_bs else z,
+                                          wd.max() if N else z + 1.0,
+                                          ((yt == 0) | (yt == 1)).all().double()]).tolist()
+        labels_binary = y01 != 0.0
     if init_booster is not None:
         base_score = float(init_booster.base_score)
     elif params.base_score is None:
@@ -578,7 +583,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
         # follow from them (8 fewer bytes per row in every gradient pass); COBALT_LABEL_IN_RECORD=0 off
         if (sample_weight is None and knob("COBALT_LABEL_IN_RECORD", "1") != "0"
                 and bd.records.shape[1] == 32 and F <= 23
-                and bool(((yt == 0) | (yt == 1)).all())):
+                and (labels_binary if labels_binary is not None else bool(((yt == 0) | (yt == 1)).all()))):
             tr.set_binary_labels(float(np.float32(spw)))
         tp = rep.mark("trainer_setup", tp, dev)
         completed = False
