@@ -597,7 +597,7 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
                 if cr == dist.rank:
                     tr.set_fault(int(knob("COBALT_FAULT_CORRUPT_TREE", "1") or 1))
             head = None
-            if checkpoint is None and T - T0 >= 64:
+            if checkpoint is None and T - T0 >= 64 and _own_device(world):
                 # Two grow calls: the first part's trees are fetched (on a side stream) and converted on
                 # the host while the GPU grows the last ones -- the host's ~1 ms per 300 trees of
                 # fetch + conversion leaves the fit's critical path.
@@ -668,6 +668,19 @@ def train_binned(bd: BinnedData, y, params: GBDTParams | dict | None = None, *, 
 
 
 _side_streams: dict = {}
+
+
+def _own_device(world: int) -> bool:
+    """Whether this rank has its GPU to itself, so a second stream of its own is safe. Ranks that share
+    a device (the one-GPU rehearsals: torchrun with more ranks than devices, dp_check's processes) are
+    time-sliced or CU-partitioned, and their exchange kernels wait on each other inside the GPU: an
+    extra hardware queue per process measured as a 120 s exchange deadlock there
+    (tests/test_00gpu_dp_ipc.py, unmasked ranks with a CU budget)."""
+    if world <= 1:
+        return True
+    lw = os.environ.get("LOCAL_WORLD_SIZE")
+    return (lw is not None and knob("COBALT_BENCH_SHARED_DEVICE", "0") != "1"
+            and int(lw) <= torch.cuda.device_count())
 
 
 def _side_stream(dev) -> torch.cuda.Stream:

@@ -585,17 +585,6 @@ def _sk_transpose(lib, X, stream):
     return X.t().contiguous()
 
 
-_side_streams: dict = {}
-
-
-def _side_stream(dev) -> torch.cuda.Stream:
-    """A second stream of ``dev`` (created once) for sketch work that overlaps the main stream's."""
-    key = torch.device(dev).index or 0
-    if key not in _side_streams:
-        _side_streams[key] = torch.cuda.Stream(torch.device("cuda", key))
-    return _side_streams[key]
-
-
 # the device plan's arrays, in the order of csrc/sketch.hip SkArr (their int64 word offsets inside the
 # plan workspace come from cobalt_sk_plan_layout)
 _PLAN_ARRS = ("sel", "fstat", "fbase", "summary", "q0", "thr", "pre", "tb", "need", "slot", "seg_feat", "seg_bucket",
@@ -643,13 +632,10 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
     S = samp.shape[0]
     bounds = torch.empty((F, NBND), dtype=torch.float32, device=dev)
     m = torch.empty(F, dtype=torch.int32, device=dev)
-    side = None  # the boundary sort runs on a side stream (20 blocks) beside the first transpose
     if 0 < S <= lib.cobalt_sk_sample_cap():
         sp = samp if samp.dtype == torch.float32 else samp.to(torch.float32)
-        side = _side_stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
         chk(lib.cobalt_sk_sample_bounds(sp.data_ptr(), sp.stride(0), sp.stride(1), S, F, bounds.data_ptr(),
-                                        m.data_ptr(), _native.stream_handle(side)), "cobalt_sk_sample_bounds")
+                                        m.data_ptr(), stream), "cobalt_sk_sample_bounds")
         mark("sort")
     elif S:
         sv = torch.sort((samp.t() + 0.0).contiguous(), dim=1).values                 # [F, S], NaN last
@@ -683,9 +669,6 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
         Xc = Xc.to(torch.float32)
         n = Xc.shape[0]
         XT = _sk_transpose(lib, Xc, stream)
-        if side is not None:  # pass 1 needs the boundaries
-            torch.cuda.current_stream(dev).wait_stream(side)
-            side = None
         mark("transpose")
         # one chunk (the in-core sketch): pass 1 also keeps every value's bucket, so the candidate pass
         # reads 2 bytes per value instead of searching the boundaries again
@@ -696,8 +679,6 @@ def _exact_core(chunks, single, N, F, dev, samp, has_missing, max_bin, dist, wei
                                      _ptr(w_loc), vmin.data_ptr(), vmax.data_ptr(), stream), "cobalt_sk_reduce")
         if single:
             kept = (XT, n, wq, nblk, cnt_slab, bid)
-    if side is not None:  # (no chunks)
-        torch.cuda.current_stream(dev).wait_stream(side)
     cnt_h, w_h = cnt_loc, w_loc
     if world > 1:  # collective 2
         cnt_h, w_h, vmin, vmax = _allreduce_buckets(dist, dev, cnt_loc, w_loc, vmin, vmax)
