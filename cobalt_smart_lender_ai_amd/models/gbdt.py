@@ -671,16 +671,14 @@ _side_streams: dict = {}
 
 
 def _own_device(world: int) -> bool:
-    """Whether this rank has its GPU to itself, so a second stream of its own is safe. Ranks that share
-    a device (the one-GPU rehearsals: torchrun with more ranks than devices, dp_check's processes) are
-    time-sliced or CU-partitioned, and their exchange kernels wait on each other inside the GPU: an
-    extra hardware queue per process measured as a 120 s exchange deadlock there
-    (tests/test_00gpu_dp_ipc.py, unmasked ranks with a CU budget)."""
-    if world <= 1:
-        return True
-    lw = os.environ.get("LOCAL_WORLD_SIZE")
-    return (lw is not None and knob("COBALT_BENCH_SHARED_DEVICE", "0") != "1"
-            and int(lw) <= torch.cuda.device_count())
+    """Whether the fit may take a second stream of its own (the fetch overlap): one process only. Ranks
+    that share a device (the one-GPU rehearsals) are time-sliced or CU-partitioned, and their exchange
+    kernels wait on each other inside the GPU: an extra stream per process deadlocked unmasked ranks for
+    the 120 s exchange deadline (tests/test_00gpu_dp_ipc.py, a CU budget without masks) and slowed
+    CU-masked ranks 9x (2 ranks, 2M rows: 945.6 vs 102.7 ms per fit,
+    profiles/round6/ab_sketch_side_stream.txt). Data-parallel fits on separate GPUs would not share
+    queues, but that configuration cannot be rehearsed on one GPU, so they keep one stream too."""
+    return world <= 1
 
 
 def _side_stream(dev) -> torch.cuda.Stream:
