@@ -207,8 +207,9 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_gather(const float* __restric
 }
 
 // Row-major X [n][F] -> feature-major XT [F][n] (F <= 32): a tile of 256 rows is read as one
-// contiguous run into LDS (rows padded to F + 1 words: conflict-free column reads), then written as
-// F runs of 256 values.
+// contiguous run into LDS (rows padded to F + 1 words), then written as F runs of 256 values. 16-byte
+// loads when the tile starts 16-byte aligned, 16-byte stores (4 rows of one feature) for whole tiles
+// when n % 4 == 0; scalar otherwise.
 constexpr int kTrRows = 256;
 __global__ __launch_bounds__(256) void k_sk_transpose(const float* __restrict__ X, int64_t n, int F,
                                                       float* __restrict__ XT) {
@@ -216,14 +217,43 @@ __global__ __launch_bounds__(256) void k_sk_transpose(const float* __restrict__ 
   const int64_t r0 = (int64_t)blockIdx.x * kTrRows;
   const int rows = (int)min((int64_t)kTrRows, n - r0);
   const float* src = X + r0 * F;
-  for (int j = threadIdx.x; j < rows * F; j += blockDim.x) {
+  const int tot = rows * F, P = F + 1;
+  int j0 = 0;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    const int t4 = tot >> 2;
+    for (int j = threadIdx.x; j < t4; j += blockDim.x) {
+      const float4 v = reinterpret_cast<const float4*>(src)[j];
+      int i = (4 * j) / F, f = 4 * j - i * F;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        s_t[i * P + f] = vv[c];
+        if (++f == F) { f = 0; ++i; }
+      }
+    }
+    j0 = 4 * t4;
+  }
+  for (int j = j0 + threadIdx.x; j < tot; j += blockDim.x) {
     const int i = j / F, f = j - i * F;
-    s_t[i * (F + 1) + f] = src[j];
+    s_t[i * P + f] = src[j];
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < kTrRows * F; j += blockDim.x) {
-    const int f = j / kTrRows, i = j - f * kTrRows;
-    if (i < rows) XT[(int64_t)f * n + r0 + i] = s_t[i * (F + 1) + f];
+  if ((n & 3) == 0 && rows == kTrRows) {
+    constexpr int Q = kTrRows / 4;
+    for (int j = threadIdx.x; j < F * Q; j += blockDim.x) {
+      const int f = j / Q, q = j - f * Q;
+      float4 v;
+      v.x = s_t[(4 * q) * P + f];
+      v.y = s_t[(4 * q + 1) * P + f];
+      v.z = s_t[(4 * q + 2) * P + f];
+      v.w = s_t[(4 * q + 3) * P + f];
+      reinterpret_cast<float4*>(XT + (int64_t)f * n + r0)[q] = v;
+    }
+  } else {
+    for (int j = threadIdx.x; j < kTrRows * F; j += blockDim.x) {
+      const int f = j / kTrRows, i = j - f * kTrRows;
+      if (i < rows) XT[(int64_t)f * n + r0 + i] = s_t[i * P + f];
+    }
   }
 }
 
