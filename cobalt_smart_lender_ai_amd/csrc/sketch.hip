@@ -392,6 +392,65 @@ __global__ __launch_bounds__(kSkThreads) void k_sk_select(const float* __restric
   if (threadIdx.x == 0) ndist[s] = (int32_t)cum[len - 1];
 }
 
+// Pass 3 with unit weights: the cumulative weight of sorted position i is i + 1, so the weight scan
+// goes and target t is the closed form i = clamp(thr / maxb - prefix, 0, len - 1) -- the first i with
+// (prefix + i + 1) * maxb > thr (integers, maxb > 0). Keys only in LDS (32 KB, + 32 KB of int32 flags
+// for the distinct values): two blocks per CU where the weighted form holds one.
+__global__ __launch_bounds__(kSkThreads) void k_sk_select_u(const float* __restrict__ cval, const int64_t* __restrict__ seg_off,
+                                                           const int32_t* __restrict__ tgt_off,
+                                                           const int64_t* __restrict__ prefix, const int64_t* __restrict__ thr,
+                                                           const int64_t* __restrict__ maxb, float* __restrict__ out,
+                                                           const uint8_t* __restrict__ want, float* __restrict__ dval,
+                                                           int32_t* __restrict__ ndist) {
+  extern __shared__ uint32_t s_dyn[];
+  const int s = blockIdx.x;
+  const int64_t o0 = seg_off[s], o1 = seg_off[s + 1];
+  const int len = (int)(o1 - o0);
+  const int t0 = tgt_off[s], t1 = tgt_off[s + 1];
+  const bool wd = want != nullptr && want[s];
+  if (len <= 0 || len > kSkSortCap || (t0 >= t1 && !wd)) return;
+  int P = 1;
+  while (P < len) P <<= 1;
+  uint32_t* key = s_dyn;                 // [P]
+  int32_t* cnt = reinterpret_cast<int32_t*>(s_dyn + kSkSortCap);  // [P] distinct flags, then their scan
+  for (int i = threadIdx.x; i < P; i += blockDim.x) key[i] = i < len ? fkey(cval[o0 + i]) : 0xFFFFFFFFu;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const int ix = i ^ j;
+        if (ix > i) {
+          const uint32_t a = key[i], b = key[ix];
+          if ((a > b) == ((i & k) == 0)) {
+            key[i] = b;
+            key[ix] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
+    const int64_t i = thr[t] / maxb[t] - prefix[t];
+    out[t] = fval(key[min(max(i, (int64_t)0), (int64_t)len - 1)]);
+  }
+  if (!wd) return;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[i] = (i < len && (i == 0 || key[i] != key[i - 1])) ? 1 : 0;
+  __syncthreads();
+  for (int d = 1; d < P; d <<= 1) {
+    int32_t add[kSkSortCap / kSkThreads];
+    int c = 0;
+    for (int i = threadIdx.x; i < P; i += blockDim.x, ++c) add[c] = i >= d ? cnt[i - d] : 0;
+    __syncthreads();
+    c = 0;
+    for (int i = threadIdx.x; i < P; i += blockDim.x, ++c) cnt[i] += add[c];
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < len; i += blockDim.x)
+    if (i == 0 || key[i] != key[i - 1]) dval[o0 + cnt[i] - 1] = fval(key[i]);
+  if (threadIdx.x == 0) ndist[s] = cnt[len - 1];
+}
+
 // Exact-bin features (one bin per distinct value when a feature has <= maxb of them), one block per
 // feature: the distinct values in bucket order are the sample values whose equal bucket has rows and,
 // for a feature with rows in open buckets (every such bucket is a selected segment then), the
@@ -1055,18 +1114,19 @@ COBALT_API int cobalt_sk_select(const float* cval, const int32_t* cw, const int6
                                 float* out, const uint8_t* want, float* dval, int32_t* ndist, hipStream_t stream) {
   if (nseg <= 0) return 0;
   const size_t lds = (size_t)kSkSortCap * (sizeof(uint32_t) + sizeof(int64_t));
+  const size_t lds_u = (size_t)kSkSortCap * (sizeof(uint32_t) + sizeof(int32_t));
   static bool attr = false;
   if (!attr) {
     CK(hipFuncSetAttribute((const void*)k_sk_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    CK(hipFuncSetAttribute((const void*)k_sk_select<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFuncSetAttribute((const void*)k_sk_select_u, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_u));
     attr = true;
   }
   if (cw)
     hipLaunchKernelGGL(k_sk_select<true>, dim3(nseg), dim3(kSkThreads), lds, stream, cval, cw, seg_off, tgt_off, prefix,
                        thr, maxb, out, want, dval, ndist);
   else
-    hipLaunchKernelGGL(k_sk_select<false>, dim3(nseg), dim3(kSkThreads), lds, stream, cval, cw, seg_off, tgt_off,
-                       prefix, thr, maxb, out, want, dval, ndist);
+    hipLaunchKernelGGL(k_sk_select_u, dim3(nseg), dim3(kSkThreads), lds_u, stream, cval, seg_off, tgt_off, prefix, thr,
+                       maxb, out, want, dval, ndist);
   CK_LAUNCH();
   return 0;
 }
